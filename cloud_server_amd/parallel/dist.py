@@ -1,0 +1,85 @@
+"""Process-group bootstrap: one process per GPU, ``torch.distributed`` over RCCL/xGMI.
+
+Replaces the reference's TF ``ClusterSpec``/``tf.train.Server`` gRPC cluster
+(construct_distribute.py:344-349) and the ``--ps_hosts/--worker_hosts/--job_name/
+--task_index`` flags (:37-43).  Ranks come from the standard env:// variables that
+``torch.distributed.run`` (or our own launcher, ``parallel.launch``) sets:
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT.
+
+On ROCm the ``nccl`` backend IS RCCL; CPU tests use ``gloo`` with the same code.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rank == 0   # reference: is_chief = task_index == 0 (:385)
+
+
+def env_world() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init_distributed(device_type: str = "auto", timeout_s: float = 300.0) -> DistContext:
+    """Initialise from env. ``device_type``: 'cuda' (RCCL), 'cpu' (gloo) or 'auto'."""
+    world = env_world()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type == "auto":
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+        backend = "nccl"
+    else:
+        device = torch.device("cpu")
+        backend = "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=backend, rank=rank, world_size=world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
+
+
+def barrier(ctx: DistContext) -> None:
+    if ctx.enabled:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.local_rank])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(ctx: DistContext, value: float) -> float:
+    if not ctx.enabled:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown(ctx: DistContext) -> None:
+    if ctx.enabled and dist.is_initialized():
+        dist.destroy_process_group()

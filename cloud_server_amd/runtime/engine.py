@@ -1,0 +1,205 @@
+"""Training engine: one step = gather batch -> fwd -> bwd -> grad sync -> optimizer.
+
+Replaces the reference worker loop (construct_distribute.py:385-421), where every
+``sess.run(train_op)`` pulled all variables from the PS over gRPC, ran fwd/bwd on one
+CPU and pushed gradients back (≈142 ms per B=50 step, API.md:462-507).
+
+MI355X design:
+* the dataset is resident in HBM and batches are gathered on device (``BatchStream``),
+* the whole step — gather, forward, backward, gradient all-reduce, optimizer and the
+  accuracy/loss bookkeeping — is captured ONCE into a HIP graph and replayed, so a step
+  costs one ``hipGraphLaunch`` and zero host syncs,
+* two step programs share that contract:
+  - ``TorchProgram``: autograd over eager PyTorch ops (CPU path, reference numerics),
+  - ``HipProgram`` (``runtime.hip_program``): the hand-written CDNA4 kernels
+    (``ops.fused``) with an explicit backward and the fused optimizer,
+* metrics (per-step correct count and loss) go to a device ring buffer that the host
+  reads only every ``log_every`` steps (the reference logs every 100, :405).
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, Optional
+
+import torch
+
+from ..data.datasets import ArrayDataset
+from ..data.stream import BatchStream, DeviceDataset
+from ..models.cnn import DigitNet, build_model, loss_fn
+from ..models.dsl import TrainConfig
+from ..ops import optim_ref
+from ..parallel.dist import DistContext
+from ..parallel.dp import GradSync
+
+RING = 4096
+
+
+class StepProgram:
+    """Interface: ``run()`` performs one full training step on device (capturable)."""
+
+    def run(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class TorchProgram(StepProgram):
+    def __init__(self, eng: "TrainEngine"):
+        self.e = eng
+
+    def run(self) -> None:
+        e = self.e
+        idx = e.stream.current()
+        x, y = e.data.batch(idx)
+        logits = e.model(x)
+        loss = loss_fn(e.cfg.loss_name, logits, y)
+        e.flat_grad.zero_()
+        (loss * e.sync.grad_scale).backward()
+        with torch.no_grad():
+            e.apply_update()
+            correct = (logits.argmax(1) == y).sum().to(torch.int32)
+            e.record(correct, loss.detach())
+
+
+class TrainEngine:
+    def __init__(self, cfg: TrainConfig, train: ArrayDataset, device="cpu",
+                 ctx: Optional[DistContext] = None, backend: str = "auto",
+                 use_graph: Optional[bool] = None, strategy: str = "allreduce",
+                 stream_chunk: int = 512):
+        self.cfg = cfg
+        self.ctx = ctx or DistContext(device=torch.device(device))
+        self.device = torch.device(device)
+        self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world)
+        self.model.train()
+        self.flat = self.model.flat.data
+        self.flat_grad = torch.zeros_like(self.flat)
+        self.model.flat.grad = self.flat_grad
+        self.sync = GradSync(self.ctx, self.flat.numel(), strategy)
+        self.sync.broadcast_params(self.flat)
+        self.opt_id = optim_ref.OPT_IDS[cfg.effective_optimizer]
+        self.lr = cfg.effective_lr
+        lo, hi = self.sync.shard_range()
+        self.slots = optim_ref.init_slots(self.opt_id, hi - lo, self.device)
+        self.grad_shard = torch.zeros(hi - lo, device=self.device) if strategy == "ps" else None
+        self.data = DeviceDataset(train, self.device)
+        self.stream = BatchStream(self.data.n, cfg.batch_size, self.device, seed=cfg.seed,
+                                  chunk=stream_chunk, rank=self.ctx.rank, world=self.ctx.world)
+        # device-side counters / metric rings (read by host every log interval)
+        self.dstep = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.ring_correct = torch.zeros(RING, dtype=torch.int32, device=self.device)
+        self.ring_loss = torch.zeros(RING, dtype=torch.float32, device=self.device)
+        self.host_step = 0
+        if backend == "auto":
+            backend = "hip" if self.device.type == "cuda" else "torch"
+        self.backend = backend
+        if backend == "hip":
+            from .hip_program import HipProgram
+            self.program: StepProgram = HipProgram(self)
+        else:
+            self.program = TorchProgram(self)
+        if use_graph is None:
+            use_graph = self.device.type == "cuda"
+        self.use_graph = use_graph and self.device.type == "cuda"
+        self.graph = None
+
+    # ---------------- pieces used by the programs (device ops only) ----------------
+    def adam_lr_tensor(self) -> torch.Tensor:
+        t = (self.dstep + 1).to(torch.float32)
+        return self.lr * torch.sqrt(1 - optim_ref.ADAM_B2 ** t) / (1 - optim_ref.ADAM_B1 ** t)
+
+    def apply_update(self) -> None:
+        """Grad sync + optimizer on the flat buffers (torch ops; the HIP program fuses this)."""
+        if self.sync.strategy == "ps" and self.ctx.enabled:
+            lo, hi = self.sync.shard_range()
+            self.sync.reduce_scatter(self.flat_grad, self.grad_shard)
+            self._opt(self.flat[lo:hi], self.grad_shard, self.slots)
+            self.sync.all_gather_params(self.flat)
+        else:
+            self.sync.allreduce(self.flat_grad)
+            self._opt(self.flat, self.flat_grad, self.slots)
+
+    def _opt(self, w, g, slots) -> None:
+        if self.opt_id == optim_ref.OPT_ADAM:
+            m, v = slots[0], slots[1]
+            m.mul_(optim_ref.ADAM_B1).add_(g, alpha=1 - optim_ref.ADAM_B1)
+            v.mul_(optim_ref.ADAM_B2).addcmul_(g, g, value=1 - optim_ref.ADAM_B2)
+            w.sub_(self.adam_lr_tensor() * m / (v.sqrt() + optim_ref.ADAM_EPS))
+        else:
+            optim_ref.step_ref(self.opt_id, w, g, slots, self.lr, 1)
+
+    def record(self, correct: torch.Tensor, loss: torch.Tensor) -> None:
+        pos = torch.remainder(self.dstep, RING)
+        self.ring_correct.index_copy_(0, pos, correct.view(1).to(torch.int32))
+        self.ring_loss.index_copy_(0, pos, loss.view(1).to(torch.float32))
+        self.dstep.add_(1)
+
+    # ---------------- host API ----------------
+    def _capture(self) -> None:
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        saved = (self.flat.clone(), self.slots.clone(), self.dstep.clone(),
+                 self.stream.cursor.clone())
+        with torch.cuda.stream(s):
+            for _ in range(2):      # warm up allocator / autotuning / RCCL comms off-graph
+                self.program.run()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        # undo the warm-up's effect on the model state
+        self.flat.copy_(saved[0]); self.slots.copy_(saved[1])
+        self.dstep.copy_(saved[2]); self.stream.cursor.copy_(saved[3])
+        self.program.reset_after_warmup() if hasattr(self.program, "reset_after_warmup") else None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.program.run()
+        self.graph = g
+        # capture does not execute: the cursor/step still point at this step
+
+    def step(self) -> None:
+        self.stream.before_step()
+        if self.use_graph:
+            if self.graph is None:
+                self._capture()
+            self.graph.replay()
+        else:
+            self.program.run()
+        self.host_step += 1
+
+    def sync_device(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def metrics_since(self, start_step: int) -> Dict[str, float]:
+        """Mean accuracy/loss of steps [start_step, host_step) (host sync happens here)."""
+        n = self.host_step - start_step
+        if n <= 0:
+            return {"accuracy": float("nan"), "loss": float("nan"), "steps": 0}
+        n = min(n, RING)
+        pos = [(self.host_step - 1 - i) % RING for i in range(n)]
+        idx = torch.tensor(pos, device=self.device)
+        c = self.ring_correct.index_select(0, idx).double().sum().item()
+        l = self.ring_loss.index_select(0, idx).double().mean().item()
+        return {"accuracy": c / (n * self.cfg.batch_size), "loss": l, "steps": n}
+
+    def last_batch_accuracy(self) -> float:
+        pos = (self.host_step - 1) % RING
+        return float(self.ring_correct[pos].item()) / self.cfg.batch_size
+
+    @torch.no_grad()
+    def evaluate(self, ds: ArrayDataset, batch: int = 4096) -> float:
+        """Test accuracy with eval-mode BN (running stats unless bn_mode == 'batch')."""
+        if len(ds) == 0:
+            return float("nan")
+        self.model.eval()
+        correct = 0
+        imgs = torch.from_numpy(ds.images).to(self.device)
+        labs = torch.from_numpy(ds.labels).to(self.device)
+        for i in range(0, len(ds), batch):
+            x = imgs[i:i + batch].float().div_(255.0)
+            pred = self.predict_logits(x).argmax(1)
+            correct += int((pred == labs[i:i + batch]).sum().item())
+        self.model.train()
+        return correct / len(ds)
+
+    def predict_logits(self, x: torch.Tensor) -> torch.Tensor:
+        if self.backend == "hip" and hasattr(self.program, "predict_logits"):
+            return self.program.predict_logits(x)
+        return self.model(x)
