@@ -1,0 +1,128 @@
+// Shared device helpers for the cloud_server_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * activations are NHWC fp32, conv weights HWIO, dense weights [in, out] row-major
+//    (the reference's TF layouts, construct_distribute.py:91-118, 168-182);
+//  * wave = 64 lanes; block sizes are multiples of 64;
+//  * a launcher never allocates, copies or synchronises (everything is HIP-graph
+//    capturable); scratch comes from a caller-owned workspace;
+//  * every launcher returns hipGetLastError() as an int (0 == ok).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CSA_API extern "C" __attribute__((visibility("default")))
+
+namespace csa {
+
+enum Act : int { ACT_NONE = 0, ACT_SIGMOID = 1, ACT_RELU = 2, ACT_LEAKY = 3 };
+
+__device__ __forceinline__ float act_fwd(float x, int act, float alpha) {
+  switch (act) {
+    case ACT_SIGMOID: return 1.0f / (1.0f + __expf(-x));
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_LEAKY: return fmaxf(x, alpha * x);  // tf.maximum(x, a*x)
+    default: return x;
+  }
+}
+
+// derivative expressed through the pre-activation x and the output y
+__device__ __forceinline__ float act_bwd(float g, float x, float y, int act, float alpha) {
+  switch (act) {
+    case ACT_SIGMOID: return g * y * (1.0f - y);
+    case ACT_RELU: return x > 0.f ? g : 0.f;
+    case ACT_LEAKY: return (x >= alpha * x) ? g : g * alpha;
+    default: return g;
+  }
+}
+
+// Division by a runtime constant through a float reciprocal (exact for 0 <= x < 2^22
+// after a +-1 fix-up): ~6 VALU ops instead of the ~40-op integer division sequence.
+struct FastDiv {
+  int d; float inv;
+  __host__ __device__ FastDiv() : d(1), inv(1.f) {}
+  __host__ __device__ explicit FastDiv(int dd) : d(dd < 1 ? 1 : dd), inv(1.0f / (float)(dd < 1 ? 1 : dd)) {}
+  __device__ __forceinline__ int div(int x) const {
+    int q = __float2int_rz((float)x * inv);
+    if ((q + 1) * d <= x) ++q;
+    if (q * d > x) --q;
+    return q;
+  }
+  __device__ __forceinline__ void divmod(int x, int& q, int& r) const {
+    q = div(x);
+    r = x - q * d;
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------
+// BatchNorm statistics travel between kernels as per-workgroup partial slabs
+// [nslab][2][C] = {sum x, sum x^2} (forward) or {sum dz, sum dz*xhat} (backward).
+// A consumer reduces the slab itself at kernel start (a few KB, L2-resident), which
+// removes the separate "finalize" launch a textbook BN needs.
+// ---------------------------------------------------------------------------------
+struct BNRef {
+  const float* slab;    // [nslab][2][C] forward partial sums
+  int nslab;
+  int C;
+  float count;          // elements per channel (B*H*W)
+  float eps;
+  const float* scale;   // [C]
+  const float* offset;  // [C]
+};
+
+// Sum a partial slab [nslab][2C] over its rows into s_out[2C], using the whole block.
+// Each thread owns one fixed column (t % 2C) so it sums locally and issues ONE LDS atomic
+// (a serial per-channel loop over the rows was latency-bound: ~60 µs per launch).
+// Must be called by every thread of the block; ends with a barrier.
+__device__ __forceinline__ void slab_sum_to_lds(const float* slab, int nslab, int C2, float* s_out) {
+  for (int i = threadIdx.x; i < C2; i += blockDim.x) s_out[i] = 0.f;
+  __syncthreads();
+  const int per = (int)blockDim.x / C2;          // threads per column
+  if (per > 0) {
+    const int col = threadIdx.x % C2, lane_row = threadIdx.x / C2;
+    if (lane_row < per) {
+      float acc = 0.f;
+#pragma unroll 4
+      for (int r = lane_row; r < nslab; r += per) acc += slab[(size_t)r * C2 + col];
+      atomicAdd(&s_out[col], acc);
+    }
+  } else {
+    for (int col = threadIdx.x; col < C2; col += blockDim.x) {
+      float acc = 0.f;
+      for (int r = 0; r < nslab; ++r) acc += slab[(size_t)r * C2 + col];
+      s_out[col] = acc;
+    }
+  }
+  __syncthreads();
+}
+
+// Reduce the forward slab into LDS tables with y = x * s_a[c] + s_b[c]
+// (a = scale*rstd, b = offset - mean*a).  s_tmp needs 2C floats.  Every thread must call.
+__device__ __forceinline__ void bn_reduce_to_lds(const BNRef& bn, float* s_mean, float* s_rstd,
+                                                 float* s_a, float* s_b, float* s_tmp) {
+  slab_sum_to_lds(bn.slab, bn.nslab, 2 * bn.C, s_tmp);
+  for (int c = threadIdx.x; c < bn.C; c += blockDim.x) {
+    float mean = s_tmp[c] / bn.count;
+    float var = fmaxf(s_tmp[bn.C + c] / bn.count - mean * mean, 0.f);
+    float rstd = rsqrtf(var + bn.eps);
+    float a = bn.scale[c] * rstd;
+    s_mean[c] = mean;
+    s_rstd[c] = rstd;
+    s_a[c] = a;
+    s_b[c] = bn.offset[c] - mean * a;
+  }
+}
+
+}  // namespace csa

@@ -1,0 +1,470 @@
+// Direct NHWC convolution kernels for the DSL's small convs (gfx950 / CDNA4).
+//
+// Reference ops: tf.nn.conv2d (construct_distribute.py:91-118) with TF 'SAME'/'VALID'
+// padding, tf.nn.max_pool (:121-130), activation (:133-152) and BatchNorm (:155-165).
+// The reference's convs are tiny (2x2 kernels, 1->10->20 channels): VALU work, not MFMA
+// work.  Layout of the forward / input-gradient kernels:
+//   * one workgroup per (image, row band, channel block): the band's input rows are
+//     staged ONCE into LDS with coalesced loads — with the input transform (uint8
+//     gather + /255, or BN-apply + activation) applied during staging, so it costs one
+//     evaluation per element instead of one per use;
+//   * one lane per output pixel with a register block of output channels; the weight
+//     addresses are wave-uniform (channel block from blockIdx.y), so they become scalar
+//     loads and the inner loop is v_fma_f32 with an SGPR operand;
+//   * fused epilogues: bias, activation, max-pool (argmax kept as uint8 for backward)
+//     and the BatchNorm partial statistics of the output (per-workgroup slab).
+// Weight gradients are an implicit GEMM on MFMA (gemm.hip, csa_conv_wgrad).
+#include "common.h"
+#include <algorithm>
+
+namespace csa {
+
+constexpr int CONV_THREADS = 256;
+
+struct ConvGeom {
+  int B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout;
+};
+
+struct PoolGeom {
+  int on;                      // pool fused after conv (+act)
+  int KH, KW, SH, SW, PT, PL, OH, OW;
+};
+
+struct ConvFwdArgs {
+  ConvGeom g;
+  PoolGeom pool;
+  int nbands, band_rows;       // output rows (pooled rows if pool) per band
+  int band_rows_in;            // max staged input rows per band (LDS carve)
+  int nslab;                   // BN slab rows (workgroups fold into blockIdx % nslab)
+  const float* x;              // fp32 NHWC input (or null)
+  const uint8_t* img;          // uint8 dataset [N][H*W*Cin] (first layer) ...
+  const int64_t* idx;          // ... gathered through idx[b]
+  BNRef in_bn; int in_bn_on; int in_act; float in_alpha;   // input transform
+  const float* w; const float* bias; int out_act; float out_alpha;
+  float* y;                    // [B, OH|POH, OW|POW, Cout] post-act (post-pool) output
+  uint8_t* argmax;             // [B, POH, POW, Cout] window index (pool only)
+  float* stat_slab;            // [B*nbands][2][Cout] partial {sum y, sum y^2} or null
+};
+
+template <int CB, bool U8>
+__global__ __launch_bounds__(CONV_THREADS) void conv_fwd_kernel(ConvFwdArgs a) {
+  // dynamic LDS: [input rows of the band][W][Cin] then weights [(i,j,ci)][Cout]
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  __shared__ float s_stat[2 * 128];
+  const ConvGeom& g = a.g;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x % a.nbands;
+  const int G = (g.Cout + CB - 1) / CB;            // channel groups (one per lane of a pixel)
+  const int OHo = a.pool.on ? a.pool.OH : g.OH;
+  const int OWo = a.pool.on ? a.pool.OW : g.OW;
+  const int r0 = band * a.band_rows, r1 = min(OHo, r0 + a.band_rows);
+  int c0 = r0, c1 = r1;                             // conv-output rows of the band
+  if (a.pool.on) {
+    c0 = max(0, r0 * a.pool.SH - a.pool.PT);
+    c1 = min(g.OH, (r1 - 1) * a.pool.SH - a.pool.PT + a.pool.KH);
+  }
+  const int y0 = max(0, c0 * g.SH - g.PT);
+  const int y1 = min(g.H, (c1 - 1) * g.SH - g.PT + g.KH);
+  const int rowlen = g.W * g.Cin;
+  const int nin = max(0, y1 - y0) * rowlen;
+  const int nw = g.KH * g.KW * g.Cin * g.Cout;
+  float* s_in = smem;
+  float* s_w = smem + ((a.band_rows_in * rowlen + 3) & ~3);
+
+  if (a.in_bn_on) bn_reduce_to_lds(a.in_bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
+  for (int i = threadIdx.x; i < 2 * g.Cout; i += blockDim.x) s_stat[i] = 0.f;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) s_w[i] = a.w[i];
+  if (U8) {
+    const uint8_t* src = a.img + a.idx[b] * (long)(g.H * rowlen) + (long)y0 * rowlen;
+    for (int i = threadIdx.x; i < nin; i += blockDim.x) s_in[i] = (float)src[i] * (1.0f / 255.0f);
+  } else {
+    __syncthreads();   // BN tables ready
+    const float* src = a.x + ((long)b * g.H + y0) * rowlen;
+    const float* ta = s_bn + 256;
+    const float* tb = s_bn + 384;
+    for (int i = threadIdx.x; i < nin; i += blockDim.x) {
+      float v = src[i];
+      if (a.in_bn_on) { const int ci = i % g.Cin; v = v * ta[ci] + tb[ci]; }
+      s_in[i] = act_fwd(v, a.in_act, a.in_alpha);
+    }
+  }
+  __syncthreads();
+
+  const int npix = (r1 - r0) * OWo;
+  const int npos = a.pool.on ? a.pool.KH * a.pool.KW : 1;
+  const int cg = threadIdx.x % G;
+  const int co0 = cg * CB;
+  const int nco = min(CB, g.Cout - co0);
+  float bsum[CB], bsq[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) { bsum[c] = 0.f; bsq[c] = 0.f; }
+  const int ppp = blockDim.x / G;                   // pixels per pass
+  for (int q = threadIdx.x / G; q < npix && threadIdx.x < ppp * G; q += ppp) {
+    const int oy = r0 + q / OWo, ox = q % OWo;
+    float out[CB];
+    int amax[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) { out[c] = -INFINITY; amax[c] = 0; }
+    for (int pos = 0; pos < npos; ++pos) {
+      int cy = oy, cx = ox;
+      if (a.pool.on) {
+        cy = oy * a.pool.SH - a.pool.PT + pos / a.pool.KW;
+        cx = ox * a.pool.SW - a.pool.PL + pos % a.pool.KW;
+        if (cy < 0 || cy >= g.OH || cx < 0 || cx >= g.OW) continue;   // -inf padding
+      }
+      float acc[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) acc[c] = (a.bias && c < nco) ? a.bias[co0 + c] : 0.f;
+      for (int i = 0; i < g.KH; ++i) {
+        const int yy = cy * g.SH - g.PT + i;
+        if (yy < 0 || yy >= g.H) continue;
+        for (int j = 0; j < g.KW; ++j) {
+          const int xx = cx * g.SW - g.PL + j;
+          if (xx < 0 || xx >= g.W) continue;
+          const float* in = s_in + (yy - y0) * rowlen + xx * g.Cin;
+          const float* wr = s_w + (i * g.KW + j) * g.Cin * g.Cout + co0;
+          for (int ci = 0; ci < g.Cin; ++ci) {
+            const float v = in[ci];
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+              if (c < nco) acc[c] = fmaf(v, wr[ci * g.Cout + c], acc[c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        const float v = act_fwd(acc[c], a.out_act, a.out_alpha);
+        if (v > out[c]) { out[c] = v; amax[c] = pos; }
+      }
+    }
+    const long p = ((long)b * OHo + oy) * OWo + ox;
+    float* yrow = a.y + p * g.Cout + co0;
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+      if (c < nco) { yrow[c] = out[c]; bsum[c] += out[c]; bsq[c] += out[c] * out[c]; }
+    if (a.pool.on && a.argmax) {
+      uint8_t* arow = a.argmax + p * g.Cout + co0;
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+        if (c < nco) arow[c] = (uint8_t)amax[c];
+    }
+  }
+  if (a.stat_slab) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+      if (c < nco) { atomicAdd(&s_stat[co0 + c], bsum[c]); atomicAdd(&s_stat[g.Cout + co0 + c], bsq[c]); }
+    __syncthreads();
+    // fold into one of a.nslab rows (atomics, zeroed each step by the optimizer launch)
+    float* row = a.stat_slab + (size_t)(blockIdx.x % a.nslab) * 2 * g.Cout;
+    for (int i = threadIdx.x; i < 2 * g.Cout; i += blockDim.x) atomicAdd(&row[i], s_stat[i]);
+  }
+}
+
+// -----------------------------------------------------------------------------------
+// Backward of a conv unit's OUTPUT side: BatchNorm backward (if the unit output fed a
+// norm), activation backward and max-pool routing.  One lane per unit-output element.
+//   dz   : grad wrt the BN output (or wrt the unit output if no BN)       [B,h,w,C]
+//   y    : unit output (post act, post pool) = BN input                  [B,h,w,C]
+//   dc   : grad wrt the conv pre-activation output                        [B,OH,OW,C]
+// BN backward: dx = a*(dz - S1/N - xhat*S2/N), a = scale*rstd, S1 = sum dz, S2 = sum dz*xhat.
+// Block 0 also writes dscale = S2, doffset = S1 into the gradient buffer.
+// -----------------------------------------------------------------------------------
+struct RouteArgs {
+  const float* dz; const float* y; const uint8_t* argmax; float* dc;
+  int B, h, w, C;             // unit-output geometry
+  int OH, OW;                 // conv output geometry (pre-pool)
+  int pool_on, PKW, PSH, PSW, PPT, PPL, overlap;
+  int out_act; float out_alpha;
+  BNRef bn; int bn_on; const float* bwd_slab; int bwd_nslab;
+  float* dscale; float* doffset;
+  float* run_mean; float* run_var; float momentum;   // BN running statistics (block 0)
+};
+
+__global__ __launch_bounds__(256) void route_bwd_kernel(RouteArgs a) {
+  __shared__ float s_bn[4 * 128];
+  __shared__ float s_s[2 * 128];
+  if (a.bn_on) {
+    bn_reduce_to_lds(a.bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_s);
+    __syncthreads();
+    slab_sum_to_lds(a.bwd_slab, a.bwd_nslab, 2 * a.C, s_s);
+    if (blockIdx.x == 0)
+      for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+        a.doffset[c] = s_s[c];
+        a.dscale[c] = s_s[a.C + c];
+        if (a.run_mean) {   // running stats from this step's batch statistics
+          const float mean = s_bn[c];
+          const float var = 1.0f / (s_bn[128 + c] * s_bn[128 + c]) - a.bn.eps;
+          a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
+          a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var;
+        }
+      }
+  }
+  __syncthreads();
+  const long n = (long)a.B * a.h * a.w * a.C;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int c = (int)(e % a.C);
+  float g = a.dz[e];
+  const float yv = a.y[e];
+  if (a.bn_on) {
+    const float inv_n = 1.0f / a.bn.count;
+    const float xhat = (yv - s_bn[c]) * s_bn[128 + c];
+    g = s_bn[256 + c] * (g - s_s[c] * inv_n - xhat * s_s[a.C + c] * inv_n);
+  }
+  // activation backward (y is the post-activation value; pooling keeps the max's value)
+  g = act_bwd(g, yv, yv, a.out_act, a.out_alpha);
+  if (!a.pool_on) { a.dc[e] = g; return; }
+  const long pix = e / a.C;
+  const int px = (int)(pix % a.w), py = (int)((pix / a.w) % a.h), b = (int)(pix / ((long)a.w * a.h));
+  const int am = a.argmax[e];
+  // non-overlapping windows (kernel == stride): this lane owns its whole window and
+  // writes it with plain stores (zeros included); otherwise atomics into a zeroed dc.
+  const int ky = am / a.PKW, kx = am % a.PKW;
+  const int cy = py * a.PSH - a.PPT + ky, cx = px * a.PSW - a.PPL + kx;
+  if (a.overlap) {
+    atomicAdd(&a.dc[(((long)b * a.OH + cy) * a.OW + cx) * a.C + c], g);
+  } else {
+    for (int wy = 0; wy < a.PSH; ++wy)
+      for (int wx = 0; wx < a.PSW; ++wx) {
+        const int yy = py * a.PSH - a.PPT + wy, xx = px * a.PSW - a.PPL + wx;
+        if (yy < 0 || yy >= a.OH || xx < 0 || xx >= a.OW) continue;
+        a.dc[(((long)b * a.OH + yy) * a.OW + xx) * a.C + c] = (yy == cy && xx == cx) ? g : 0.f;
+      }
+  }
+}
+
+// -----------------------------------------------------------------------------------
+// Conv input gradient:  dx[b,y,x,ci] = sum_{i,j,co} dc[b,oy,ox,co] * W[i,j,ci,co]
+// (one workgroup per image x row band x input-channel block, dc rows staged in LDS),
+// then through the input transform of the forward (act, BN) like the dense dgrad
+// epilogue: stores dz and emits the BN-backward slab {sum dz, sum dz*xhat}.
+// -----------------------------------------------------------------------------------
+struct ConvDgradArgs {
+  ConvGeom g;
+  int nbands, band_rows;       // input rows per band
+  int band_rows_in;            // max staged dc rows per band
+  int nslab;
+  const float* dc; const float* w; float* dx;
+  const float* x_fwd; int in_act; float in_alpha; BNRef in_bn; int in_bn_on;
+  float* bwd_slab;   // [B*nbands][2][Cin]
+};
+
+template <int CB>
+__global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs a) {
+  // dynamic LDS: dc rows of the band [rows][OW][Cout] then weights [(i,j,ci)][Cout]
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  __shared__ float s_stat[2 * 128];
+  const ConvGeom& g = a.g;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x % a.nbands;
+  const int G = (g.Cin + CB - 1) / CB;
+  const int y0 = band * a.band_rows, y1 = min(g.H, y0 + a.band_rows);
+  // dc rows that touch input rows [y0, y1): oy*SH - PT + i in [y0, y1)
+  const int o0 = max(0, (y0 + g.PT - g.KH + 1 + g.SH - 1) / g.SH);
+  const int o1 = min(g.OH, (y1 - 1 + g.PT) / g.SH + 1);
+  const int rowlen = g.OW * g.Cout;
+  const int nw = g.KH * g.KW * g.Cin * g.Cout;
+  float* s_dc = smem;
+  float* s_w = smem + ((a.band_rows_in * rowlen + 3) & ~3);
+  if (a.in_bn_on) bn_reduce_to_lds(a.in_bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
+  for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) s_stat[i] = 0.f;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) s_w[i] = a.w[i];
+  const int nd = max(0, o1 - o0) * rowlen;
+  const float* src = a.dc + ((long)b * g.OH + o0) * rowlen;
+  for (int i = threadIdx.x; i < nd; i += blockDim.x) s_dc[i] = src[i];
+  __syncthreads();
+
+  const int npix = (y1 - y0) * g.W;
+  const int cg = threadIdx.x % G;
+  const int ci0 = cg * CB;
+  const int nci = min(CB, g.Cin - ci0);
+  float dsum[CB], dxs[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) { dsum[c] = 0.f; dxs[c] = 0.f; }
+  const int ppp = blockDim.x / G;
+  for (int q = threadIdx.x / G; q < npix && threadIdx.x < ppp * G; q += ppp) {
+    const int y = y0 + q / g.W, x = q % g.W;
+    float acc[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) acc[c] = 0.f;
+    for (int i = 0; i < g.KH; ++i) {
+      const int ty = y + g.PT - i;
+      if (ty < 0 || ty % g.SH) continue;
+      const int oy = ty / g.SH;
+      if (oy >= g.OH) continue;
+      for (int j = 0; j < g.KW; ++j) {
+        const int tx = x + g.PL - j;
+        if (tx < 0 || tx % g.SW) continue;
+        const int ox = tx / g.SW;
+        if (ox >= g.OW) continue;
+        const float* drow = s_dc + (oy - o0) * rowlen + ox * g.Cout;
+        const float* wbase = s_w + ((i * g.KW + j) * g.Cin + ci0) * g.Cout;
+        for (int co = 0; co < g.Cout; ++co) {
+          const float gv = drow[co];
+#pragma unroll
+          for (int c = 0; c < CB; ++c)
+            if (c < nci) acc[c] = fmaf(gv, wbase[c * g.Cout + co], acc[c]);
+        }
+      }
+    }
+    const long p = ((long)b * g.H + y) * g.W + x;
+    const float* xrow = a.x_fwd ? a.x_fwd + p * g.Cin + ci0 : nullptr;
+    float* dxrow = a.dx + p * g.Cin + ci0;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      if (c >= nci) break;
+      float gv = acc[c];
+      if (xrow && (a.in_act || a.in_bn_on)) {
+        const float xv = xrow[c];
+        const int ch = ci0 + c;
+        const float z = a.in_bn_on ? xv * s_bn[256 + ch] + s_bn[384 + ch] : xv;
+        const float yv = act_fwd(z, a.in_act, a.in_alpha);
+        gv = act_bwd(gv, z, yv, a.in_act, a.in_alpha);
+        if (a.in_bn_on) {
+          const float xh = (xv - s_bn[ch]) * s_bn[128 + ch];
+          dsum[c] += gv;
+          dxs[c] += gv * xh;
+        }
+      }
+      dxrow[c] = gv;
+    }
+  }
+  if (a.in_bn_on && a.bwd_slab) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+      if (c < nci) { atomicAdd(&s_stat[ci0 + c], dsum[c]); atomicAdd(&s_stat[g.Cin + ci0 + c], dxs[c]); }
+    __syncthreads();
+    float* row = a.bwd_slab + (size_t)(blockIdx.x % a.nslab) * 2 * g.Cin;
+    for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) atomicAdd(&row[i], s_stat[i]);
+  }
+}
+
+constexpr int CB_T = 4;                  // channels per lane
+constexpr int STAGE_FLOATS = 12288;      // 48 KiB of staged rows per workgroup
+constexpr int SLAB_ROWS = 32;            // BN partial-slab rows (atomically folded)
+
+static int groups(int c) { return (c + CB_T - 1) / CB_T; }
+
+// Rows per band: one pass of the 256 lanes over (pixel, channel-group) pairs, and the
+// staged input rows within STAGE_FLOATS.
+static void fwd_bands(const ConvGeom& g, const PoolGeom& p, int& nbands, int& rows, int& rows_in) {
+  const int out_rows = p.on ? p.OH : g.OH, out_w = p.on ? p.OW : g.OW;
+  const int ppp = CONV_THREADS / groups(g.Cout);
+  rows = std::max(1, std::min(out_rows, ppp / std::max(1, out_w)));
+  auto in_rows = [&](int r) {
+    int crow = p.on ? (r - 1) * p.SH + p.KH : r;
+    return std::min(g.H, (crow - 1) * g.SH + g.KH);
+  };
+  while (rows > 1 && in_rows(rows) * g.W * g.Cin > STAGE_FLOATS) --rows;
+  nbands = (out_rows + rows - 1) / rows;
+  rows_in = in_rows(rows);
+}
+
+static void dgrad_bands(const ConvGeom& g, int& nbands, int& rows, int& rows_in) {
+  const int ppp = CONV_THREADS / groups(g.Cin);
+  rows = std::max(1, std::min(g.H, ppp / std::max(1, g.W)));
+  auto in_rows = [&](int r) { return std::min(g.OH, (r + g.KH - 1) / g.SH + 1); };
+  while (rows > 1 && in_rows(rows) * g.OW * g.Cout > STAGE_FLOATS) --rows;
+  nbands = (g.H + rows - 1) / rows;
+  rows_in = in_rows(rows);
+}
+
+static ConvGeom geom_from(const int* v) {
+  return ConvGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12]};
+}
+
+static bool set_lds_attr(const void* fn) {
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;
+}
+
+}  // namespace csa
+
+using namespace csa;
+
+// Number of BN partial-slab rows a csa_conv_fwd launch writes (the slab must be zeroed
+// before every launch: rows are accumulated with atomics).
+CSA_API int csa_conv_fwd_nslab(const int* geom, const int* pool) {
+  (void)geom; (void)pool;
+  return SLAB_ROWS;
+}
+
+// Forward conv unit: y = pool(act(conv(T(x)) + bias)), T = optional bn+act on the input.
+CSA_API int csa_conv_fwd(const float* x, const uint8_t* img, const int64_t* idx, const float* w,
+                         const float* bias, float* y, uint8_t* argmax, float* stat_slab,
+                         const int* geom /*13*/, const int* pool /*9*/, const float* in_bn_slab,
+                         int in_bn_nslab, float in_bn_count, float in_bn_eps,
+                         const float* in_bn_scale, const float* in_bn_offset, int in_act,
+                         float in_alpha, int out_act, float out_alpha, hipStream_t st) {
+  ConvFwdArgs a{};
+  a.g = geom_from(geom);
+  a.pool = PoolGeom{pool[0], pool[1], pool[2], pool[3], pool[4], pool[5], pool[6], pool[7], pool[8]};
+  if (a.g.Cin > 128 || a.g.Cout > 128) return -1;
+  a.x = x; a.img = img; a.idx = idx;
+  a.in_bn = BNRef{in_bn_slab, in_bn_nslab, a.g.Cin, in_bn_count, in_bn_eps, in_bn_scale, in_bn_offset};
+  a.in_bn_on = in_bn_slab != nullptr;
+  a.in_act = in_act; a.in_alpha = in_alpha;
+  a.w = w; a.bias = bias; a.out_act = out_act; a.out_alpha = out_alpha;
+  a.y = y; a.argmax = argmax; a.stat_slab = stat_slab; a.nslab = SLAB_ROWS;
+  fwd_bands(a.g, a.pool, a.nbands, a.band_rows, a.band_rows_in);
+  const size_t nin = ((size_t)a.band_rows_in * a.g.W * a.g.Cin + 3) & ~(size_t)3;
+  const size_t shm = (nin + (size_t)a.g.KH * a.g.KW * a.g.Cin * a.g.Cout) * sizeof(float);
+  if (shm > 150 * 1024) return -2;
+  static bool attr = set_lds_attr((const void*)conv_fwd_kernel<CB_T, true>) &&
+                     set_lds_attr((const void*)conv_fwd_kernel<CB_T, false>);
+  (void)attr;
+  dim3 grid((unsigned)(a.g.B * a.nbands));
+  if (img) hipLaunchKernelGGL((conv_fwd_kernel<CB_T, true>), grid, dim3(CONV_THREADS), shm, st, a);
+  else hipLaunchKernelGGL((conv_fwd_kernel<CB_T, false>), grid, dim3(CONV_THREADS), shm, st, a);
+  return (int)hipGetLastError();
+}
+
+// g = {B, h, w, C, OH, OW, pool_on, PKH, PKW, PSH, PSW, PPT, PPL}.  When the pool windows
+// are not a tiling (kernel != stride) dc must be zeroed by the caller (atomics).
+CSA_API int csa_route_bwd(const float* dz, const float* y, const uint8_t* argmax, float* dc,
+                          const int* g /*13*/, int out_act, float out_alpha, const float* bn_slab,
+                          int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                          const float* bn_offset, const float* bwd_slab, int bwd_nslab,
+                          float* dscale, float* doffset, float* run_mean, float* run_var,
+                          float momentum, hipStream_t st) {
+  RouteArgs a{};
+  a.run_mean = run_mean; a.run_var = run_var; a.momentum = momentum;
+  a.dz = dz; a.y = y; a.argmax = argmax; a.dc = dc;
+  a.B = g[0]; a.h = g[1]; a.w = g[2]; a.C = g[3]; a.OH = g[4]; a.OW = g[5];
+  a.pool_on = g[6]; a.PKW = g[8]; a.PSH = g[9]; a.PSW = g[10]; a.PPT = g[11]; a.PPL = g[12];
+  if (a.C > 128) return -1;
+  a.overlap = a.pool_on && (g[7] != g[9] || g[8] != g[10]);
+  a.out_act = out_act; a.out_alpha = out_alpha;
+  a.bn = BNRef{bn_slab, bn_nslab, a.C, bn_count, bn_eps, bn_scale, bn_offset};
+  a.bn_on = bn_slab != nullptr;
+  a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab; a.dscale = dscale; a.doffset = doffset;
+  long n = (long)a.B * a.h * a.w * a.C;
+  hipLaunchKernelGGL(route_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_conv_dgrad_nslab(const int* geom) {
+  (void)geom;
+  return SLAB_ROWS;
+}
+
+CSA_API int csa_conv_dgrad(const float* dc, const float* w, float* dx, const int* geom,
+                           const float* x_fwd, int in_act, float in_alpha, const float* bn_slab,
+                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                           const float* bn_offset, float* bwd_slab, hipStream_t st) {
+  ConvDgradArgs a{};
+  a.g = geom_from(geom);
+  if (a.g.Cin > 128 || a.g.Cout > 128) return -1;
+  a.dc = dc; a.w = w; a.dx = dx; a.x_fwd = x_fwd; a.in_act = in_act; a.in_alpha = in_alpha;
+  a.in_bn = BNRef{bn_slab, bn_nslab, a.g.Cin, bn_count, bn_eps, bn_scale, bn_offset};
+  a.in_bn_on = bn_slab != nullptr;
+  a.bwd_slab = bwd_slab; a.nslab = SLAB_ROWS;
+  dgrad_bands(a.g, a.nbands, a.band_rows, a.band_rows_in);
+  const size_t nd = ((size_t)a.band_rows_in * a.g.OW * a.g.Cout + 3) & ~(size_t)3;
+  const size_t shm = (nd + (size_t)a.g.KH * a.g.KW * a.g.Cin * a.g.Cout) * sizeof(float);
+  if (shm > 150 * 1024) return -2;
+  static bool attr = set_lds_attr((const void*)conv_dgrad_kernel<CB_T>);
+  (void)attr;
+  dim3 grid((unsigned)(a.g.B * a.nbands));
+  hipLaunchKernelGGL((conv_dgrad_kernel<CB_T>), grid, dim3(CONV_THREADS), shm, st, a);
+  return (int)hipGetLastError();
+}

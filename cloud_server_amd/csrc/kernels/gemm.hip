@@ -1,0 +1,419 @@
+// f32 MFMA GEMM family for the digit-CNN training step (gfx950 / CDNA4).
+//
+// The dense layers of the reference model (construct_distribute.py:168-182, 252-264) are
+// skinny: M = per-GPU batch (50), N and K in the hundreds/thousands.  A square-tile library
+// GEMM leaves most of the chip idle on such shapes (hipBLASLt took 7-17 µs per call in
+// profiles/r1_torch_baseline.md).  This kernel instead:
+//   * uses the exact-f32 MFMA v_mfma_f32_32x32x2_f32 (one 32x32 accumulator per wave),
+//   * splits K across the 4 waves of a workgroup (WK) and across workgroups (split-K),
+//     so every shape launches ~1000 waves (one per SIMD) even at M = 50,
+//   * builds operands through loader functors: row-major, transposed, im2col (conv
+//     weight-gradient as an implicit GEMM) and a fused BatchNorm-apply + activation
+//     prologue, so normalised / activated tensors are never materialised in HBM,
+//   * ends in epilogue functors: store, split-K atomic add, bias, and the fused
+//     activation-backward + BatchNorm-backward partial statistics.
+//
+// MFMA 32x32x2 f32 operand map (cdna_hip_programming.md §3):
+//   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
+//   D: reg r of lane l is D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31]
+#include "common.h"
+
+namespace csa {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int KC = 16;        // K chunk staged per iteration (8 MFMAs)
+constexpr int LDS_PAD = 33;   // row stride of the 32-wide staging tiles (conflict-free)
+constexpr int MAXC = 128;     // max BatchNorm channels handled in LDS
+
+// LDS tables shared by loaders/epilogues: [mean | rstd | a | b] x MAXC
+struct BNTables { const float *mean, *rstd, *a, *b; };
+
+// ----------------------------------------------------------------------------------
+// Loaders: value(r, c) with r the "outer" index (m for A, n for B) and c the K index.
+// KCONTIG says whether consecutive K are contiguous in memory (picks the lane mapping).
+// ----------------------------------------------------------------------------------
+struct LoadRowMajor {          // elem(r, c) = p[r * ld + c]
+  const float* p; long ld; int rows, cols;
+  static constexpr bool KCONTIG = true;
+  __device__ void bind(const BNTables&) {}
+  __device__ float operator()(int r, int c) const {
+    return (r < rows && c < cols) ? p[(long)r * ld + c] : 0.f;
+  }
+};
+
+struct LoadColMajor {          // elem(r, c) = p[c * ld + r]
+  const float* p; long ld; int rows, cols;
+  static constexpr bool KCONTIG = false;
+  __device__ void bind(const BNTables&) {}
+  __device__ float operator()(int r, int c) const {
+    return (r < rows && c < cols) ? p[(long)c * ld + r] : 0.f;
+  }
+};
+
+// Activation tensor X[m][f] read through an optional BN-apply (channel = f % C) and act.
+// ROWS_ARE_BATCH: elem(r=m, c=f) (dense fwd A);  else elem(r=f, c=m) (dense wgrad A).
+// ones_row: for wgrad, row f == feat returns 1 (m < batch) -> bias gradient row.
+template <bool ROWS_ARE_BATCH>
+struct LoadBNAct {
+  const float* x; long ld; int batch, feat; FastDiv C; int act; float alpha; int has_bn, ones_row;
+  const float* ta; const float* tb;
+  static constexpr bool KCONTIG = ROWS_ARE_BATCH;
+  __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
+  __device__ float operator()(int r, int c) const {
+    int m = ROWS_ARE_BATCH ? r : c, f = ROWS_ARE_BATCH ? c : r;
+    if (m >= batch) return 0.f;
+    if (f >= feat) return (ones_row && f == feat) ? 1.f : 0.f;
+    float v = x[(long)m * ld + f];
+    if (has_bn) { int q, ch; C.divmod(f, q, ch); v = v * ta[ch] + tb[ch]; }
+    return act_fwd(v, act, alpha);
+  }
+};
+
+// im2col^T for conv weight gradients: elem(r = kconv, c = p), kconv = (i, j, ci),
+// p = (b, oy, ox) over the conv OUTPUT pixels; reads the conv input (NHWC fp32, or the
+// raw uint8 dataset gathered through idx for the first layer).  Row kconv == KH*KW*Cin
+// is the ones row (bias gradient).  The input may carry a BN-apply + act transform.
+template <bool U8>
+struct LoadIm2colT {
+  const float* x; const uint8_t* img; const int64_t* idx;
+  int B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, ones_row, has_bn, act; float alpha;
+  FastDiv dCin, dKW, dOW, dOH;
+  const float* ta; const float* tb;
+  static constexpr bool KCONTIG = false;
+  __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
+  __device__ float operator()(int r, int c) const {
+    const int kc = KH * KW * Cin, P = B * OH * OW;
+    if (c >= P) return 0.f;
+    if (r >= kc) return (ones_row && r == kc) ? 1.f : 0.f;
+    int t, ci, i, j, t2, ox, b, oy;
+    dCin.divmod(r, t, ci);
+    dKW.divmod(t, i, j);
+    dOW.divmod(c, t2, ox);
+    dOH.divmod(t2, b, oy);
+    int y = oy * SH - PT + i, xx = ox * SW - PL + j;
+    if (y < 0 || y >= H || xx < 0 || xx >= W) return 0.f;
+    if (U8) return (float)img[idx[b] * (long)(H * W * Cin) + ((long)y * W + xx) * Cin + ci] * (1.0f / 255.0f);
+    float v = x[(((long)b * H + y) * W + xx) * Cin + ci];
+    if (has_bn) v = v * ta[ci] + tb[ci];
+    return act_fwd(v, act, alpha);
+  }
+};
+
+// ----------------------------------------------------------------------------------
+// Epilogues: called once per output element with the fully (intra-WG) reduced value.
+// ----------------------------------------------------------------------------------
+struct EpiStore {              // C[m][n] (+)= v (+ bias[n] once); row m == M -> extra row
+  float* c; long ldc; int M, N; const float* bias; int atomic; float* extra; float scale;
+  static constexpr bool NEEDS_LDS = false;
+  __device__ void bind(const BNTables&) {}
+  __device__ void operator()(int m, int n, float v, bool first_split, float*) const {
+    if (n >= N) return;
+    float* p;
+    if (m < M) p = c + (long)m * ldc + n;
+    else if (extra && m == M) p = extra + n;
+    else return;
+    v *= scale;
+    if (bias && first_split && m < M) v += bias[n];
+    if (atomic) atomicAdd(p, v); else *p = v;
+  }
+};
+
+// Dense/conv dgrad epilogue through the activation (and optional BatchNorm) that formed
+// the GEMM's A operand in the forward pass: g = dL/dh with h = act(bn(x)):
+//   dz = act'(g); store dz; per-channel {sum dz, sum dz*xhat} into LDS for BN backward.
+struct EpiActBNBwd {
+  float* dz; long ld; int M, F; FastDiv C; const float* x; int act; float alpha; int has_bn;
+  BNTables t;
+  static constexpr bool NEEDS_LDS = true;
+  __device__ void bind(const BNTables& tt) { t = tt; }
+  __device__ void operator()(int m, int f, float g, bool, float* lds_acc) const {
+    if (m >= M || f >= F) return;
+    float xv = x[(long)m * ld + f];
+    int q, ch;
+    C.divmod(f, q, ch);
+    float z = has_bn ? xv * t.a[ch] + t.b[ch] : xv;
+    float y = act_fwd(z, act, alpha);
+    float d = act_bwd(g, z, y, act, alpha);
+    dz[(long)m * ld + f] = d;
+    if (has_bn) {
+      float xhat = (xv - t.mean[ch]) * t.rstd[ch];
+      atomicAdd(&lds_acc[ch], d);
+      atomicAdd(&lds_acc[MAXC + ch], d * xhat);
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------------
+// The kernel.  Grid: x = N tiles, y = M tiles, z = split-K slices.
+// WG tile = (32*WM) x (32*WN); its K slice is split WK ways across the waves.
+// ----------------------------------------------------------------------------------
+template <int WM, int WN, int WK, class LA, class LB, class EPI>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
+                                                       int k_per_split, BNRef bn, int bn_on,
+                                                       float* bn_slab_out, int slab_C) {
+  static_assert(WM * WN * WK == 4, "4 waves per workgroup");
+  constexpr int PER = (32 * KC) / 64;   // staged elements per lane per operand per chunk
+  __shared__ float s_stage[4][2][KC * LDS_PAD];
+  __shared__ float s_red[(WK > 1) ? (WM * WN * (WK - 1) * 16 * 64) : 1];
+  __shared__ float s_bn[4 * MAXC];
+  __shared__ float s_acc[2 * MAXC];
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wk = wave / (WM * WN), wmn = wave % (WM * WN);
+  const int wm = wmn / WN, wn = wmn % WN;
+  const int m0 = blockIdx.y * 32 * WM + wm * 32;
+  const int n0 = blockIdx.x * 32 * WN + wn * 32;
+
+  if (bn_on) bn_reduce_to_lds(bn, s_bn, s_bn + MAXC, s_bn + 2 * MAXC, s_bn + 3 * MAXC, s_acc);
+  if (EPI::NEEDS_LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * MAXC; i += blockDim.x) s_acc[i] = 0.f;
+  }
+  __syncthreads();
+  const BNTables tabs{s_bn, s_bn + MAXC, s_bn + 2 * MAXC, s_bn + 3 * MAXC};
+  la.bind(tabs);
+  lb.bind(tabs);
+  epi.bind(tabs);
+
+  // K range of this wave (multiples of KC keep every wave's chunks aligned)
+  const int ks0 = blockIdx.z * k_per_split;
+  const int ks1 = min(K, ks0 + k_per_split);
+  const int klen = max(0, ks1 - ks0);
+  const int kw_len = ((klen + WK - 1) / WK + KC - 1) / KC * KC;
+  const int kb = ks0 + wk * kw_len;
+  const int ke = min(ks1, kb + kw_len);
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  float* sa = s_stage[wave][0];
+  float* sb = s_stage[wave][1];
+  // lane -> (row, kk) maps per operand
+  int ra_[PER], ka_[PER], rb_[PER], kb_[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int idx = lane + 64 * e;
+    if (LA::KCONTIG) { ra_[e] = idx / KC; ka_[e] = idx % KC; } else { ka_[e] = idx / 32; ra_[e] = idx % 32; }
+    if (LB::KCONTIG) { rb_[e] = idx / KC; kb_[e] = idx % KC; } else { kb_[e] = idx / 32; rb_[e] = idx % 32; }
+  }
+  float va[PER], vb[PER];
+  auto fetch = [&](int k) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      va[e] = (k + ka_[e] < ke) ? la(m0 + ra_[e], k + ka_[e]) : 0.f;
+      vb[e] = (k + kb_[e] < ke) ? lb(n0 + rb_[e], k + kb_[e]) : 0.f;
+    }
+  };
+  if (kb < ke) fetch(kb);
+  for (int k = kb; k < ke; k += KC) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      sa[ka_[e] * LDS_PAD + ra_[e]] = va[e];
+      sb[kb_[e] * LDS_PAD + rb_[e]] = vb[e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (k + KC < ke) fetch(k + KC);     // next chunk's global loads fly under the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 2) {
+      float av = sa[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
+      float bv = sb[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+
+  if (WK > 1) {  // intra-workgroup split-K reduction through LDS
+    if (wk > 0) {
+      float* dst = s_red + ((size_t)(wmn * (WK - 1) + (wk - 1)) * 16 * 64);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dst[i * 64 + lane] = acc[i];
+    }
+    __syncthreads();
+    if (wk == 0) {
+      for (int s = 0; s < WK - 1; ++s) {
+        const float* src = s_red + ((size_t)(wmn * (WK - 1) + s) * 16 * 64);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] += src[i * 64 + lane];
+      }
+    }
+  }
+  if (wk == 0) {
+    const bool first = blockIdx.z == 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      epi(m0 + row, n0 + (lane & 31), acc[i], first, s_acc);
+    }
+  }
+  if (EPI::NEEDS_LDS && bn_slab_out) {
+    __syncthreads();
+    const int slab_row = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    for (int i = threadIdx.x; i < 2 * slab_C; i += blockDim.x)
+      bn_slab_out[(size_t)slab_row * 2 * slab_C + i] = s_acc[(i < slab_C) ? i : (MAXC + i - slab_C)];
+  }
+}
+
+// Wave layout + split-K so that one launch has ~1024 waves (one per SIMD on 256 CUs).
+struct Plan { int wm, wn, wk, splits, kps; };
+
+static Plan plan_gemm(int M, int N, int K, bool allow_split) {
+  const int target_waves = 1024;
+  int tm = (M + 31) / 32, tn = (N + 31) / 32;
+  int tiles = tm * tn;
+  Plan p;
+  if (tiles >= 512) { p.wm = 2; p.wn = 2; p.wk = 1; }
+  else if (tiles >= 256) { p.wm = 1; p.wn = 2; p.wk = 2; }
+  else { p.wm = 1; p.wn = 1; p.wk = 4; }
+  int wg = ((tm + p.wm - 1) / p.wm) * ((tn + p.wn - 1) / p.wn);
+  int waves = wg * 4;
+  int splits = 1;
+  if (allow_split)
+    while (waves * splits * 2 <= target_waves && K / (splits * 2 * p.wk) >= 48) splits *= 2;
+  p.splits = splits;
+  int kps = (K + splits - 1) / splits;
+  p.kps = (kps + KC - 1) / KC * KC;
+  return p;
+}
+
+static int grid_slabs(const Plan& p, int M, int N) {
+  return ((N + 32 * p.wn - 1) / (32 * p.wn)) * ((M + 32 * p.wm - 1) / (32 * p.wm)) * p.splits;
+}
+
+template <class LA, class LB, class EPI>
+static int launch_gemm(const Plan& p, LA la, LB lb, EPI epi, int M, int N, int K, const BNRef& bn,
+                       int bn_on, float* slab_out, int slab_C, hipStream_t st) {
+  dim3 grid((N + 32 * p.wn - 1) / (32 * p.wn), (M + 32 * p.wm - 1) / (32 * p.wm), p.splits);
+#define CSA_L(WM, WN, WK)                                                                   \
+  hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, WK, LA, LB, EPI>), grid, dim3(256), 0, st, la, \
+                     lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C)
+  if (p.wm == 2 && p.wn == 2) CSA_L(2, 2, 1);
+  else if (p.wm == 1 && p.wn == 2) CSA_L(1, 2, 2);
+  else CSA_L(1, 1, 4);
+#undef CSA_L
+  return (int)hipGetLastError();
+}
+
+static BNRef make_bn(const float* slab, int nslab, int C, float count, float eps,
+                     const float* scale, const float* offset) {
+  return BNRef{slab, nslab, C, count, eps, scale, offset};
+}
+
+}  // namespace csa
+
+using namespace csa;
+
+// ===================================================================================
+// C ABI (called through ctypes from cloud_server_amd/ops/fused.py)
+// ===================================================================================
+
+// How many split-K slices a dense forward of this shape uses (>1 => Y must be zeroed).
+CSA_API int csa_dense_fwd_splits(int M, int N, int K) { return plan_gemm(M, N, K, true).splits; }
+
+// Y[M][N] (+)= act(bn(X))[M][K] @ W[K][N] + bias.  Y zeroed by caller when splits > 1.
+CSA_API int csa_dense_fwd(const float* X, const float* W, const float* bias, float* Y, int M,
+                          int N, int K, const float* bn_slab, int bn_nslab, int bn_C,
+                          float bn_count, float bn_eps, const float* bn_scale,
+                          const float* bn_offset, int in_act, float in_alpha, hipStream_t st) {
+  if (bn_slab && bn_C > MAXC) return -1;
+  Plan p = plan_gemm(M, N, K, true);
+  BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
+  LoadBNAct<true> la{X, (long)K, M, K, FastDiv(bn_C > 0 ? bn_C : 1), in_act, in_alpha, bn_slab != nullptr, 0,
+                     nullptr, nullptr};
+  LoadColMajor lb{W, (long)N, N, K};          // B(k, n) = W[k][n]
+  EpiStore epi{Y, (long)N, M, N, bias, p.splits > 1, nullptr, 1.f};
+  return launch_gemm(p, la, lb, epi, M, N, K, bn, bn_slab != nullptr, nullptr, 0, st);
+}
+
+// dX[M][Kin] = dY[M][Nout] @ W[Kin][Nout]^T, then (optionally) through the forward
+// input transform h = act(bn(x)):  stores dz = dL/d(bn input or act input) and emits
+// the BN-backward partial slab [nslab][2][C] ({sum dz, sum dz*xhat}).
+// Returns the slab row count used (>= 1) or a negative error.
+CSA_API int csa_dense_dgrad(const float* dY, const float* W, float* dX, int M, int Kin, int Nout,
+                            const float* x_fwd, int act, float alpha, const float* bn_slab,
+                            int bn_nslab, int bn_C, float bn_count, float bn_eps,
+                            const float* bn_scale, const float* bn_offset, float* bwd_slab,
+                            hipStream_t st) {
+  if (bn_slab && bn_C > MAXC) return -1;
+  const bool transform = (act != ACT_NONE) || (bn_slab != nullptr);
+  Plan p = plan_gemm(M, Kin, Nout, !transform);
+  BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
+  LoadRowMajor la{dY, (long)Nout, M, Nout};   // A(m, k=n) = dY[m][n]
+  LoadRowMajor lb{W, (long)Nout, Kin, Nout};  // B(k=n, j) = W[j][n]
+  int rc;
+  if (transform) {
+    EpiActBNBwd epi{dX, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), x_fwd, act, alpha,
+                    bn_slab != nullptr, BNTables{}};
+    rc = launch_gemm(p, la, lb, epi, M, Kin, Nout, bn, bn_slab != nullptr,
+                     bn_slab ? bwd_slab : nullptr, bn_C, st);
+  } else {
+    EpiStore epi{dX, (long)Kin, M, Kin, nullptr, p.splits > 1, nullptr, 1.f};
+    rc = launch_gemm(p, la, lb, epi, M, Kin, Nout, bn, 0, nullptr, 0, st);
+  }
+  if (rc) return -rc;
+  return grid_slabs(p, M, Kin);
+}
+
+CSA_API int csa_dense_dgrad_splits(int M, int Kin, int Nout, int transform) {
+  return plan_gemm(M, Kin, Nout, !transform).splits;
+}
+
+CSA_API int csa_dense_dgrad_slabs(int M, int Kin, int Nout) {
+  Plan p = plan_gemm(M, Kin, Nout, false);
+  return grid_slabs(p, M, Kin);
+}
+
+// dW[Kin][Nout] (+)= act(bn(X))^T @ dY * scale, db[Nout] (+)= colsum(dY) * scale.
+// Output accumulated with atomics when split (caller zeroes dW/db) — see *_splits.
+CSA_API int csa_dense_wgrad_splits(int M, int Kin, int Nout) {
+  return plan_gemm(Kin + 1, Nout, M, true).splits;
+}
+
+CSA_API int csa_dense_wgrad(const float* X, const float* dY, float* dW, float* db, int M, int Kin,
+                            int Nout, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
+                            float bn_eps, const float* bn_scale, const float* bn_offset, int in_act,
+                            float in_alpha, float scale, hipStream_t st) {
+  if (bn_slab && bn_C > MAXC) return -1;
+  const int Mg = Kin + (db ? 1 : 0);
+  Plan p = plan_gemm(Mg, Nout, M, true);
+  BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
+  LoadBNAct<false> la{X, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), in_act, in_alpha,
+                      bn_slab != nullptr, db != nullptr, nullptr, nullptr};
+  LoadColMajor lb{dY, (long)Nout, Nout, M};   // B(k=m, n) = dY[m][n]
+  EpiStore epi{dW, (long)Nout, Kin, Nout, nullptr, p.splits > 1, db, scale};
+  return launch_gemm(p, la, lb, epi, Mg, Nout, M, bn, bn_slab != nullptr, nullptr, 0, st);
+}
+
+// Conv weight gradient as implicit GEMM:  dW[(i,j,ci)][co] = sum_p im2col(x)[p][(i,j,ci)] dOut[p][co]
+// x: fp32 NHWC [B,H,W,Cin] (optionally through bn+act) or, if img != null, the raw uint8
+// dataset gathered through idx.  dOut: [B,OH,OW,Cout].  Always atomic (caller zeroes).
+CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* idx, const float* dOut,
+                           float* dW, float* db, int B, int H, int W, int Cin, int KH, int KW, int SH,
+                           int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
+                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                           const float* bn_offset, int in_act, float in_alpha, hipStream_t st) {
+  if (bn_slab && Cin > MAXC) return -1;
+  const int kc = KH * KW * Cin;
+  const int Mg = kc + (db ? 1 : 0);
+  const int P = B * OH * OW;
+  Plan p = plan_gemm(Mg, Cout, P, true);
+  // conv wgrad is always accumulated with atomics (split-K over pixels)
+  BNRef bn = make_bn(bn_slab, bn_nslab, Cin, bn_count, bn_eps, bn_scale, bn_offset);
+  LoadColMajor lb{dOut, (long)Cout, Cout, P};  // B(k=p, co) = dOut[p][co]
+  EpiStore epi{dW, (long)Cout, kc, Cout, nullptr, 1, db, 1.f};
+  if (img) {
+    LoadIm2colT<true> la{nullptr, img, idx, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW,
+                         db != nullptr, 0, 0, 0.f, FastDiv(Cin), FastDiv(KW), FastDiv(OW), FastDiv(OH),
+                         nullptr, nullptr};
+    return launch_gemm(p, la, lb, epi, Mg, Cout, P, bn, 0, nullptr, 0, st);
+  }
+  LoadIm2colT<false> la{x, nullptr, nullptr, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW,
+                        db != nullptr, bn_slab != nullptr, in_act, in_alpha, FastDiv(Cin), FastDiv(KW),
+                        FastDiv(OW), FastDiv(OH), nullptr, nullptr};
+  return launch_gemm(p, la, lb, epi, Mg, Cout, P, bn, bn_slab != nullptr, nullptr, 0, st);
+}

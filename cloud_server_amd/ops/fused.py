@@ -1,0 +1,100 @@
+"""ctypes bindings for ``libcsa_kernels.so`` (the hand-written gfx950 kernels).
+
+The library is plain HIP with a C ABI (no torch C++ extension, no hipify): tensors are
+passed as raw device pointers and every launcher takes the current HIP stream, so calls
+made while ``torch.cuda.graph`` is capturing become graph nodes.  ``import torch`` must
+come first so the library binds to the HIP runtime torch already loaded (same SONAME).
+
+``load(required=True)`` raises if the library is missing — a GPU run never silently
+falls back to PyTorch ops.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import torch
+
+from . import build as _build
+
+_LIB: Optional[C.CDLL] = None
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_long
+F = C.c_float
+
+ACT_IDS = {None: 0, "none": 0, "sigmoid": 1, "relu": 2, "leaky_relu": 3}
+
+_SIGS = {
+    "csa_dense_fwd_splits": (I, [I, I, I]),
+    "csa_dense_fwd": (I, [P, P, P, P, I, I, I, P, I, I, F, F, P, P, I, F, P]),
+    "csa_dense_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P]),
+    "csa_dense_dgrad_splits": (I, [I, I, I, I]),
+    "csa_dense_dgrad_slabs": (I, [I, I, I]),
+    "csa_dense_wgrad_splits": (I, [I, I, I]),
+    "csa_dense_wgrad": (I, [P, P, P, P, I, I, I, P, I, I, F, F, P, P, I, F, F, P]),
+    "csa_conv_wgrad": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I,
+                           P, I, F, F, P, P, I, F, P]),
+    "csa_conv_fwd_nslab": (I, [P, P]),
+    "csa_conv_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, F, F, P, P, I, F, I, F, P]),
+    "csa_route_bwd": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, I, P, P, P, P, F, P]),
+    "csa_conv_dgrad_nslab": (I, [P]),
+    "csa_conv_dgrad": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, P]),
+    "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P]),
+    "csa_optimizer": (I, [I, P, P, P, P, L, F, P, P, P, I, P, P, P, P, P, P, F, I, P]),
+    "csa_zero": (I, [P, P, I, P]),
+}
+
+
+def lib_path() -> str:
+    return _build.KERNEL_LIB
+
+
+def available() -> bool:
+    return os.path.exists(lib_path())
+
+
+def load(required: bool = True) -> Optional[C.CDLL]:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        if os.environ.get("CSA_AUTOBUILD", "1") == "1":
+            try:
+                _build.build_kernels()
+            except Exception as e:  # pragma: no cover - reported below
+                if required:
+                    raise RuntimeError(f"cannot build {path}: {e}") from e
+        if not os.path.exists(path):
+            if required:
+                raise RuntimeError(f"HIP kernel library missing: {path} (run python -m cloud_server_amd.ops.build)")
+            return None
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0 or (rc > 0 and what.endswith("!")):
+        raise RuntimeError(f"{what.rstrip('!')} failed with code {rc}")
+    return rc
+
+
+def ints(vals: Sequence[int]):
+    arr = (C.c_int * len(vals))(*[int(v) for v in vals])
+    return arr

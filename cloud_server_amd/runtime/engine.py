@@ -91,9 +91,15 @@ class TrainEngine:
         if backend == "auto":
             backend = "hip" if self.device.type == "cuda" else "torch"
         self.backend = backend
+        self.fallback_reason = ""
         if backend == "hip":
-            from .hip_program import HipProgram
-            self.program: StepProgram = HipProgram(self)
+            from .hip_program import HipProgram, Unsupported
+            try:
+                self.program: StepProgram = HipProgram(self)
+            except Unsupported as exc:   # config outside the fused-kernel family
+                self.fallback_reason = str(exc)
+                self.backend = backend = "torch"
+                self.program = TorchProgram(self)
         else:
             self.program = TorchProgram(self)
         if use_graph is None:
@@ -116,6 +122,15 @@ class TrainEngine:
         else:
             self.sync.allreduce(self.flat_grad)
             self._opt(self.flat, self.flat_grad, self.slots)
+
+    def after_backward_sync(self) -> None:
+        """Gradient sync between backward and the (fused) optimizer of the HIP program."""
+        if not self.ctx.enabled:
+            return
+        if self.sync.strategy == "ps":
+            self.sync.reduce_scatter(self.flat_grad, self.grad_shard)
+        else:
+            self.sync.allreduce(self.flat_grad)
 
     def _opt(self, w, g, slots) -> None:
         if self.opt_id == optim_ref.OPT_ADAM:

@@ -1,0 +1,410 @@
+"""Lower a DSL network to the hand-written gfx950 kernels (the MI355X training step).
+
+Lowering groups the reference layer list (construct_distribute.py:208-265) into:
+
+* **conv units** ``conv [act] [pool]`` — one ``csa_conv_fwd`` launch each (bias, act and
+  max-pool fused, argmax kept for backward, BN partial statistics emitted when a norm
+  follows);
+* **transforms** ``[norm] [act]`` between units — never materialised: the CONSUMER applies
+  BN-apply + activation while loading its input (conv input read, GEMM A-prologue,
+  im2col loader) and its dgrad epilogue applies the activation backward and emits the
+  BN-backward statistics;
+* **dense units** ``connect`` — MFMA GEMMs (``csa_dense_fwd/_dgrad/_wgrad``);
+* the **head** — one single-workgroup kernel: logits, loss, accuracy, head gradients,
+  input gradient and the step/metric bookkeeping.
+
+Backward runs the units in reverse (``csa_route_bwd`` = BN backward + act backward +
+max-pool routing; ``csa_conv_dgrad``; ``csa_conv_wgrad`` as an implicit MFMA GEMM),
+then gradient all-reduce (data parallel) and ONE fused optimizer launch which also
+zeroes next step's atomic accumulators and updates BN running statistics.
+
+Patterns outside this family (e.g. a 2-D norm after a dense layer, a standalone pool
+after a norm, a norm directly before the head) raise ``Unsupported``; the engine then
+uses ``TorchProgram`` for that job.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from ..models.dsl import ActSpec, ConvSpec, DenseSpec, LayerPlan, NormSpec, PoolSpec
+from ..ops import fused as K
+from ..ops import optim_ref
+
+
+class Unsupported(Exception):
+    pass
+
+
+def _act_id(sp: Optional[ActSpec]) -> int:
+    if sp is None:
+        return 0
+    if sp.func == "leaky_relu" and sp.alpha <= 0:
+        raise Unsupported("leaky_relu with alpha <= 0")
+    return K.ACT_IDS[sp.func]
+
+
+def _alpha(sp: Optional[ActSpec]) -> float:
+    return float(sp.alpha) if sp is not None else 0.0
+
+
+@dataclass
+class Transform:
+    """Pending ``[norm] [act]`` applied by the consumer of a tensor."""
+    norm: Optional[LayerPlan] = None
+    act: Optional[ActSpec] = None
+    slab: Optional[torch.Tensor] = None     # forward BN partial slab of the tensor
+    nslab: int = 0
+    count: float = 0.0
+    bwd_slab: Optional[torch.Tensor] = None  # filled by the consumer's dgrad
+    bwd_nslab: int = 0
+
+    @property
+    def has_bn(self) -> bool:
+        return self.norm is not None
+
+
+@dataclass
+class Unit:
+    kind: str                               # "conv" | "dense"
+    layer: LayerPlan
+    act: Optional[ActSpec] = None           # conv: fused output act
+    pool: Optional[LayerPlan] = None        # conv: fused pool
+    in_tf: Transform = field(default_factory=Transform)   # transform of this unit's INPUT
+    x: Optional[torch.Tensor] = None        # input tensor (pre-transform), None = raw images
+    y: Optional[torch.Tensor] = None        # output (post act/pool)
+    argmax: Optional[torch.Tensor] = None
+    dy: Optional[torch.Tensor] = None       # grad wrt output (or wrt the next BN output)
+    dc: Optional[torch.Tensor] = None       # conv: grad wrt pre-act conv output
+    splits_fwd: int = 1
+
+
+class HipProgram:
+    def __init__(self, eng):
+        self.e = eng
+        self.lib = K.load(required=True)
+        if eng.device.type != "cuda":
+            raise Unsupported("HIP program needs a GPU device")
+        self.B = eng.cfg.batch_size
+        self.model = eng.model
+        self.views = eng.model.state.views(eng.flat)
+        self.gviews = eng.model.state.views(eng.flat_grad)
+        self._lower()
+        self._alloc()
+        self.zero_regions: List[torch.Tensor] = []
+        self._collect_zero_regions()
+        self._zero_now()
+
+    # ------------------------------------------------------------------ lowering
+    def _lower(self) -> None:
+        layers = self.e.model.plan.layers
+        units: List[Unit] = []
+        pending = Transform()
+        i = 0
+        while i < len(layers):
+            lp = layers[i]
+            sp = lp.spec
+            if isinstance(sp, ConvSpec):
+                u = Unit("conv", lp, in_tf=pending)
+                pending = Transform()
+                j = i + 1
+                if j < len(layers) and isinstance(layers[j].spec, ActSpec):
+                    u.act = layers[j].spec
+                    j += 1
+                if j < len(layers) and isinstance(layers[j].spec, PoolSpec):
+                    u.pool = layers[j]
+                    j += 1
+                units.append(u)
+                i = j
+            elif isinstance(sp, DenseSpec):
+                units.append(Unit("dense", lp, in_tf=pending))
+                pending = Transform()
+                i += 1
+            elif isinstance(sp, NormSpec):
+                if pending.norm is not None or pending.act is not None:
+                    raise Unsupported("norm after norm/act")
+                if not lp.in_shape.is_spatial or not units or units[-1].kind != "conv":
+                    raise Unsupported("norm must follow a conv unit")
+                if lp.in_shape.c > 128:
+                    raise Unsupported("norm over > 128 channels")
+                pending.norm = lp
+                i += 1
+            elif isinstance(sp, ActSpec):
+                if pending.act is not None:
+                    raise Unsupported("two activations in a row")
+                pending.act = sp
+                _act_id(sp)
+                i += 1
+            elif isinstance(sp, PoolSpec):
+                raise Unsupported("pool not directly after a conv")
+            else:  # pragma: no cover
+                raise Unsupported(str(sp))
+        if pending.norm is not None:
+            raise Unsupported("norm directly before the head")
+        if not units:
+            raise Unsupported("no conv/dense layers")
+        self.units = units
+        self.head_tf = pending
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self) -> None:
+        dev, B = self.e.device, self.B
+        f32 = dict(device=dev, dtype=torch.float32)
+        prev: Optional[Unit] = None
+        for u in self.units:
+            u.x = prev.y if prev is not None else None
+            if prev is None and u.kind == "dense":
+                # first layer dense: materialise the gathered float input once per step
+                self.x_dense_in = torch.zeros(B, u.layer.in_shape.numel, **f32)
+                u.x = self.x_dense_in
+            lp = u.layer
+            if u.kind == "conv":
+                oh, ow = lp.out_shape.hw
+                if u.pool is not None:
+                    ph, pw = u.pool.out_shape.hw
+                    u.y = torch.zeros(B, ph, pw, lp.out_shape.c, **f32)
+                    u.argmax = torch.zeros(B, ph, pw, lp.out_shape.c, device=dev, dtype=torch.uint8)
+                else:
+                    u.y = torch.zeros(B, oh, ow, lp.out_shape.c, **f32)
+                u.dc = torch.zeros(B, oh, ow, lp.out_shape.c, **f32)
+            else:
+                u.y = torch.zeros(B, lp.spec.hidden, **f32)
+            u.dy = torch.zeros_like(u.y)
+            # forward BN slab for the transform consuming this unit's output
+            prev = u
+        # forward stat slabs: the unit BEFORE a transform with norm produces the slab
+        for k, u in enumerate(self.units):
+            tf = u.in_tf
+            if tf.has_bn:
+                src = self.units[k - 1]
+                ph, pw = src.y.shape[1], src.y.shape[2]
+                nslab = self.lib.csa_conv_fwd_nslab(self._conv_geom(src.layer, B), self._pool_geom(src))
+                tf.slab = torch.zeros(nslab, 2, src.y.shape[3], **f32)
+                tf.nslab = nslab
+                tf.count = float(B * ph * pw)
+                # backward slab is produced by THIS unit's dgrad
+                C = src.y.shape[3]
+                if u.kind == "dense":
+                    nb = self.lib.csa_dense_dgrad_slabs(B, u.layer.in_shape.numel, u.layer.spec.hidden)
+                else:
+                    nb = self.lib.csa_conv_dgrad_nslab(self._conv_geom(u.layer, B))
+                tf.bwd_slab = torch.zeros(nb, 2, C, **f32)
+                tf.bwd_nslab = nb
+        self.dlast = self.units[-1].dy     # head input grad
+        self.idx = None
+
+    def _collect_zero_regions(self) -> None:
+        B = self.B
+        regs = []
+        for k, u in enumerate(self.units):
+            lp = u.layer
+            if u.kind == "dense":
+                fin, fout = lp.in_shape.numel, lp.spec.hidden
+                u.splits_fwd = self.lib.csa_dense_fwd_splits(B, fout, fin)
+                if u.splits_fwd > 1:
+                    regs.append(u.y)
+                if k > 0:
+                    tfm = u.in_tf.has_bn or u.in_tf.act is not None
+                    if self.lib.csa_dense_dgrad_splits(B, fin, fout, int(tfm)) > 1:
+                        regs.append(self.units[k - 1].dy)
+                if self.lib.csa_dense_wgrad_splits(B, fin, fout) > 1:
+                    regs.append(self.gviews[f"{lp.name}.weight"].view(-1))
+                    regs.append(self.gviews[f"{lp.name}.bias"])
+            else:
+                regs.append(self.gviews[f"{lp.name}.weight"].view(-1))
+                if lp.spec.bias:
+                    regs.append(self.gviews[f"{lp.name}.bias"])
+                if u.pool is not None:
+                    pk, ps = u.pool.spec.kernel, u.pool.spec.stride
+                    if tuple(pk) != tuple(ps):
+                        regs.append(u.dc.view(-1))
+        for u in self.units:
+            if u.in_tf.has_bn:
+                regs.append(u.in_tf.slab.view(-1))          # forward stats (atomic rows)
+                if u.kind == "conv":
+                    regs.append(u.in_tf.bwd_slab.view(-1))  # conv dgrad folds rows atomically
+        self.zero_regions = regs
+        if len(regs) > 16:
+            raise Unsupported("too many accumulator regions")
+
+    def _zero_now(self) -> None:
+        for r in self.zero_regions:
+            r.zero_()
+
+    def reset_after_warmup(self) -> None:
+        self._zero_now()
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _conv_geom(lp: LayerPlan, B: int):
+        sp = lp.spec
+        h, w = lp.in_shape.hw
+        oh, ow = lp.out_shape.hw
+        return K.ints([B, h, w, lp.in_shape.c, sp.kh, sp.kw, sp.stride[0], sp.stride[1],
+                       lp.pads[0], lp.pads[2], oh, ow, sp.cout])
+
+    @staticmethod
+    def _pool_geom(u: Unit):
+        if u.pool is None:
+            return K.ints([0] * 9)
+        lp = u.pool
+        sp = lp.spec
+        oh, ow = lp.out_shape.hw
+        return K.ints([1, sp.kernel[0], sp.kernel[1], sp.stride[0], sp.stride[1],
+                       lp.pads[0], lp.pads[2], oh, ow])
+
+    def _bn_args(self, tf: Transform):
+        if not tf.has_bn:
+            return (None, 0, 0.0, 0.0, None, None)
+        name = tf.norm.name
+        return (K.ptr(tf.slab), tf.nslab, tf.count, float(tf.norm.spec.epsilon),
+                K.ptr(self.views[f"{name}.scale"]), K.ptr(self.views[f"{name}.offset"]))
+
+    def _bn_args_c(self, tf: Transform):
+        """BN args with the channel count (dense launchers: channel = feature % C)."""
+        a = self._bn_args(tf)
+        C_ = tf.slab.shape[2] if tf.has_bn else 0
+        return (a[0], a[1], C_, a[2], a[3], a[4], a[5])
+
+    def _rc(self, rc: int, what: str) -> int:
+        if rc < 0 or (rc > 0 and not what.startswith("slabs:")):
+            raise RuntimeError(f"{what} failed: {rc}")
+        return rc
+
+    # ------------------------------------------------------------------ the step
+    def run(self) -> None:
+        e, lib, B = self.e, self.lib, self.B
+        st = K.stream()
+        idx = e.stream.current()          # [B] int64 dataset rows of this step
+        self.idx = idx
+        img = e.data.images
+        V, G = self.views, self.gviews
+
+        # ---------------- forward ----------------
+        for k, u in enumerate(self.units):
+            lp, tf = u.layer, u.in_tf
+            bn = self._bn_args(tf)
+            in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
+            next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
+            if u.kind == "conv":
+                oslab = next_tf.slab if next_tf.has_bn else None
+                raw = u.x is None
+                self._rc(lib.csa_conv_fwd(
+                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(idx) if raw else None,
+                    K.ptr(V[f"{lp.name}.weight"]), K.ptr(V.get(f"{lp.name}.bias")) if lp.spec.bias else None,
+                    K.ptr(u.y), K.ptr(u.argmax), K.ptr(oslab),
+                    self._conv_geom(lp, B), self._pool_geom(u), *bn, in_act, in_alpha,
+                    _act_id(u.act), _alpha(u.act), st), "conv_fwd")
+            else:
+                if u.x is self.__dict__.get("x_dense_in"):
+                    self.x_dense_in.copy_(img.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
+                fin, fout = lp.in_shape.numel, lp.spec.hidden
+                self._rc(lib.csa_dense_fwd(
+                    K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
+                    B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
+
+        # ---------------- head (loss, head grads, input grad, metrics) ----------------
+        last = self.units[-1]
+        hin = last.y.view(B, -1)
+        self._rc(lib.csa_head(
+            K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
+            K.ptr(V["head.weight"]), K.ptr(V["head.bias"]), K.ptr(e.data.labels), K.ptr(idx),
+            0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
+            K.ptr(G["head.weight"]), K.ptr(G["head.bias"]), K.ptr(last.dy), None,
+            K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(), st), "head")
+
+        # ---------------- backward ----------------
+        for k in range(len(self.units) - 1, -1, -1):
+            u = self.units[k]
+            lp, tf = u.layer, u.in_tf
+            bn = self._bn_args(tf)
+            in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
+            prev = self.units[k - 1] if k > 0 else None
+            if u.kind == "dense":
+                fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if prev is not None:
+                    xf = u.x.view(B, -1)
+                    self._rc(lib.csa_dense_dgrad(
+                        K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
+                        K.ptr(xf), in_act, in_alpha, *self._bn_args_c(tf), K.ptr(tf.bwd_slab), st),
+                        "slabs:dense_dgrad")
+                self._rc(lib.csa_dense_wgrad(
+                    K.ptr(u.x), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+                    B, fin, fout, *self._bn_args_c(tf), in_act, in_alpha, 1.0, st), "dense_wgrad")
+            else:
+                # output side: (BN backward of the NEXT transform) + act backward + pool routing
+                next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
+                need_route = next_tf.has_bn or u.act is not None or u.pool is not None
+                if need_route:
+                    oh, ow = lp.out_shape.hw
+                    g = [B, u.y.shape[1], u.y.shape[2], u.y.shape[3], oh, ow,
+                         1 if u.pool is not None else 0]
+                    if u.pool is not None:
+                        ps = u.pool.spec
+                        g += [ps.kernel[0], ps.kernel[1], ps.stride[0], ps.stride[1],
+                              u.pool.pads[0], u.pool.pads[2]]
+                    else:
+                        g += [1, 1, 1, 1, 0, 0]
+                    nbn = self._bn_args(next_tf)
+                    dsc = G[f"{next_tf.norm.name}.scale"] if next_tf.has_bn else None
+                    dof = G[f"{next_tf.norm.name}.offset"] if next_tf.has_bn else None
+                    rm = rv = None
+                    if next_tf.has_bn:
+                        rm = getattr(self.model, f"bn{next_tf.norm.index}_mean")
+                        rv = getattr(self.model, f"bn{next_tf.norm.index}_var")
+                    self._rc(lib.csa_route_bwd(
+                        K.ptr(u.dy), K.ptr(u.y), K.ptr(u.argmax), K.ptr(u.dc), K.ints(g),
+                        _act_id(u.act), _alpha(u.act), *nbn, K.ptr(next_tf.bwd_slab), next_tf.bwd_nslab,
+                        K.ptr(dsc), K.ptr(dof), K.ptr(rm), K.ptr(rv), float(self.model.bn_momentum), st),
+                        "route_bwd")
+                    dc = u.dc
+                else:
+                    dc = u.dy
+                geom = self._conv_geom(lp, B)
+                raw = u.x is None
+                sp = lp.spec
+                h, w = lp.in_shape.hw
+                oh, ow = lp.out_shape.hw
+                self._rc(lib.csa_conv_wgrad(
+                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(idx) if raw else None,
+                    K.ptr(dc), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]) if sp.bias else None,
+                    B, h, w, lp.in_shape.c, sp.kh, sp.kw, sp.stride[0], sp.stride[1], lp.pads[0], lp.pads[2],
+                    oh, ow, sp.cout, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], in_act, in_alpha, st),
+                    "conv_wgrad")
+                if prev is not None:
+                    self._rc(lib.csa_conv_dgrad(
+                        K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
+                        K.ptr(u.x), in_act, in_alpha, *bn, K.ptr(tf.bwd_slab), st), "conv_dgrad")
+
+        # ---------------- gradient sync + optimizer ----------------
+        e.after_backward_sync()
+        self._optimizer(st)
+
+    def _optimizer(self, st) -> None:
+        e, lib = self.e, self.lib
+        lo, hi = e.sync.shard_range()
+        if e.sync.strategy == "ps" and e.ctx.enabled:
+            w, g = e.flat[lo:hi], e.grad_shard
+        else:
+            w, g = e.flat, e.flat_grad
+        s0 = e.slots[0] if e.slots.shape[0] > 0 else None
+        s1 = e.slots[1] if e.slots.shape[0] > 1 else None
+        zp = (C.c_void_p * 16)(*[r.data_ptr() for r in self.zero_regions])
+        zn = (C.c_long * 16)(*[r.numel() for r in self.zero_regions])
+        bns = []   # BN running statistics are updated by csa_route_bwd (block 0)
+        nb = len(bns)
+        slabs = (C.c_void_p * 8)(*[tf.slab.data_ptr() for tf, _ in bns])
+        nsl = (C.c_int * 8)(*[tf.nslab for tf, _ in bns])
+        cs = (C.c_int * 8)(*[tf.slab.shape[2] for tf, _ in bns])
+        cnt = (C.c_float * 8)(*[tf.count for tf, _ in bns])
+        rm = (C.c_void_p * 8)(*[getattr(self.model, f"bn{tf.norm.index}_mean").data_ptr() for tf, _ in bns])
+        rv = (C.c_void_p * 8)(*[getattr(self.model, f"bn{tf.norm.index}_var").data_ptr() for tf, _ in bns])
+        self._rc(lib.csa_optimizer(
+            e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), float(e.lr), K.ptr(e.dstep),
+            zp, zn, len(self.zero_regions), slabs, nsl, cs, cnt, rm, rv, float(self.model.bn_momentum), nb, st),
+            "optimizer")
+        if e.sync.strategy == "ps" and e.ctx.enabled:
+            e.sync.all_gather_params(e.flat)
