@@ -19,7 +19,7 @@ enum Act : int { ACT_NONE = 0, ACT_SIGMOID = 1, ACT_RELU = 2, ACT_LEAKY = 3 };
 
 __device__ __forceinline__ float act_fwd(float x, int act, float alpha) {
   switch (act) {
-    case ACT_SIGMOID: return 1.0f / (1.0f + __expf(-x));
+    case ACT_SIGMOID: return __builtin_amdgcn_rcpf(1.0f + __expf(-x));   // v_exp + v_rcp
     case ACT_RELU: return x > 0.f ? x : 0.f;
     case ACT_LEAKY: return fmaxf(x, alpha * x);  // tf.maximum(x, a*x)
     default: return x;
@@ -53,6 +53,28 @@ struct FastDiv {
     r = x - q * d;
   }
 };
+
+// Block-cooperative copy global -> LDS with a per-element transform, issuing UNROLL
+// independent loads per thread before any store (branch-free clamped addresses), so a
+// thread waits for one memory round trip per UNROLL elements instead of one per element
+// (hipcc otherwise emits load -> s_waitcnt vmcnt(0) -> store for every iteration).
+template <int UNROLL, class T, class F>
+__device__ __forceinline__ void stage_to_lds(float* dst, const T* src, int n, F f) {
+  const int step = blockDim.x * UNROLL;
+  for (int base = 0; base < n; base += step) {
+    T v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int i = base + u * blockDim.x + threadIdx.x;
+      v[u] = src[i < n ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int i = base + u * blockDim.x + threadIdx.x;
+      if (i < n) dst[i] = f(v[u], i);
+    }
+  }
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

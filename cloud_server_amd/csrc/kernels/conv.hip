@@ -38,7 +38,8 @@ struct ConvFwdArgs {
   int nslab;                   // BN slab rows (workgroups fold into blockIdx % nslab)
   const float* x;              // fp32 NHWC input (or null)
   const uint8_t* img;          // uint8 dataset [N][H*W*Cin] (first layer) ...
-  const int64_t* idx;          // ... gathered through idx[b]
+  const int64_t* idx;          // ... gathered through idx[b] (rows of the index stream)
+  const int64_t* cursor;       // if set: this step's row = idx + cursor[0] * B
   BNRef in_bn; int in_bn_on; int in_act; float in_alpha;   // input transform
   const float* w; const float* bias; int out_act; float out_alpha;
   float* y;                    // [B, OH|POH, OW|POW, Cout] post-act (post-pool) output
@@ -73,20 +74,23 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_fwd_kernel(ConvFwdArgs a) {
 
   if (a.in_bn_on) bn_reduce_to_lds(a.in_bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
   for (int i = threadIdx.x; i < 2 * g.Cout; i += blockDim.x) s_stat[i] = 0.f;
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) s_w[i] = a.w[i];
+  stage_to_lds<4>(s_w, a.w, nw, [](float v, int) { return v; });
   if (U8) {
-    const uint8_t* src = a.img + a.idx[b] * (long)(g.H * rowlen) + (long)y0 * rowlen;
-    for (int i = threadIdx.x; i < nin; i += blockDim.x) s_in[i] = (float)src[i] * (1.0f / 255.0f);
+    const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * g.B : a.idx;
+    const uint8_t* src = a.img + idx[b] * (long)(g.H * rowlen) + (long)y0 * rowlen;
+    stage_to_lds<8>(s_in, src, nin, [](uint8_t v, int) { return (float)v * (1.0f / 255.0f); });
   } else {
     __syncthreads();   // BN tables ready
     const float* src = a.x + ((long)b * g.H + y0) * rowlen;
     const float* ta = s_bn + 256;
     const float* tb = s_bn + 384;
-    for (int i = threadIdx.x; i < nin; i += blockDim.x) {
-      float v = src[i];
-      if (a.in_bn_on) { const int ci = i % g.Cin; v = v * ta[ci] + tb[ci]; }
-      s_in[i] = act_fwd(v, a.in_act, a.in_alpha);
-    }
+    const FastDiv dc(g.Cin);
+    const int bn_on = a.in_bn_on, act = a.in_act;
+    const float alpha = a.in_alpha;
+    stage_to_lds<8>(s_in, src, nin, [&](float v, int i) {
+      if (bn_on) { int q, ci; dc.divmod(i, q, ci); v = v * ta[ci] + tb[ci]; }
+      return act_fwd(v, act, alpha);
+    });
   }
   __syncthreads();
 
@@ -123,11 +127,26 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_fwd_kernel(ConvFwdArgs a) {
           if (xx < 0 || xx >= g.W) continue;
           const float* in = s_in + (yy - y0) * rowlen + xx * g.Cin;
           const float* wr = s_w + (i * g.KW + j) * g.Cin * g.Cout + co0;
-          for (int ci = 0; ci < g.Cin; ++ci) {
+          // 4 input channels per step: all 4 + 4*CB LDS reads issue before the FMAs
+          // (a runtime-bound loop otherwise waits on every ds_read).
+          int ci = 0;
+          for (; ci + 4 <= g.Cin; ci += 4) {
+            float v[4], w[4][CB];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              v[u] = in[ci + u];
+#pragma unroll
+              for (int c = 0; c < CB; ++c) w[u][c] = wr[(ci + u) * g.Cout + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int c = 0; c < CB; ++c) acc[c] = fmaf(v[u], w[u][c], acc[c]);
+          }
+          for (; ci < g.Cin; ++ci) {
             const float v = in[ci];
 #pragma unroll
-            for (int c = 0; c < CB; ++c)
-              if (c < nco) acc[c] = fmaf(v, wr[ci * g.Cout + c], acc[c]);
+            for (int c = 0; c < CB; ++c) acc[c] = fmaf(v, wr[ci * g.Cout + c], acc[c]);
           }
         }
       }
@@ -268,10 +287,10 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs 
   float* s_w = smem + ((a.band_rows_in * rowlen + 3) & ~3);
   if (a.in_bn_on) bn_reduce_to_lds(a.in_bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
   for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) s_stat[i] = 0.f;
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) s_w[i] = a.w[i];
+  stage_to_lds<4>(s_w, a.w, nw, [](float v, int) { return v; });
   const int nd = max(0, o1 - o0) * rowlen;
   const float* src = a.dc + ((long)b * g.OH + o0) * rowlen;
-  for (int i = threadIdx.x; i < nd; i += blockDim.x) s_dc[i] = src[i];
+  stage_to_lds<8>(s_dc, src, nd, [](float v, int) { return v; });
   __syncthreads();
 
   const int npix = (y1 - y0) * g.W;
@@ -299,11 +318,24 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs 
         if (ox >= g.OW) continue;
         const float* drow = s_dc + (oy - o0) * rowlen + ox * g.Cout;
         const float* wbase = s_w + ((i * g.KW + j) * g.Cin + ci0) * g.Cout;
-        for (int co = 0; co < g.Cout; ++co) {
+        int co = 0;
+        for (; co + 4 <= g.Cout; co += 4) {
+          float gv[4], w[CB][4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            gv[u] = drow[co + u];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) w[c][u] = wbase[c * g.Cout + co + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[c] = fmaf(gv[u], w[c][u], acc[c]);
+        }
+        for (; co < g.Cout; ++co) {
           const float gv = drow[co];
 #pragma unroll
-          for (int c = 0; c < CB; ++c)
-            if (c < nci) acc[c] = fmaf(gv, wbase[c * g.Cout + co], acc[c]);
+          for (int c = 0; c < CB; ++c) acc[c] = fmaf(gv, wbase[c * g.Cout + co], acc[c]);
         }
       }
     }
@@ -394,8 +426,10 @@ CSA_API int csa_conv_fwd(const float* x, const uint8_t* img, const int64_t* idx,
                          const int* geom /*13*/, const int* pool /*9*/, const float* in_bn_slab,
                          int in_bn_nslab, float in_bn_count, float in_bn_eps,
                          const float* in_bn_scale, const float* in_bn_offset, int in_act,
-                         float in_alpha, int out_act, float out_alpha, hipStream_t st) {
+                         float in_alpha, int out_act, float out_alpha, const int64_t* cursor,
+                         hipStream_t st) {
   ConvFwdArgs a{};
+  a.cursor = cursor;
   a.g = geom_from(geom);
   a.pool = PoolGeom{pool[0], pool[1], pool[2], pool[3], pool[4], pool[5], pool[6], pool[7], pool[8]};
   if (a.g.Cin > 128 || a.g.Cout > 128) return -1;

@@ -17,6 +17,7 @@
 //   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
 //   D: reg r of lane l is D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31]
 #include "common.h"
+#include <type_traits>
 
 namespace csa {
 
@@ -30,41 +31,75 @@ constexpr int MAXC = 128;     // max BatchNorm channels handled in LDS
 struct BNTables { const float *mean, *rstd, *a, *b; };
 
 // ----------------------------------------------------------------------------------
-// Loaders: value(r, c) with r the "outer" index (m for A, n for B) and c the K index.
+// Loaders: element (r, c) with r the "outer" index (m for A, n for B), c the K index.
+// Split in two so the staging loop stays branch-free around memory:
+//   raw(r, c)      -> issues ONE load from a clamped address (no branch around it),
+//   post(v, r, c)  -> validity select + transform (BN-apply, activation, /255) applied
+//                     when the chunk is committed to LDS, i.e. after the loads of the
+//                     whole chunk are in flight (hipcc otherwise waits vmcnt(0) per load).
 // KCONTIG says whether consecutive K are contiguous in memory (picks the lane mapping).
 // ----------------------------------------------------------------------------------
+template <bool V4 = false>
 struct LoadRowMajor {          // elem(r, c) = p[r * ld + c]
   const float* p; long ld; int rows, cols;
   static constexpr bool KCONTIG = true;
-  __device__ void bind(const BNTables&) {}
-  __device__ float operator()(int r, int c) const {
-    return (r < rows && c < cols) ? p[(long)r * ld + c] : 0.f;
+  static constexpr bool VEC4 = V4;   // ld % 4 == 0 && cols % 4 == 0 (launcher checks)
+  __device__ float4 raw4(int r, int c) const {   // (r, c..c+3), c % 4 == 0
+    const int rr = r < rows ? r : 0;
+    const int cc = min(c, cols - 4);
+    return *reinterpret_cast<const float4*>(p + (long)rr * ld + cc);
   }
+  __device__ void bind(const BNTables&) {}
+  __device__ float raw(int r, int c) const {
+    const bool ok = r < rows && c < cols;
+    return p[ok ? (long)r * ld + c : 0];
+  }
+  __device__ float post(float v, int r, int c) const { return (r < rows && c < cols) ? v : 0.f; }
 };
 
+template <bool V4 = false>
 struct LoadColMajor {          // elem(r, c) = p[c * ld + r]
   const float* p; long ld; int rows, cols;
   static constexpr bool KCONTIG = false;
-  __device__ void bind(const BNTables&) {}
-  __device__ float operator()(int r, int c) const {
-    return (r < rows && c < cols) ? p[(long)c * ld + r] : 0.f;
+  static constexpr bool VEC4 = V4;   // ld % 4 == 0 && rows % 4 == 0
+  __device__ float4 raw4(int r, int c) const {   // (r..r+3, c), r % 4 == 0
+    const int rr = min(r, rows - 4);
+    const int cc = c < cols ? c : 0;
+    return *reinterpret_cast<const float4*>(p + (long)cc * ld + rr);
   }
+  __device__ void bind(const BNTables&) {}
+  __device__ float raw(int r, int c) const {
+    const bool ok = r < rows && c < cols;
+    return p[ok ? (long)c * ld + r : 0];
+  }
+  __device__ float post(float v, int r, int c) const { return (r < rows && c < cols) ? v : 0.f; }
 };
 
 // Activation tensor X[m][f] read through an optional BN-apply (channel = f % C) and act.
 // ROWS_ARE_BATCH: elem(r=m, c=f) (dense fwd A);  else elem(r=f, c=m) (dense wgrad A).
 // ones_row: for wgrad, row f == feat returns 1 (m < batch) -> bias gradient row.
-template <bool ROWS_ARE_BATCH>
+template <bool ROWS_ARE_BATCH, bool V4 = false>
 struct LoadBNAct {
   const float* x; long ld; int batch, feat; FastDiv C; int act; float alpha; int has_bn, ones_row;
   const float* ta; const float* tb;
   static constexpr bool KCONTIG = ROWS_ARE_BATCH;
-  __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
-  __device__ float operator()(int r, int c) const {
+  static constexpr bool VEC4 = V4;   // ld % 4 == 0 && feat % 4 == 0
+  __device__ float4 raw4(int r, int c) const {   // 4 consecutive features of one row m
     int m = ROWS_ARE_BATCH ? r : c, f = ROWS_ARE_BATCH ? c : r;
+    m = m < batch ? m : 0;
+    f = min(f, feat - 4);
+    return *reinterpret_cast<const float4*>(x + (long)m * ld + f);
+  }
+  __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
+  __device__ float raw(int r, int c) const {
+    const int m = ROWS_ARE_BATCH ? r : c, f = ROWS_ARE_BATCH ? c : r;
+    const bool ok = m < batch && f < feat;
+    return x[ok ? (long)m * ld + f : 0];
+  }
+  __device__ float post(float v, int r, int c) const {
+    const int m = ROWS_ARE_BATCH ? r : c, f = ROWS_ARE_BATCH ? c : r;
     if (m >= batch) return 0.f;
     if (f >= feat) return (ones_row && f == feat) ? 1.f : 0.f;
-    float v = x[(long)m * ld + f];
     if (has_bn) { int q, ch; C.divmod(f, q, ch); v = v * ta[ch] + tb[ch]; }
     return act_fwd(v, act, alpha);
   }
@@ -80,21 +115,44 @@ struct LoadIm2colT {
   int B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, ones_row, has_bn, act; float alpha;
   FastDiv dCin, dKW, dOW, dOH;
   const float* ta; const float* tb;
+  const int64_t* cursor;   // if set: idx += cursor[0] * B (resolved in-kernel by bind)
   static constexpr bool KCONTIG = false;
-  __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
-  __device__ float operator()(int r, int c) const {
+  static constexpr bool VEC4 = false;
+  __device__ float4 raw4(int, int) const { return float4{0.f, 0.f, 0.f, 0.f}; }
+  __device__ void bind(const BNTables& t) {
+    ta = t.a; tb = t.b;
+    if (U8 && cursor) { idx += cursor[0] * B; cursor = nullptr; }
+  }
+  // Branch-free address computation; ok = false for padding / out of range.
+  __device__ long offset(int r, int c, int& ci, bool& ok) const {
     const int kc = KH * KW * Cin, P = B * OH * OW;
-    if (c >= P) return 0.f;
-    if (r >= kc) return (ones_row && r == kc) ? 1.f : 0.f;
-    int t, ci, i, j, t2, ox, b, oy;
-    dCin.divmod(r, t, ci);
+    const int rr = min(r, kc - 1), cc = min(c, P - 1);
+    int t, i, j, t2, ox, b, oy;
+    dCin.divmod(rr, t, ci);
     dKW.divmod(t, i, j);
-    dOW.divmod(c, t2, ox);
+    dOW.divmod(cc, t2, ox);
     dOH.divmod(t2, b, oy);
-    int y = oy * SH - PT + i, xx = ox * SW - PL + j;
-    if (y < 0 || y >= H || xx < 0 || xx >= W) return 0.f;
-    if (U8) return (float)img[idx[b] * (long)(H * W * Cin) + ((long)y * W + xx) * Cin + ci] * (1.0f / 255.0f);
-    float v = x[(((long)b * H + y) * W + xx) * Cin + ci];
+    const int y = oy * SH - PT + i, xx = ox * SW - PL + j;
+    ok = (c < P) && (r < kc) && y >= 0 && y < H && xx >= 0 && xx < W;
+    const long pix = ((long)(ok ? y : 0) * W + (ok ? xx : 0)) * Cin + ci;
+    if (U8) return idx[b] * (long)(H * W * Cin) + pix;   // idx[b] always in range
+    return (long)b * H * W * Cin + pix;
+  }
+  __device__ float raw(int r, int c) const {
+    int ci;
+    bool ok;
+    const long o = offset(r, c, ci, ok);
+    if (U8) return (float)img[o];
+    return x[o];
+  }
+  __device__ float post(float v, int r, int c) const {
+    const int kc = KH * KW * Cin;
+    if (r >= kc) return (ones_row && r == kc && c < B * OH * OW) ? 1.f : 0.f;
+    int ci;
+    bool ok;
+    (void)offset(r, c, ci, ok);
+    if (!ok) return 0.f;
+    if (U8) return v * (1.0f / 255.0f);
     if (has_bn) v = v * ta[ci] + tb[ci];
     return act_fwd(v, act, alpha);
   }
@@ -145,6 +203,60 @@ struct EpiActBNBwd {
 };
 
 // ----------------------------------------------------------------------------------
+// Per-wave staging of one operand tile (32 outer rows x KC) into LDS [kk][r] (pad 33).
+// Scalar path: PER branch-free loads per lane.  VEC4 path: 2 float4 loads per lane
+// along the operand's contiguous dimension.  fetch() only issues loads; commit()
+// applies validity + transform and writes LDS (after the loads had a chunk to land).
+// ----------------------------------------------------------------------------------
+template <class L>
+struct Stage {
+  static constexpr int PER = (32 * KC) / 64;
+  static constexpr int NV = L::VEC4 ? PER / 4 : PER;
+  int ro[NV], ko[NV];
+  float v[PER];
+  __device__ void init(int lane) {
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      const int idx = lane + 64 * e;
+      if (L::VEC4) {
+        if (L::KCONTIG) { ro[e] = idx >> 2; ko[e] = (idx & 3) * 4; }
+        else { ko[e] = idx >> 3; ro[e] = (idx & 7) * 4; }
+      } else {
+        if (L::KCONTIG) { ro[e] = idx / KC; ko[e] = idx % KC; }
+        else { ko[e] = idx / 32; ro[e] = idx % 32; }
+      }
+    }
+  }
+  __device__ void fetch(const L& l, int r0, int k, int ke) {
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      if (L::VEC4) {
+        const int kk = L::KCONTIG ? min(k + ko[e], ke - 4) : min(k + ko[e], ke - 1);
+        const float4 q = l.raw4(r0 + ro[e], kk);
+        v[4 * e] = q.x; v[4 * e + 1] = q.y; v[4 * e + 2] = q.z; v[4 * e + 3] = q.w;
+      } else {
+        v[e] = l.raw(r0 + ro[e], min(k + ko[e], ke - 1));
+      }
+    }
+  }
+  __device__ void commit(const L& l, float* dst, int r0, int k, int ke) const {
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      if (L::VEC4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = L::KCONTIG ? ro[e] : ro[e] + u;
+          const int kk = L::KCONTIG ? ko[e] + u : ko[e];
+          dst[kk * LDS_PAD + r] = (k + kk < ke) ? l.post(v[4 * e + u], r0 + r, k + kk) : 0.f;
+        }
+      } else {
+        dst[ko[e] * LDS_PAD + ro[e]] = (k + ko[e] < ke) ? l.post(v[e], r0 + ro[e], k + ko[e]) : 0.f;
+      }
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------------
 // The kernel.  Grid: x = N tiles, y = M tiles, z = split-K slices.
 // WG tile = (32*WM) x (32*WN); its K slice is split WK ways across the waves.
 // ----------------------------------------------------------------------------------
@@ -190,33 +302,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
 
   float* sa = s_stage[wave][0];
   float* sb = s_stage[wave][1];
-  // lane -> (row, kk) maps per operand
-  int ra_[PER], ka_[PER], rb_[PER], kb_[PER];
-#pragma unroll
-  for (int e = 0; e < PER; ++e) {
-    const int idx = lane + 64 * e;
-    if (LA::KCONTIG) { ra_[e] = idx / KC; ka_[e] = idx % KC; } else { ka_[e] = idx / 32; ra_[e] = idx % 32; }
-    if (LB::KCONTIG) { rb_[e] = idx / KC; kb_[e] = idx % KC; } else { kb_[e] = idx / 32; rb_[e] = idx % 32; }
-  }
-  float va[PER], vb[PER];
-  auto fetch = [&](int k) {
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      va[e] = (k + ka_[e] < ke) ? la(m0 + ra_[e], k + ka_[e]) : 0.f;
-      vb[e] = (k + kb_[e] < ke) ? lb(n0 + rb_[e], k + kb_[e]) : 0.f;
-    }
-  };
-  if (kb < ke) fetch(kb);
+  // Each operand tile (32 rows x KC) is PER scalar or PER/4 float4 loads per lane.
+  Stage<LA> stA;
+  Stage<LB> stB;
+  stA.init(lane);
+  stB.init(lane);
+  if (kb < ke) { stA.fetch(la, m0, kb, ke); stB.fetch(lb, n0, kb, ke); }
   for (int k = kb; k < ke; k += KC) {
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      sa[ka_[e] * LDS_PAD + ra_[e]] = va[e];
-      sb[kb_[e] * LDS_PAD + rb_[e]] = vb[e];
-    }
+    stA.commit(la, sa, m0, k, ke);
+    stB.commit(lb, sb, n0, k, ke);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (k + KC < ke) fetch(k + KC);     // next chunk's global loads fly under the MFMAs
+    if (k + KC < ke) {   // next chunk's global loads fly under the MFMAs
+      stA.fetch(la, m0, k + KC, ke);
+      stB.fetch(lb, n0, k + KC, ke);
+    }
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 2) {
       float av = sa[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
@@ -299,6 +400,18 @@ static int launch_gemm(const Plan& p, LA la, LB lb, EPI epi, int M, int N, int K
   return (int)hipGetLastError();
 }
 
+// Call f(std::integral_constant<bool, a>, std::integral_constant<bool, b>) — picks the
+// float4 loader instantiations when the operands' strides allow it.
+template <class F>
+static int dispatch2(bool a, bool b, F f) {
+  using T = std::true_type;
+  using Fl = std::false_type;
+  if (a && b) return f(T{}, T{});
+  if (a) return f(T{}, Fl{});
+  if (b) return f(Fl{}, T{});
+  return f(Fl{}, Fl{});
+}
+
 static BNRef make_bn(const float* slab, int nslab, int C, float count, float eps,
                      const float* scale, const float* offset) {
   return BNRef{slab, nslab, C, count, eps, scale, offset};
@@ -323,11 +436,13 @@ CSA_API int csa_dense_fwd(const float* X, const float* W, const float* bias, flo
   if (bn_slab && bn_C > MAXC) return -1;
   Plan p = plan_gemm(M, N, K, true);
   BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
-  LoadBNAct<true> la{X, (long)K, M, K, FastDiv(bn_C > 0 ? bn_C : 1), in_act, in_alpha, bn_slab != nullptr, 0,
-                     nullptr, nullptr};
-  LoadColMajor lb{W, (long)N, N, K};          // B(k, n) = W[k][n]
   EpiStore epi{Y, (long)N, M, N, bias, p.splits > 1, nullptr, 1.f};
-  return launch_gemm(p, la, lb, epi, M, N, K, bn, bn_slab != nullptr, nullptr, 0, st);
+  return dispatch2(K % 4 == 0 && K >= 4, N % 4 == 0 && N >= 4, [&](auto va, auto vb) {
+    LoadBNAct<true, decltype(va)::value> la{X, (long)K, M, K, FastDiv(bn_C > 0 ? bn_C : 1), in_act,
+                                             in_alpha, bn_slab != nullptr, 0, nullptr, nullptr};
+    LoadColMajor<decltype(vb)::value> lb{W, (long)N, N, K};          // B(k, n) = W[k][n]
+    return launch_gemm(p, la, lb, epi, M, N, K, bn, bn_slab != nullptr, nullptr, 0, st);
+  });
 }
 
 // dX[M][Kin] = dY[M][Nout] @ W[Kin][Nout]^T, then (optionally) through the forward
@@ -343,18 +458,19 @@ CSA_API int csa_dense_dgrad(const float* dY, const float* W, float* dX, int M, i
   const bool transform = (act != ACT_NONE) || (bn_slab != nullptr);
   Plan p = plan_gemm(M, Kin, Nout, !transform);
   BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
-  LoadRowMajor la{dY, (long)Nout, M, Nout};   // A(m, k=n) = dY[m][n]
-  LoadRowMajor lb{W, (long)Nout, Kin, Nout};  // B(k=n, j) = W[j][n]
-  int rc;
-  if (transform) {
-    EpiActBNBwd epi{dX, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), x_fwd, act, alpha,
-                    bn_slab != nullptr, BNTables{}};
-    rc = launch_gemm(p, la, lb, epi, M, Kin, Nout, bn, bn_slab != nullptr,
-                     bn_slab ? bwd_slab : nullptr, bn_C, st);
-  } else {
+  const bool v4 = Nout % 4 == 0 && Nout >= 4;
+  int rc = dispatch2(v4, v4, [&](auto va, auto vb) {
+    LoadRowMajor<decltype(va)::value> la{dY, (long)Nout, M, Nout};   // A(m, k=n) = dY[m][n]
+    LoadRowMajor<decltype(vb)::value> lb{W, (long)Nout, Kin, Nout};  // B(k=n, j) = W[j][n]
+    if (transform) {
+      EpiActBNBwd epi{dX, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), x_fwd, act, alpha,
+                      bn_slab != nullptr, BNTables{}};
+      return launch_gemm(p, la, lb, epi, M, Kin, Nout, bn, bn_slab != nullptr,
+                         bn_slab ? bwd_slab : nullptr, bn_C, st);
+    }
     EpiStore epi{dX, (long)Kin, M, Kin, nullptr, p.splits > 1, nullptr, 1.f};
-    rc = launch_gemm(p, la, lb, epi, M, Kin, Nout, bn, 0, nullptr, 0, st);
-  }
+    return launch_gemm(p, la, lb, epi, M, Kin, Nout, bn, 0, nullptr, 0, st);
+  });
   if (rc) return -rc;
   return grid_slabs(p, M, Kin);
 }
@@ -382,11 +498,13 @@ CSA_API int csa_dense_wgrad(const float* X, const float* dY, float* dW, float* d
   const int Mg = Kin + (db ? 1 : 0);
   Plan p = plan_gemm(Mg, Nout, M, true);
   BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
-  LoadBNAct<false> la{X, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), in_act, in_alpha,
-                      bn_slab != nullptr, db != nullptr, nullptr, nullptr};
-  LoadColMajor lb{dY, (long)Nout, Nout, M};   // B(k=m, n) = dY[m][n]
   EpiStore epi{dW, (long)Nout, Kin, Nout, nullptr, p.splits > 1, db, scale};
-  return launch_gemm(p, la, lb, epi, Mg, Nout, M, bn, bn_slab != nullptr, nullptr, 0, st);
+  return dispatch2(Kin % 4 == 0 && Kin >= 4, Nout % 4 == 0 && Nout >= 4, [&](auto va, auto vb) {
+    LoadBNAct<false, decltype(va)::value> la{X, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), in_act,
+                                              in_alpha, bn_slab != nullptr, db != nullptr, nullptr, nullptr};
+    LoadColMajor<decltype(vb)::value> lb{dY, (long)Nout, Nout, M};   // B(k=m, n) = dY[m][n]
+    return launch_gemm(p, la, lb, epi, Mg, Nout, M, bn, bn_slab != nullptr, nullptr, 0, st);
+  });
 }
 
 // Conv weight gradient as implicit GEMM:  dW[(i,j,ci)][co] = sum_p im2col(x)[p][(i,j,ci)] dOut[p][co]
@@ -396,7 +514,8 @@ CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* id
                            float* dW, float* db, int B, int H, int W, int Cin, int KH, int KW, int SH,
                            int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
                            int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                           const float* bn_offset, int in_act, float in_alpha, hipStream_t st) {
+                           const float* bn_offset, int in_act, float in_alpha, const int64_t* cursor,
+                           hipStream_t st) {
   if (bn_slab && Cin > MAXC) return -1;
   const int kc = KH * KW * Cin;
   const int Mg = kc + (db ? 1 : 0);
@@ -404,16 +523,18 @@ CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* id
   Plan p = plan_gemm(Mg, Cout, P, true);
   // conv wgrad is always accumulated with atomics (split-K over pixels)
   BNRef bn = make_bn(bn_slab, bn_nslab, Cin, bn_count, bn_eps, bn_scale, bn_offset);
-  LoadColMajor lb{dOut, (long)Cout, Cout, P};  // B(k=p, co) = dOut[p][co]
   EpiStore epi{dW, (long)Cout, kc, Cout, nullptr, 1, db, 1.f};
+  return dispatch2(Cout % 4 == 0 && Cout >= 4, false, [&](auto vb, auto) {
+  LoadColMajor<decltype(vb)::value> lb{dOut, (long)Cout, Cout, P};  // B(k=p, co) = dOut[p][co]
   if (img) {
     LoadIm2colT<true> la{nullptr, img, idx, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW,
                          db != nullptr, 0, 0, 0.f, FastDiv(Cin), FastDiv(KW), FastDiv(OW), FastDiv(OH),
-                         nullptr, nullptr};
+                         nullptr, nullptr, cursor};
     return launch_gemm(p, la, lb, epi, Mg, Cout, P, bn, 0, nullptr, 0, st);
   }
   LoadIm2colT<false> la{x, nullptr, nullptr, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW,
                         db != nullptr, bn_slab != nullptr, in_act, in_alpha, FastDiv(Cin), FastDiv(KW),
-                        FastDiv(OW), FastDiv(OH), nullptr, nullptr};
+                        FastDiv(OW), FastDiv(OH), nullptr, nullptr, nullptr};
   return launch_gemm(p, la, lb, epi, Mg, Cout, P, bn, bn_slab != nullptr, nullptr, 0, st);
+  });
 }

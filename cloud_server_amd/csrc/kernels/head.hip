@@ -24,6 +24,7 @@ struct HeadArgs {
   const float* w; const float* b;          // [K][10], [10]
   const int64_t* labels;                   // dataset labels ...
   const int64_t* idx;                      // ... gathered through the batch index stream
+  const int64_t* cursor;                   // if set: this step's row = idx + cursor[0] * M
   int loss;                                // 0 = softmax xent, 1 = mse
   float grad_scale;
   float* dw; float* db; float* dh;         // grads (dh may be null)
@@ -40,10 +41,13 @@ __global__ __launch_bounds__(HT) void head_kernel(HeadArgs a) {
   float* s_w = s_red + 32;                      // [K][10]   (STAGED)
   float* s_h = s_w + a.K * NCLS;                // [M][K]    T(h) (STAGED)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = HT / 64;
+  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * a.M : a.idx;
   if (tid == 0) *s_cor = 0;
   if (STAGED) {
-    for (int e = tid; e < a.K * NCLS; e += HT) s_w[e] = a.w[e];
-    for (long e = tid; e < (long)a.M * a.K; e += HT) s_h[e] = act_fwd(a.h[e], a.in_act, a.in_alpha);
+    stage_to_lds<4>(s_w, a.w, a.K * NCLS, [](float v, int) { return v; });
+    const int act = a.in_act;
+    const float alpha = a.in_alpha;
+    stage_to_lds<8>(s_h, a.h, a.M * a.K, [&](float v, int) { return act_fwd(v, act, alpha); });
     __syncthreads();
   }
   auto TH = [&](int m, int k) -> float {
@@ -72,7 +76,7 @@ __global__ __launch_bounds__(HT) void head_kernel(HeadArgs a) {
   // 2) loss / dlogits / accuracy: one lane per row
   float lsum = 0.f;
   for (int m = tid; m < a.M; m += HT) {
-    const int y = (int)a.labels[a.idx[m]];
+    const int y = (int)a.labels[idx[m]];
     float* row = s_log + m * NCLS;
     float mx = row[0];
     int am = 0;
@@ -121,7 +125,15 @@ __global__ __launch_bounds__(HT) void head_kernel(HeadArgs a) {
   for (int e = tid; e < a.K * NCLS; e += HT) {
     const int k = e / NCLS, j = e % NCLS;
     float acc = 0.f;
-    for (int m = 0; m < a.M; ++m) acc = fmaf(TH(m, k), s_log[m * NCLS + j], acc);
+    int m = 0;
+    for (; m + 8 <= a.M; m += 8) {     // 16 LDS reads in flight per step
+      float hv[8], lv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { hv[u] = TH(m + u, k); lv[u] = s_log[(m + u) * NCLS + j]; }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = fmaf(hv[u], lv[u], acc);
+    }
+    for (; m < a.M; ++m) acc = fmaf(TH(m, k), s_log[m * NCLS + j], acc);
     a.dw[e] = acc;
   }
   if (tid < NCLS) {
@@ -137,8 +149,13 @@ __global__ __launch_bounds__(HT) void head_kernel(HeadArgs a) {
 #pragma unroll
       for (int j = 0; j < NCLS; ++j) acc = fmaf(s_log[m * NCLS + j], WW(k, j), acc);
       if (a.in_act) {
-        const float x = a.h[e];
-        acc = act_bwd(acc, x, STAGED ? s_h[e] : act_fwd(x, a.in_act, a.in_alpha), a.in_act, a.in_alpha);
+        if (STAGED) {   // post-activation value decides every supported derivative
+          const float y = s_h[e];
+          acc = act_bwd(acc, y, y, a.in_act, a.in_alpha);
+        } else {
+          const float x = a.h[e];
+          acc = act_bwd(acc, x, act_fwd(x, a.in_act, a.in_alpha), a.in_act, a.in_alpha);
+        }
       }
       a.dh[e] = acc;
     }
@@ -152,10 +169,11 @@ using namespace csa;
 CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
                      const float* b, const int64_t* labels, const int64_t* idx, int loss,
                      float grad_scale, float* dw, float* db, float* dh, float* logits_out,
-                     int64_t* step, float* ring_loss, int* ring_correct, int ring, hipStream_t st) {
+                     int64_t* step, float* ring_loss, int* ring_correct, int ring,
+                     const int64_t* cursor, hipStream_t st) {
   if (M <= 0 || M > 4096) return -1;
-  HeadArgs a{h, M, K, in_act, in_alpha, w, b, labels, idx, loss, grad_scale, dw, db, dh, logits_out,
-             step, ring_loss, ring_correct, ring};
+  HeadArgs a{h, M, K, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dw, db, dh,
+             logits_out, step, ring_loss, ring_correct, ring};
   const size_t base = ((size_t)M * NCLS + 32) * sizeof(float);
   const size_t staged = base + ((size_t)K * NCLS + (size_t)M * K) * sizeof(float);
   if (staged <= HEAD_LDS_MAX) {

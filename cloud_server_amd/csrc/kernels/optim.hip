@@ -29,6 +29,7 @@ struct OptArgs {
   int opt; float* w; const float* g; float* s0; float* s1; long n;
   float lr; const int64_t* step;   // 1-based step AFTER the head kernel's increment
   ZeroList z; BNRunList bn;
+  int64_t* cursor;                 // batch-stream cursor: += 1 at the end of the step
 };
 
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
@@ -95,6 +96,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const long n = a.z.n[z];
     for (long i = tid; i < n; i += nth) p[i] = 0.f;
   }
+  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) *a.cursor += 1;
   // BN running statistics (one block)
   if (blockIdx.x == gridDim.x - 1) {
     for (int r = 0; r < a.bn.count; ++r) {
@@ -123,9 +125,11 @@ CSA_API int csa_optimizer(int opt, float* w, const float* g, float* s0, float* s
                           const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
                           int nzero, const float* const* bn_slabs, const int* bn_nslab,
                           const int* bn_C, const float* bn_count, float* const* bn_rmean,
-                          float* const* bn_rvar, float momentum, int nbn, hipStream_t st) {
+                          float* const* bn_rvar, float momentum, int nbn, int64_t* cursor,
+                          hipStream_t st) {
   if (n % 4 || nzero > MAXZ || nbn > MAXBN) return -1;
   OptArgs a{};
+  a.cursor = cursor;
   a.opt = opt; a.w = w; a.g = g; a.s0 = s0; a.s1 = s1; a.n = n; a.lr = lr; a.step = step;
   a.z.count = nzero;
   for (int i = 0; i < nzero; ++i) { a.z.p[i] = zero_ptrs[i]; a.z.n[i] = zero_ns[i]; }

@@ -278,8 +278,12 @@ class HipProgram:
     def run(self) -> None:
         e, lib, B = self.e, self.lib, self.B
         st = K.stream()
-        idx = e.stream.current()          # [B] int64 dataset rows of this step
-        self.idx = idx
+        # this step's dataset rows = stream.rows[cursor]; the kernels resolve the cursor on
+        # device and the optimizer launch advances it (no torch index/add launches).
+        rows, cur = e.stream.rows, e.stream.cursor
+        if self.__dict__.get("x_dense_in") is not None:
+            idx = rows.index_select(0, cur).view(-1)
+            self.x_dense_in.copy_(e.data.images.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
         img = e.data.images
         V, G = self.views, self.gviews
 
@@ -293,14 +297,12 @@ class HipProgram:
                 oslab = next_tf.slab if next_tf.has_bn else None
                 raw = u.x is None
                 self._rc(lib.csa_conv_fwd(
-                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(idx) if raw else None,
+                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
                     K.ptr(V[f"{lp.name}.weight"]), K.ptr(V.get(f"{lp.name}.bias")) if lp.spec.bias else None,
                     K.ptr(u.y), K.ptr(u.argmax), K.ptr(oslab),
                     self._conv_geom(lp, B), self._pool_geom(u), *bn, in_act, in_alpha,
-                    _act_id(u.act), _alpha(u.act), st), "conv_fwd")
+                    _act_id(u.act), _alpha(u.act), K.ptr(cur) if raw else None, st), "conv_fwd")
             else:
-                if u.x is self.__dict__.get("x_dense_in"):
-                    self.x_dense_in.copy_(img.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
                 self._rc(lib.csa_dense_fwd(
                     K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
@@ -311,10 +313,11 @@ class HipProgram:
         hin = last.y.view(B, -1)
         self._rc(lib.csa_head(
             K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
-            K.ptr(V["head.weight"]), K.ptr(V["head.bias"]), K.ptr(e.data.labels), K.ptr(idx),
+            K.ptr(V["head.weight"]), K.ptr(V["head.bias"]), K.ptr(e.data.labels), K.ptr(rows),
             0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
             K.ptr(G["head.weight"]), K.ptr(G["head.bias"]), K.ptr(last.dy), None,
-            K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(), st), "head")
+            K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(),
+            K.ptr(cur), st), "head")
 
         # ---------------- backward ----------------
         for k in range(len(self.units) - 1, -1, -1):
@@ -369,11 +372,11 @@ class HipProgram:
                 h, w = lp.in_shape.hw
                 oh, ow = lp.out_shape.hw
                 self._rc(lib.csa_conv_wgrad(
-                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(idx) if raw else None,
+                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
                     K.ptr(dc), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]) if sp.bias else None,
                     B, h, w, lp.in_shape.c, sp.kh, sp.kw, sp.stride[0], sp.stride[1], lp.pads[0], lp.pads[2],
-                    oh, ow, sp.cout, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], in_act, in_alpha, st),
-                    "conv_wgrad")
+                    oh, ow, sp.cout, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], in_act, in_alpha,
+                    K.ptr(cur) if raw else None, st), "conv_wgrad")
                 if prev is not None:
                     self._rc(lib.csa_conv_dgrad(
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
@@ -404,7 +407,7 @@ class HipProgram:
         rv = (C.c_void_p * 8)(*[getattr(self.model, f"bn{tf.norm.index}_var").data_ptr() for tf, _ in bns])
         self._rc(lib.csa_optimizer(
             e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), float(e.lr), K.ptr(e.dstep),
-            zp, zn, len(self.zero_regions), slabs, nsl, cs, cnt, rm, rv, float(self.model.bn_momentum), nb, st),
-            "optimizer")
+            zp, zn, len(self.zero_regions), slabs, nsl, cs, cnt, rm, rv, float(self.model.bn_momentum), nb,
+            K.ptr(e.stream.cursor), st), "optimizer")
         if e.sync.strategy == "ps" and e.ctx.enabled:
             e.sync.all_gather_params(e.flat)
