@@ -23,9 +23,10 @@ namespace csa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int KC = 16;        // K chunk staged per iteration (8 MFMAs)
+constexpr int KC = 64;        // K chunk staged per iteration (32 MFMAs); most waves need 1-2
 constexpr int LDS_PAD = 33;   // row stride of the 32-wide staging tiles (conflict-free)
 constexpr int MAXC = 128;     // max BatchNorm channels handled in LDS
+constexpr int KTAB = 512;     // max K slice per workgroup for table-driven loaders (im2col)
 
 // LDS tables shared by loaders/epilogues: [mean | rstd | a | b] x MAXC
 struct BNTables { const float *mean, *rstd, *a, *b; };
@@ -49,6 +50,7 @@ struct LoadRowMajor {          // elem(r, c) = p[r * ld + c]
     const int cc = min(c, cols - 4);
     return *reinterpret_cast<const float4*>(p + (long)rr * ld + cc);
   }
+  __device__ void prepare(int*, int, int, int, int) {}
   __device__ void bind(const BNTables&) {}
   __device__ float raw(int r, int c) const {
     const bool ok = r < rows && c < cols;
@@ -67,6 +69,7 @@ struct LoadColMajor {          // elem(r, c) = p[c * ld + r]
     const int cc = c < cols ? c : 0;
     return *reinterpret_cast<const float4*>(p + (long)cc * ld + rr);
   }
+  __device__ void prepare(int*, int, int, int, int) {}
   __device__ void bind(const BNTables&) {}
   __device__ float raw(int r, int c) const {
     const bool ok = r < rows && c < cols;
@@ -90,6 +93,7 @@ struct LoadBNAct {
     f = min(f, feat - 4);
     return *reinterpret_cast<const float4*>(x + (long)m * ld + f);
   }
+  __device__ void prepare(int*, int, int, int, int) {}
   __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
   __device__ float raw(int r, int c) const {
     const int m = ROWS_ARE_BATCH ? r : c, f = ROWS_ARE_BATCH ? c : r;
@@ -123,20 +127,42 @@ struct LoadIm2colT {
     ta = t.a; tb = t.b;
     if (U8 && cursor) { idx += cursor[0] * B; cursor = nullptr; }
   }
-  // Branch-free address computation; ok = false for padding / out of range.
+  // Per-workgroup tables (built once by prepare(), then 2 LDS reads per element instead
+  // of four runtime divisions):
+  //   col c in [klo, khi): {base offset of pixel's image, (oy*SH-PT) << 16 | (ox*SW-PL)}
+  //   row r in [rlo, rhi): {(i*W + j)*Cin + ci, i << 16 | j}, ci in the low bits of a 3rd
+  int* tcol; int* trow; int klo, rlo;
+  __device__ void prepare(int* tab, int rlo_, int rhi, int klo_, int khi) {
+    tcol = tab; trow = tab + 2 * KTAB; klo = klo_; rlo = rlo_;
+    const int kc = KH * KW * Cin, P = B * OH * OW, HWC = H * W * Cin;
+    for (int c = klo + (int)threadIdx.x; c < khi; c += blockDim.x) {
+      int t2, ox, b, oy;
+      dOW.divmod(min(c, P - 1), t2, ox);
+      dOH.divmod(t2, b, oy);
+      const long base = U8 ? idx[b] * (long)HWC : (long)b * HWC;
+      tcol[2 * (c - klo)] = (int)base;
+      tcol[2 * (c - klo) + 1] = ((oy * SH - PT) << 16) | ((ox * SW - PL) & 0xffff);
+    }
+    for (int r = rlo + (int)threadIdx.x; r < rhi; r += blockDim.x) {
+      int t, ci, i, j;
+      dCin.divmod(min(r, kc - 1), t, ci);
+      dKW.divmod(t, i, j);
+      trow[3 * (r - rlo)] = (i * W + j) * Cin + ci;
+      trow[3 * (r - rlo) + 1] = (i << 16) | j;
+      trow[3 * (r - rlo) + 2] = ci;
+    }
+  }
   __device__ long offset(int r, int c, int& ci, bool& ok) const {
     const int kc = KH * KW * Cin, P = B * OH * OW;
-    const int rr = min(r, kc - 1), cc = min(c, P - 1);
-    int t, i, j, t2, ox, b, oy;
-    dCin.divmod(rr, t, ci);
-    dKW.divmod(t, i, j);
-    dOW.divmod(cc, t2, ox);
-    dOH.divmod(t2, b, oy);
-    const int y = oy * SH - PT + i, xx = ox * SW - PL + j;
-    ok = (c < P) && (r < kc) && y >= 0 && y < H && xx >= 0 && xx < W;
-    const long pix = ((long)(ok ? y : 0) * W + (ok ? xx : 0)) * Cin + ci;
-    if (U8) return idx[b] * (long)(H * W * Cin) + pix;   // idx[b] always in range
-    return (long)b * H * W * Cin + pix;
+    const int cb = tcol[2 * (c - klo)], cyx = tcol[2 * (c - klo) + 1];
+    const int* rt = trow + 3 * (r - rlo);
+    const int ro = rt[0], rij = rt[1];
+    ci = rt[2];
+    const int y = (cyx >> 16) + (rij >> 16);
+    const int x = (short)(cyx & 0xffff) + (rij & 0xffff);
+    ok = (c < P) && (r < kc) && y >= 0 && y < H && x >= 0 && x < W;
+    const int pix = ((cyx >> 16) * W + (short)(cyx & 0xffff)) * Cin + ro;
+    return (long)cb + (ok ? pix : 0);
   }
   __device__ float raw(int r, int c) const {
     int ci;
@@ -210,47 +236,50 @@ struct EpiActBNBwd {
 // ----------------------------------------------------------------------------------
 template <class L>
 struct Stage {
-  static constexpr int PER = (32 * KC) / 64;
-  static constexpr int NV = L::VEC4 ? PER / 4 : PER;
-  int ro[NV], ko[NV];
+  static constexpr int PER = (32 * KC) / 64;          // elements per lane per chunk
+  static constexpr int NV = L::VEC4 ? PER / 4 : PER;  // loads per lane per chunk
   float v[PER];
-  __device__ void init(int lane) {
-#pragma unroll
-    for (int e = 0; e < NV; ++e) {
-      const int idx = lane + 64 * e;
-      if (L::VEC4) {
-        if (L::KCONTIG) { ro[e] = idx >> 2; ko[e] = (idx & 3) * 4; }
-        else { ko[e] = idx >> 3; ro[e] = (idx & 7) * 4; }
-      } else {
-        if (L::KCONTIG) { ro[e] = idx / KC; ko[e] = idx % KC; }
-        else { ko[e] = idx / 32; ro[e] = idx % 32; }
-      }
+  int lane;
+  // lane/e -> (outer row, k) of load e (compile-time e: pure shifts, no index arrays)
+  __device__ __forceinline__ void map(int e, int& ro, int& ko) const {
+    const int idx = lane + 64 * e;
+    if (L::VEC4) {
+      if (L::KCONTIG) { ro = idx / (KC / 4); ko = (idx % (KC / 4)) * 4; }
+      else { ko = idx >> 3; ro = (idx & 7) * 4; }
+    } else {
+      if (L::KCONTIG) { ro = idx / KC; ko = idx % KC; }
+      else { ko = idx >> 5; ro = idx & 31; }
     }
   }
+  __device__ void init(int l) { lane = l; }
   __device__ void fetch(const L& l, int r0, int k, int ke) {
 #pragma unroll
     for (int e = 0; e < NV; ++e) {
+      int ro, ko;
+      map(e, ro, ko);
       if (L::VEC4) {
-        const int kk = L::KCONTIG ? min(k + ko[e], ke - 4) : min(k + ko[e], ke - 1);
-        const float4 q = l.raw4(r0 + ro[e], kk);
+        const int kk = L::KCONTIG ? min(k + ko, ke - 4) : min(k + ko, ke - 1);
+        const float4 q = l.raw4(r0 + ro, kk);
         v[4 * e] = q.x; v[4 * e + 1] = q.y; v[4 * e + 2] = q.z; v[4 * e + 3] = q.w;
       } else {
-        v[e] = l.raw(r0 + ro[e], min(k + ko[e], ke - 1));
+        v[e] = l.raw(r0 + ro, min(k + ko, ke - 1));
       }
     }
   }
   __device__ void commit(const L& l, float* dst, int r0, int k, int ke) const {
 #pragma unroll
     for (int e = 0; e < NV; ++e) {
+      int ro, ko;
+      map(e, ro, ko);
       if (L::VEC4) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int r = L::KCONTIG ? ro[e] : ro[e] + u;
-          const int kk = L::KCONTIG ? ko[e] + u : ko[e];
+          const int r = L::KCONTIG ? ro : ro + u;
+          const int kk = L::KCONTIG ? ko + u : ko;
           dst[kk * LDS_PAD + r] = (k + kk < ke) ? l.post(v[4 * e + u], r0 + r, k + kk) : 0.f;
         }
       } else {
-        dst[ko[e] * LDS_PAD + ro[e]] = (k + ko[e] < ke) ? l.post(v[e], r0 + ro[e], k + ko[e]) : 0.f;
+        dst[ko * LDS_PAD + ro] = (k + ko < ke) ? l.post(v[e], r0 + ro, k + ko) : 0.f;
       }
     }
   }
@@ -260,39 +289,38 @@ struct Stage {
 // The kernel.  Grid: x = N tiles, y = M tiles, z = split-K slices.
 // WG tile = (32*WM) x (32*WN); its K slice is split WK ways across the waves.
 // ----------------------------------------------------------------------------------
+__device__ long long* g_gemm_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
+#define GEMM_STAMP(i)                                                                       \
+  do {                                                                                      \
+    if (g_gemm_dbg && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) \
+      g_gemm_dbg[i] = (long long)__builtin_amdgcn_s_memtime();                               \
+  } while (0)
+
 template <int WM, int WN, int WK, class LA, class LB, class EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
                                                        int k_per_split, BNRef bn, int bn_on,
                                                        float* bn_slab_out, int slab_C) {
   static_assert(WM * WN * WK == 4, "4 waves per workgroup");
-  constexpr int PER = (32 * KC) / 64;   // staged elements per lane per operand per chunk
-  __shared__ float s_stage[4][2][KC * LDS_PAD];
-  __shared__ float s_red[(WK > 1) ? (WM * WN * (WK - 1) * 16 * 64) : 1];
+  __shared__ float s_stage[4][2][KC * LDS_PAD];   // per-wave tiles; reused for the WK reduction
   __shared__ float s_bn[4 * MAXC];
   __shared__ float s_acc[2 * MAXC];
+  __shared__ int s_tab[2 * KTAB + 3 * 64];
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN);
   const int wm = wmn / WN, wn = wmn % WN;
   const int m0 = blockIdx.y * 32 * WM + wm * 32;
   const int n0 = blockIdx.x * 32 * WN + wn * 32;
-
-  if (bn_on) bn_reduce_to_lds(bn, s_bn, s_bn + MAXC, s_bn + 2 * MAXC, s_bn + 3 * MAXC, s_acc);
-  if (EPI::NEEDS_LDS) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < 2 * MAXC; i += blockDim.x) s_acc[i] = 0.f;
-  }
-  __syncthreads();
+  GEMM_STAMP(0);
   const BNTables tabs{s_bn, s_bn + MAXC, s_bn + 2 * MAXC, s_bn + 3 * MAXC};
   la.bind(tabs);
   lb.bind(tabs);
   epi.bind(tabs);
-
   // K range of this wave (multiples of KC keep every wave's chunks aligned)
   const int ks0 = blockIdx.z * k_per_split;
   const int ks1 = min(K, ks0 + k_per_split);
   const int klen = max(0, ks1 - ks0);
-  const int kw_len = ((klen + WK - 1) / WK + KC - 1) / KC * KC;
+  const int kw_len = ((klen + WK - 1) / WK + 3) / 4 * 4;
   const int kb = ks0 + wk * kw_len;
   const int ke = min(ks1, kb + kw_len);
 
@@ -302,13 +330,30 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
 
   float* sa = s_stage[wave][0];
   float* sb = s_stage[wave][1];
-  // Each operand tile (32 rows x KC) is PER scalar or PER/4 float4 loads per lane.
   Stage<LA> stA;
   Stage<LB> stB;
   stA.init(lane);
   stB.init(lane);
+  {  // loader tables for this workgroup's rows / K slice
+    const int rlo = blockIdx.y * 32 * WM, rhi = rlo + 32 * WM;
+    const int klo = blockIdx.z * k_per_split, khi = min(K, klo + k_per_split);
+    la.prepare(s_tab, rlo, rhi, klo, khi);
+    __syncthreads();
+  }
+  GEMM_STAMP(1);
+  // first chunk's operand loads go out BEFORE the BN-slab reduction, so the two
+  // memory round trips overlap
   if (kb < ke) { stA.fetch(la, m0, kb, ke); stB.fetch(lb, n0, kb, ke); }
+  if (bn_on) bn_reduce_to_lds(bn, s_bn, s_bn + MAXC, s_bn + 2 * MAXC, s_bn + 3 * MAXC, s_acc);
+  if (EPI::NEEDS_LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * MAXC; i += blockDim.x) s_acc[i] = 0.f;
+  }
+  __syncthreads();
+  int it = 0;
   for (int k = kb; k < ke; k += KC) {
+    if (it < 4) GEMM_STAMP(2 + it);
+    ++it;
     stA.commit(la, sa, m0, k, ke);
     stB.commit(lb, sb, n0, k, ke);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -329,16 +374,16 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 
-  if (WK > 1) {  // intra-workgroup split-K reduction through LDS
-    if (wk > 0) {
-      float* dst = s_red + ((size_t)(wmn * (WK - 1) + (wk - 1)) * 16 * 64);
+  GEMM_STAMP(6);
+  if (WK > 1) {  // intra-workgroup split-K reduction through LDS (each wave's own stage area)
+    float* mine = s_stage[wave][0];
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dst[i * 64 + lane] = acc[i];
-    }
+    for (int i = 0; i < 16; ++i) mine[i * 64 + lane] = acc[i];
     __syncthreads();
     if (wk == 0) {
-      for (int s = 0; s < WK - 1; ++s) {
-        const float* src = s_red + ((size_t)(wmn * (WK - 1) + s) * 16 * 64);
+      for (int s2 = 1; s2 < WK; ++s2) {
+        const float* src = s_stage[s2 * (WM * WN) + wmn][0];
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] += src[i * 64 + lane];
       }
@@ -352,6 +397,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
       epi(m0 + row, n0 + (lane & 31), acc[i], first, s_acc);
     }
   }
+  GEMM_STAMP(7);
   if (EPI::NEEDS_LDS && bn_slab_out) {
     __syncthreads();
     const int slab_row = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
@@ -364,21 +410,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
 struct Plan { int wm, wn, wk, splits, kps; };
 
 static Plan plan_gemm(int M, int N, int K, bool allow_split) {
-  const int target_waves = 1024;
   int tm = (M + 31) / 32, tn = (N + 31) / 32;
   int tiles = tm * tn;
   Plan p;
   if (tiles >= 512) { p.wm = 2; p.wn = 2; p.wk = 1; }
   else if (tiles >= 256) { p.wm = 1; p.wn = 2; p.wk = 2; }
   else { p.wm = 1; p.wn = 1; p.wk = 4; }
-  int wg = ((tm + p.wm - 1) / p.wm) * ((tn + p.wn - 1) / p.wn);
-  int waves = wg * 4;
+  const int wg = ((tm + p.wm - 1) / p.wm) * ((tn + p.wn - 1) / p.wn);
+  // split K across workgroups until each wave owns <= one KC chunk (one memory round
+  // trip per wave), keeping the launch under ~4096 waves and 512 slices
   int splits = 1;
   if (allow_split)
-    while (waves * splits * 2 <= target_waves && K / (splits * 2 * p.wk) >= 48) splits *= 2;
+    while ((K + splits * p.wk - 1) / (splits * p.wk) > KC && wg * 4 * splits * 2 <= 4096 && splits < 512)
+      splits *= 2;
   p.splits = splits;
-  int kps = (K + splits - 1) / splits;
-  p.kps = (kps + KC - 1) / KC * KC;
+  const int kps = (K + splits - 1) / splits;
+  p.kps = (kps + 3) / 4 * 4;
   return p;
 }
 
@@ -424,6 +471,11 @@ using namespace csa;
 // ===================================================================================
 // C ABI (called through ctypes from cloud_server_amd/ops/fused.py)
 // ===================================================================================
+
+// Diagnostics: set the device pointer that receives GEMM stamps (null disables).
+CSA_API int csa_gemm_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_dbg), &p, sizeof(p));
+}
 
 // How many split-K slices a dense forward of this shape uses (>1 => Y must be zeroed).
 CSA_API int csa_dense_fwd_splits(int M, int N, int K) { return plan_gemm(M, N, K, true).splits; }
@@ -521,6 +573,10 @@ CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* id
   const int Mg = kc + (db ? 1 : 0);
   const int P = B * OH * OW;
   Plan p = plan_gemm(Mg, Cout, P, true);
+  while (p.kps > KTAB) {   // the im2col tables cover one K slice per workgroup
+    p.splits *= 2;
+    p.kps = ((P + p.splits - 1) / p.splits + 3) / 4 * 4;
+  }
   // conv wgrad is always accumulated with atomics (split-K over pixels)
   BNRef bn = make_bn(bn_slab, bn_nslab, Cin, bn_count, bn_eps, bn_scale, bn_offset);
   EpiStore epi{dW, (long)Cout, kc, Cout, nullptr, 1, db, 1.f};

@@ -45,6 +45,8 @@ _SIGS = {
     "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P]),
     "csa_optimizer": (I, [I, P, P, P, P, L, F, P, P, P, I, P, P, P, P, P, P, F, I, P, P]),
     "csa_zero": (I, [P, P, I, P]),
+    "csa_gemm_debug": (I, [P]),
+    "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),
 }
 
 

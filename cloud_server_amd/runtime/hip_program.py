@@ -80,6 +80,7 @@ class Unit:
     dy: Optional[torch.Tensor] = None       # grad wrt output (or wrt the next BN output)
     dc: Optional[torch.Tensor] = None       # conv: grad wrt pre-act conv output
     splits_fwd: int = 1
+    xt: Optional[torch.Tensor] = None       # dense: materialised act(bn(x)) (BN inputs)
 
 
 class HipProgram:
@@ -193,6 +194,11 @@ class HipProgram:
                     nb = self.lib.csa_conv_dgrad_nslab(self._conv_geom(u.layer, B))
                 tf.bwd_slab = torch.zeros(nb, 2, C, **f32)
                 tf.bwd_nslab = nb
+        # dense consumers of a BatchNorm'd tensor get it materialised once per step
+        for u in self.units:
+            u.xt = None
+            if u.kind == "dense" and u.in_tf.has_bn and u.layer.in_shape.numel % 4 == 0:
+                u.xt = torch.zeros(B, u.layer.in_shape.numel, **f32)
         self.dlast = self.units[-1].dy     # head input grad
         self.idx = None
 
@@ -304,9 +310,17 @@ class HipProgram:
                     _act_id(u.act), _alpha(u.act), K.ptr(cur) if raw else None, st), "conv_fwd")
             else:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
-                self._rc(lib.csa_dense_fwd(
-                    K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
-                    B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
+                if u.xt is not None:
+                    self._rc(lib.csa_bn_act_apply(
+                        K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha, st),
+                        "bn_act_apply")
+                    self._rc(lib.csa_dense_fwd(
+                        K.ptr(u.xt), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
+                        B, fout, fin, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, st), "dense_fwd")
+                else:
+                    self._rc(lib.csa_dense_fwd(
+                        K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
+                        B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
 
         # ---------------- head (loss, head grads, input grad, metrics) ----------------
         last = self.units[-1]
@@ -334,9 +348,14 @@ class HipProgram:
                         K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
                         K.ptr(xf), in_act, in_alpha, *self._bn_args_c(tf), K.ptr(tf.bwd_slab), st),
                         "slabs:dense_dgrad")
-                self._rc(lib.csa_dense_wgrad(
-                    K.ptr(u.x), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
-                    B, fin, fout, *self._bn_args_c(tf), in_act, in_alpha, 1.0, st), "dense_wgrad")
+                if u.xt is not None:
+                    self._rc(lib.csa_dense_wgrad(
+                        K.ptr(u.xt), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+                        B, fin, fout, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, 1.0, st), "dense_wgrad")
+                else:
+                    self._rc(lib.csa_dense_wgrad(
+                        K.ptr(u.x), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+                        B, fin, fout, *self._bn_args_c(tf), in_act, in_alpha, 1.0, st), "dense_wgrad")
             else:
                 # output side: (BN backward of the NEXT transform) + act backward + pool routing
                 next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf

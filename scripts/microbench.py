@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Per-kernel micro-benchmarks of the HIP step program (GPU).
+
+Builds the sample-config engine, then times each kernel launch of one training step in
+isolation: the step's launch list is recorded once, and each launch is replayed N times
+back to back (plain stream launches, event-timed).  Output: one line per launch with
+µs/launch.  Run: python scripts/microbench.py [--reps 200] [--batch 50]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from cloud_server_amd.data.datasets import synthetic_mnist  # noqa: E402
+from cloud_server_amd.models.dsl import SAMPLE_CONFIG, parse_train_config  # noqa: E402
+from cloud_server_amd.ops import fused as K  # noqa: E402
+from cloud_server_amd.runtime.engine import TrainEngine  # noqa: E402
+
+
+class Recorder:
+    """Wraps the ctypes library: records (name, fn, args) of every csa_* call."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        self.calls = []
+
+    def __getattr__(self, name):
+        fn = getattr(self.lib, name)
+        if not name.startswith("csa_") or name.endswith(("_splits", "_slabs", "_nslab")):
+            return fn
+
+        def wrapped(*args):
+            self.calls.append((name, fn, args))
+            return fn(*args)
+        return wrapped
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=50)
+    a = ap.parse_args()
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer",
+                                  options={"batch_size": a.batch}))
+    eng = TrainEngine(cfg, synthetic_mnist(6000), device="cuda", backend="hip", use_graph=False)
+    for _ in range(3):
+        eng.step()
+    rec = Recorder(eng.program.lib)
+    eng.program.lib = rec
+    eng.step()
+    torch.cuda.synchronize()
+    eng.program.lib = rec.lib
+    total = 0.0
+    rows = []
+    if os.environ.get("MB_GEMM"):
+        dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name in ("csa_dense_fwd", "csa_dense_dgrad", "csa_dense_wgrad", "csa_conv_wgrad"):
+                eng.program.lib.csa_gemm_debug(dbg.data_ptr())
+                fn(*args)
+                torch.cuda.synchronize()
+                eng.program.lib.csa_gemm_debug(None)
+                t = dbg.tolist()
+                print(f"{i:2d} {name:18s} stamps:", [t[j + 1] - t[j] for j in range(7)])
+    for i, (name, fn, args) in enumerate(rec.calls):
+        for _ in range(5):
+            fn(*args)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.reps):
+            fn(*args)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) * 1e3 / a.reps
+        total += us
+        rows.append((i, name, us))
+    for i, name, us in rows:
+        print(f"{i:2d} {name:24s} {us:8.2f} us")
+    print(f"sum of isolated launches: {total:.1f} us")
+    # whole step, graph replay
+    eng2 = TrainEngine(cfg, synthetic_mnist(6000), device="cuda", backend="hip", use_graph=True)
+    for _ in range(20):
+        eng2.step()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(a.reps):
+        eng2.step()
+    e.record()
+    torch.cuda.synchronize()
+    print(f"graph step: {s.elapsed_time(e) * 1e3 / a.reps:.1f} us")
+    return 0
+
+
+def head_stamps():
+    """Phase timestamps of the head kernel (CSA_HEAD_DBG points at a device buffer)."""
+    buf = torch.zeros(8, dtype=torch.int64, device="cuda")
+    os.environ["CSA_HEAD_DBG"] = str(buf.data_ptr())
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, options={"batch_size": 50}))
+    eng = TrainEngine(cfg, synthetic_mnist(600), device="cuda", backend="hip", use_graph=False)
+    for _ in range(5):
+        eng.step()
+    torch.cuda.synchronize()
+    t = buf.tolist()
+    print("head phase cycles (s_memtime, 100MHz ref):", [t[i + 1] - t[i] for i in range(5)])
+    del os.environ["CSA_HEAD_DBG"]
+
+
+if __name__ == "__main__":
+    if os.environ.get("MB_HEAD"):
+        head_stamps()
+    sys.exit(main())

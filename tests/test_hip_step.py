@@ -125,3 +125,18 @@ def test_training_learns_sample_config():
         eng.step()
     acc = eng.evaluate(ds)
     assert acc > 0.9, acc
+
+
+@pytest.mark.parametrize("batch", [1, 7, 64, 80, 200])
+def test_batch_sizes_match_torch(batch):
+    """Odd batch sizes: head MFMA path (<= 64 rows) and generic path, GEMM M tiling."""
+    ds = synthetic_mnist(600, seed=13)
+    cfg = _cfg(CASES["sample"], lr=0.5, batch=batch)
+    eh, w0h, w1h = _run_one(cfg, "hip", ds)
+    et, w0t, w1t = _run_one(cfg, "torch", ds)
+    gh = (w0h - w1h) / cfg.effective_lr
+    gt = (w0t - w1t) / cfg.effective_lr
+    for k in eh.model.state.shapes:
+        a, b = eh.model.state.view(k, gh), et.model.state.view(k, gt)
+        scale = b.abs().max().item() + 1e-6
+        assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6, f"batch {batch} grad {k}"
