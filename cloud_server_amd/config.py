@@ -1,0 +1,74 @@
+"""Settings: one env-driven object replacing the reference's config layers.
+
+Reference: Django settings.py (hard-coded SECRET_KEY, MySQL and SMTP credentials,
+DEBUG=True, ALLOWED_HOSTS='*'; settings.py:22-170) and module constants in
+global_settings.py (storage root, container IDs, PS/worker host:port).  None of those
+secrets are reproduced: everything comes from ``CSA_*`` environment variables with safe
+local defaults.
+
+| variable              | default                         | meaning                               |
+|-----------------------|---------------------------------|---------------------------------------|
+| CSA_STORAGE_ROOT      | ~/.cloud_server_amd             | workspace root (replaces /root/)      |
+| CSA_DB_PATH           | <root>/server.sqlite3           | SQLite database file                  |
+| CSA_GPUS              | all visible                     | comma list of GPU ids the scheduler uses |
+| CSA_EXECUTOR          | process                         | process / thread / inline job runner  |
+| CSA_TOKEN_TTL_S       | 0 (never expires)               | auth token lifetime                   |
+| CSA_ALLOW_URL_FETCH   | 1                               | allow the ``url`` dataset type        |
+| CSA_MAX_UPLOAD_MB     | 512                             | request body limit                    |
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+
+def _env(name: str, default: str) -> str:
+    return os.environ.get(name, default)
+
+
+@dataclass
+class Settings:
+    storage_root: str = field(default_factory=lambda: os.path.abspath(os.path.expanduser(
+        _env("CSA_STORAGE_ROOT", "~/.cloud_server_amd"))))
+    db_path: str = ""
+    gpus: Optional[List[int]] = None
+    executor: str = field(default_factory=lambda: _env("CSA_EXECUTOR", "process"))
+    token_ttl_s: int = field(default_factory=lambda: int(_env("CSA_TOKEN_TTL_S", "0")))
+    allow_url_fetch: bool = field(default_factory=lambda: _env("CSA_ALLOW_URL_FETCH", "1") == "1")
+    max_upload_mb: int = field(default_factory=lambda: int(_env("CSA_MAX_UPLOAD_MB", "512")))
+    preprocess_backend: str = field(default_factory=lambda: _env("CSA_PREPROCESS_BACKEND", "auto"))
+    train_backend: str = field(default_factory=lambda: _env("CSA_TRAIN_BACKEND", "auto"))
+
+    def __post_init__(self):
+        if not self.db_path:
+            self.db_path = _env("CSA_DB_PATH", os.path.join(self.storage_root, "server.sqlite3"))
+        if self.gpus is None:
+            g = _env("CSA_GPUS", "")
+            self.gpus = [int(x) for x in g.split(",") if x.strip()] if g else None
+        os.makedirs(self.storage_root, exist_ok=True)
+
+    # ---- workspace layout, per user and model; no global scratch ----
+    def user_root(self, uid: int) -> str:
+        return os.path.join(self.storage_root, "NJUCloud", str(uid))
+
+    def data_dir(self, uid: int, file_class: str) -> str:
+        return os.path.join(self.user_root(uid), "data", file_class)
+
+    def model_dir(self, uid: int, model: str) -> str:
+        return os.path.join(self.user_root(uid), "model", model)
+
+
+_SETTINGS: Optional[Settings] = None
+
+
+def get_settings() -> Settings:
+    global _SETTINGS
+    if _SETTINGS is None:
+        _SETTINGS = Settings()
+    return _SETTINGS
+
+
+def set_settings(s: Settings) -> None:
+    global _SETTINGS
+    _SETTINGS = s

@@ -1,0 +1,280 @@
+"""Job manager: queue, GPU-slot placement, launch, control and bookkeeping of training jobs.
+
+Replaces the reference control plane — paramiko SSH into the cluster host, ``docker cp``
+into fixed PS/worker containers, ``pkill -9 python``, ``nohup python ...`` (C15, C21,
+C29; apps/construction/views.py:97-146) — with a local manager:
+
+* a job = one ``model.json`` in ``NJUCloud/<uid>/model/<m>/`` plus a DB row whose state
+  follows ``queued -> running -> (paused | stopped | failed | done)``;
+* placement by the native GPU-slot scheduler (``runtime.scheduler``), several small jobs
+  per GPU, data-parallel jobs over several GPUs;
+* executors: ``process`` (default; one worker process per rank, started by a launcher
+  process that is spawned before this process touches the GPU, so no process that
+  initialised HIP ever forks/execs), ``thread`` and ``inline`` (tests, CPU);
+* control: stop / pause write ``control.json`` (the trainer checks it every log
+  interval and checkpoints on pause); resume re-queues the job and the trainer restores
+  the newest checkpoint; a worker that dies is marked failed (its slots are released)
+  and can be resumed the same way.
+"""
+from __future__ import annotations
+
+import json
+import multiprocessing as mp
+import os
+import queue
+import subprocess
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, List, Optional
+
+from ..store.db import Database
+from .scheduler import make_scheduler
+from .trainer import CONTROL, STATUS, run_job, write_status
+
+TERMINAL = ("done", "stopped", "failed", "paused")
+
+
+def _launcher_main(req: "mp.Queue", resp: "mp.Queue") -> None:   # pragma: no cover - subprocess
+    """Runs in a spawned helper that never initialises HIP: owns every worker Popen."""
+    procs: Dict[int, subprocess.Popen] = {}
+    while True:
+        try:
+            msg = req.get(timeout=0.2)
+        except queue.Empty:
+            msg = None
+        if msg is not None:
+            kind = msg[0]
+            if kind == "launch":
+                _, jid, argv, env, cwd, log = msg
+                with open(log, "ab") as lf:
+                    procs[jid] = subprocess.Popen(argv, env=env, cwd=cwd, stdout=lf, stderr=subprocess.STDOUT,
+                                                  start_new_session=True)
+            elif kind == "kill":
+                p = procs.get(msg[1])
+                if p is not None and p.poll() is None:
+                    p.terminate()
+            elif kind == "exit":
+                for p in procs.values():
+                    if p.poll() is None:
+                        p.terminate()
+                return
+        for jid, p in list(procs.items()):
+            rc = p.poll()
+            if rc is not None:
+                resp.put(("exited", jid, rc))
+                del procs[jid]
+
+
+class JobManager:
+    def __init__(self, settings, db: Database, executor: Optional[str] = None,
+                 ngpu: Optional[int] = None, slots_per_gpu: int = 4):
+        self.settings = settings
+        self.db = db
+        self.executor = executor or settings.executor
+        if ngpu is None:
+            ngpu = self._count_gpus()
+        self.ngpu = ngpu
+        self.use_cpu = ngpu == 0
+        self.sched = make_scheduler(max(ngpu, 1), slots_per_gpu if ngpu else 2)
+        self.running: Dict[int, Dict[str, Any]] = {}
+        self._lock = threading.RLock()
+        self._stop = threading.Event()
+        self._launcher = None
+        if self.executor == "process":
+            ctx = mp.get_context("spawn")
+            self._req, self._resp = ctx.Queue(), ctx.Queue()
+            self._launcher = ctx.Process(target=_launcher_main, args=(self._req, self._resp), daemon=True)
+            self._launcher.start()
+        self._thread = threading.Thread(target=self._loop, name="csa-jobs", daemon=True)
+        self._thread.start()
+        self._recover()
+
+    @staticmethod
+    def _count_gpus() -> int:
+        vis = os.environ.get("CSA_GPUS")
+        if vis:
+            return len([x for x in vis.split(",") if x.strip()])
+        try:
+            import torch
+            return torch.cuda.device_count()   # does not initialise HIP on this image
+        except Exception:
+            return 0
+
+    # ------------------------------------------------------------------ public API
+    def submit(self, owner: int, model: str, datatype: str, config: Dict[str, Any],
+               ngpus: int = 1) -> int:
+        mdir = self.settings.model_dir(owner, model)
+        os.makedirs(mdir, exist_ok=True)
+        with open(os.path.join(mdir, "model.json"), "w", encoding="utf-8") as f:
+            json.dump(config, f, ensure_ascii=False)
+        try:
+            os.remove(os.path.join(mdir, CONTROL))
+        except OSError:
+            pass
+        jid = self.db.add_job(owner, model, datatype, config)
+        write_status(mdir, state="queued", job=jid)
+        ngpus = max(1, min(int(ngpus), max(self.ngpu, 1)))
+        if not self.sched.submit(jid, 1 if self.use_cpu else ngpus):
+            self.db.update_job(jid, state="failed", error="cannot place job")
+            raise ValueError("job needs more GPUs than the node has")
+        with self._lock:
+            self.running[jid] = {"owner": owner, "model": model, "mdir": mdir, "ngpus": ngpus,
+                                 "datatype": datatype, "state": "queued"}
+        if self.executor == "inline":
+            self._admit()
+        return jid
+
+    def control(self, jid: int, action: str) -> Dict[str, Any]:
+        job = self.db.get_job(jid)
+        if job is None:
+            raise KeyError(jid)
+        mdir = self.settings.model_dir(job["owner_id"], job["model"])
+        if action in ("stop", "pause"):
+            if job["state"] == "queued":
+                self.sched.cancel(jid)
+                self._finish(jid, "stopped" if action == "stop" else "paused")
+            else:
+                with open(os.path.join(mdir, CONTROL), "w") as f:
+                    json.dump({"action": action, "time": time.time()}, f)
+            return {"job": jid, "action": action}
+        if action == "resume":
+            if job["state"] not in ("paused", "stopped", "failed"):
+                raise ValueError(f"job {jid} is {job['state']}")
+            cfg = json.loads(job["config"])
+            return {"job": self.submit(job["owner_id"], job["model"], job["datatype"], cfg), "action": "resume"}
+        raise ValueError(f"unknown action {action!r}")
+
+    def status(self, jid: int) -> Dict[str, Any]:
+        job = self.db.get_job(jid)
+        if job is None:
+            raise KeyError(jid)
+        mdir = self.settings.model_dir(job["owner_id"], job["model"])
+        st = {}
+        try:
+            with open(os.path.join(mdir, STATUS)) as f:
+                st = json.load(f)
+        except (OSError, json.JSONDecodeError):
+            pass
+        out = {k: job[k] for k in ("id", "model", "datatype", "state", "created", "started", "finished", "gpu", "error")}
+        out["progress"] = st
+        return out
+
+    def wait(self, jid: int, timeout: float = 300.0) -> str:
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            j = self.db.get_job(jid)
+            if j and j["state"] in TERMINAL:
+                return j["state"]
+            time.sleep(0.05)
+        raise TimeoutError(f"job {jid} still {self.db.get_job(jid)['state']}")
+
+    def shutdown(self) -> None:
+        self._stop.set()
+        if self._launcher is not None:
+            try:
+                self._req.put(("exit",))
+                self._launcher.join(timeout=5)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ internals
+    def _recover(self) -> None:
+        """Jobs left running by a previous server instance are marked failed (resumable)."""
+        for j in self.db.active_jobs():
+            if j["id"] not in self.running:
+                self.db.update_job(j["id"], state="failed", error="server restarted", finished=time.time())
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            try:
+                self._admit()
+                self._reap()
+            except Exception:   # pragma: no cover - keep the dispatcher alive
+                traceback.print_exc()
+            time.sleep(0.05)
+
+    def _admit(self) -> None:
+        while True:
+            nxt = self.sched.next()
+            if nxt is None:
+                return
+            jid, gpus = nxt
+            with self._lock:
+                info = self.running.get(jid)
+            if info is None:
+                self.sched.release(jid)
+                continue
+            info["gpus"] = gpus
+            info["state"] = "running"
+            self.db.update_job(jid, state="running", started=time.time(),
+                               gpu=",".join(map(str, gpus)) if not self.use_cpu else "cpu")
+            self._launch(jid, info)
+
+    def _launch(self, jid: int, info: Dict[str, Any]) -> None:
+        mdir, datatype = info["mdir"], info["datatype"]
+        with open(os.path.join(mdir, "model.json"), encoding="utf-8") as f:
+            config = json.load(f)
+        if self.executor in ("inline", "thread"):
+            def body():
+                rc = 0
+                try:
+                    dev = "cpu" if self.use_cpu else f"cuda:{info['gpus'][0]}"
+                    run_job(mdir, config, datatype, device=dev, backend=self.settings.train_backend)
+                except Exception:
+                    rc = 1
+                self._exited(jid, rc)
+            if self.executor == "inline":
+                body()
+            else:
+                threading.Thread(target=body, name=f"job-{jid}", daemon=True).start()
+            return
+        env = dict(os.environ)
+        env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__))))] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+        n = len(info["gpus"])
+        if not self.use_cpu:
+            env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, info["gpus"]))
+        mod = ["-m", "cloud_server_amd.runtime.worker", "--model-dir", mdir, "--datatype", datatype,
+               "--backend", self.settings.train_backend]
+        if n > 1:
+            port = 29500 + (jid % 2000)
+            argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port)] + mod[1:]
+        else:
+            argv = [sys.executable] + mod + ["--device", "cpu" if self.use_cpu else "cuda:0"]
+        self._req.put(("launch", jid, argv, env, mdir, os.path.join(mdir, "worker.log")))
+
+    def _reap(self) -> None:
+        if self._launcher is None:
+            return
+        while True:
+            try:
+                _, jid, rc = self._resp.get_nowait()
+            except queue.Empty:
+                return
+            self._exited(jid, rc)
+
+    def _exited(self, jid: int, rc: int) -> None:
+        with self._lock:
+            info = self.running.get(jid)
+        mdir = info["mdir"] if info else None
+        state = "failed"
+        if mdir:
+            try:
+                with open(os.path.join(mdir, STATUS)) as f:
+                    s = json.load(f).get("state")
+                if rc == 0 and s in ("done", "stopped", "paused"):
+                    state = s
+            except (OSError, json.JSONDecodeError):
+                pass
+        self._finish(jid, state, None if state != "failed" else f"worker exit code {rc}")
+
+    def _finish(self, jid: int, state: str, error: Optional[str] = None) -> None:
+        self.sched.release(jid)
+        with self._lock:
+            info = self.running.pop(jid, None)
+        if info and state in ("failed", "stopped", "paused"):
+            write_status(info["mdir"], state=state)
+        self.db.update_job(jid, state=state, finished=time.time(), error=error)

@@ -1,0 +1,235 @@
+"""End-to-end REST API tests (CPU): the user flow of SURVEY.md §3.1 through FastAPI's
+TestClient — register/login, upload a zip of digit PNGs + tag.json, preprocess, build a
+model from the DSL, train it (inline executor), poll results, list/detail models, infer.
+
+Reference parity: apps/*/views.py behaviour and API.md payloads; data is synthetic
+(reference test-data images are PNGs loaded with PIL, not pickles)."""
+import base64
+import io
+import json
+import os
+import zipfile
+
+import numpy as np
+import pytest
+from fastapi.testclient import TestClient
+from PIL import Image
+
+from cloud_server_amd.api.app import create_app, validate_password
+from cloud_server_amd.api.forms import encode_multipart, parse_multipart
+from cloud_server_amd.config import Settings
+from cloud_server_amd.data.datasets import synthetic_mnist
+
+PW = "Str0ng-pass-42"
+
+
+def _png(arr):
+    b = io.BytesIO()
+    Image.fromarray(arr.astype(np.uint8)).save(b, format="PNG")
+    return b.getvalue()
+
+
+@pytest.fixture()
+def client(tmp_path):
+    s = Settings(storage_root=str(tmp_path / "store"), db_path=str(tmp_path / "db.sqlite3"),
+                 executor="inline", train_backend="torch", allow_url_fetch=True)
+    app = create_app(s, executor="inline", ngpu=0, inference_device="cpu")
+    with TestClient(app) as c:
+        c.settings = s
+        yield c
+
+
+def _auth(c, name="alice"):
+    r = c.post("/rest-auth/registration/", json={"username": name, "email": f"{name}@x.org",
+                                                   "password1": PW, "password2": PW})
+    assert r.status_code == 201, r.text
+    r = c.post("/rest-auth/login/", json={"username": name, "password": PW})
+    assert r.status_code == 200
+    return {"Authorization": "Token " + r.json()["key"]}
+
+
+def _mp(c, url, fields, files, headers):
+    body, ct = encode_multipart(fields, files)
+    return c.post(url, content=body, headers={**headers, "Content-Type": ct})
+
+
+def _digit_zip(n=60):
+    ds = synthetic_mnist(n, seed=3)
+    zb = io.BytesIO()
+    tags = {}
+    with zipfile.ZipFile(zb, "w") as z:
+        for i in range(n):
+            name = f"img_{i:03d}.png"
+            z.writestr(f"digits/{name}", _png(ds.images[i].reshape(28, 28)))
+            tags[f"digits/{name}"] = int(ds.labels[i])
+    return zb.getvalue(), tags, ds
+
+
+def test_password_validators():
+    assert validate_password("short")
+    assert validate_password("12345678901")
+    assert validate_password("password")
+    assert validate_password("alice-the-great", "alice")
+    assert not validate_password(PW, "bob", "bob@x.org")
+
+
+def test_multipart_roundtrip():
+    body, ct = encode_multipart({"a": "1", "b": "héllo"}, {"file": ("x.bin", b"\x00\r\n--x\xff", "application/x")})
+    f, files = parse_multipart(body, ct)
+    assert f == {"a": "1", "b": "héllo"}
+    assert files["file"].data == b"\x00\r\n--x\xff" and files["file"].filename == "x.bin"
+
+
+def test_auth_flow(client):
+    h = _auth(client)
+    r = client.get("/rest-auth/user/", headers=h)
+    assert r.status_code == 200 and r.json()["username"] == "alice"
+    assert client.get("/rest-auth/user/").status_code == 401
+    basic = {"Authorization": "Basic " + base64.b64encode(f"alice:{PW}".encode()).decode()}
+    assert client.get("/rest-auth/user/", headers=basic).status_code == 200
+    r = client.patch("/rest-auth/user/", json={"first_name": "Al"}, headers=h)
+    assert r.json()["first_name"] == "Al"
+    # duplicate / weak registration
+    r = client.post("/rest-auth/registration/", json={"username": "alice", "password1": "x", "password2": "y"})
+    assert r.status_code == 400 and "username" in r.json()
+    # bad login
+    assert client.post("/rest-auth/login/", json={"username": "alice", "password": "nope"}).status_code == 400
+    # password change
+    new = "An0ther-pass-77"
+    r = client.post("/rest-auth/password/change/", json={"old_password": PW, "new_password1": new,
+                                                         "new_password2": new}, headers=h)
+    assert r.status_code == 200
+    assert client.post("/rest-auth/login/", json={"username": "alice", "password": new}).status_code == 200
+    # reset via outbox mail
+    assert client.post("/rest-auth/password/reset/", json={"email": "alice@x.org"}).status_code == 200
+    box = os.path.join(client.settings.storage_root, "outbox")
+    mail = [open(os.path.join(box, f)).read() for f in sorted(os.listdir(box)) if "reset" in open(os.path.join(box, f)).read()][-1]
+    uid = mail.split("uid: ")[1].split()[0]
+    tok = mail.split("token: ")[1].split()[0]
+    third = "Thr33-pass-xyz"
+    r = client.post("/rest-auth/password/reset/confirm/", json={"uid": uid, "token": tok,
+                                                                "new_password1": third, "new_password2": third})
+    assert r.status_code == 200, r.text
+    # token is single-use
+    r = client.post("/rest-auth/password/reset/confirm/", json={"uid": uid, "token": tok,
+                                                                "new_password1": third, "new_password2": third})
+    assert r.status_code == 400
+    # logout invalidates the token
+    h2 = {"Authorization": "Token " + client.post("/rest-auth/login/", json={"username": "alice", "password": third}).json()["key"]}
+    assert client.post("/rest-auth/logout/", headers=h2).status_code == 200
+    assert client.get("/rest-auth/user/", headers=h2).status_code == 401
+
+
+def test_data_upload_detail_delete(client):
+    h = _auth(client)
+    hb = _auth(client, "bob")
+    # single csv doc
+    r = _mp(client, "/data/list/", {"file_type": "single", "file_class": "doc"},
+            {"file": ("t.csv", b"a,b\n1,2\n3,4\n", "text/csv")}, h)
+    assert r.status_code == 200, r.text
+    pk = r.json()["data_id"]
+    r = client.get(f"/data/{pk}/", headers=h)
+    assert r.json() == [{"a": "1", "b": "2"}, {"a": "3", "b": "4"}]
+    lst = client.get("/data/list/", headers=h).json()
+    assert len(lst) == 1 and lst[0]["file_type"] == "doc" and lst[0]["file_name"].startswith("t_") and lst[0]["file_name"].endswith(".csv")
+    # zip picture: tree listing + relative file download
+    zb, tags, _ = _digit_zip(4)
+    r = _mp(client, "/data/list/", {"file_type": "zip", "file_class": "picture"},
+            {"file": ("digits.zip", zb, "application/zip")}, h)
+    zpk = r.json()["data_id"]
+    tree = client.get(f"/data/{zpk}/", headers=h).json()
+    assert "digits" in json.dumps(tree)
+    r = client.get(f"/data/{zpk}/", params={"relative_path": "digits/img_000.png"}, headers=h)
+    assert r.status_code == 200 and r.content[:4] == b"\x89PNG"
+    # path escape refused
+    r = client.get(f"/data/{zpk}/", params={"relative_path": "../../../../db.sqlite3"}, headers=h)
+    assert r.status_code == 404
+    # other users cannot read or delete
+    assert client.get(f"/data/{pk}/", headers=hb).status_code == 403
+    assert client.delete(f"/data/{pk}/", headers=hb).status_code == 403
+    assert client.delete(f"/data/{pk}/", headers=h).status_code == 200
+    assert client.get(f"/data/{pk}/", headers=h).status_code == 404
+    assert client.get("/data/list/").status_code == 401
+
+
+def test_zip_slip_refused(client):
+    h = _auth(client)
+    zb = io.BytesIO()
+    with zipfile.ZipFile(zb, "w") as z:
+        z.writestr("../../evil.txt", b"x")
+        z.writestr("ok.txt", b"y")
+    r = _mp(client, "/data/list/", {"file_type": "zip", "file_class": "doc"},
+            {"file": ("e.zip", zb.getvalue(), "application/zip")}, h)
+    assert r.status_code == 200
+    assert not os.path.exists(os.path.join(client.settings.storage_root, "NJUCloud", "1", "evil.txt"))
+
+
+def test_options_and_generate(client):
+    r = client.post("/construct/options/", json={"option": "optimizer"})
+    assert r.status_code == 200 and r.json()["tokens"]["Adam Optimizer"] == "AdamOptimizer"
+    assert client.post("/construct/options/", json={"option": "nope"}).status_code == 400
+    r = client.post("/generation/generate/", json={"iter": 5, "learning_rate": 0.1, "ratio": 0.8,
+                                                   "net_config": {"middle_layer": [{"layer": "connect", "hidden": 32}]}})
+    assert r.status_code == 200, r.text
+    assert r.json()["params"] == 784 * 32 + 32 + 32 * 10 + 10
+    assert client.get("/preprocess/").status_code == 501
+    assert len(client.get("/preprocess/operations/list/").json()) == 14
+
+
+def test_full_user_flow(client):
+    h = _auth(client)
+    zb, tags, ds = _digit_zip(60)
+    assert client.post("/data/create/", json={"modelName": "m1"}, headers=h).json() == {"message": "success"}
+    assert client.post("/data/create/", json={"modelName": "m1"}, headers=h).status_code == 500
+    assert client.post("/data/create/", json={"modelName": "../x"}, headers=h).status_code == 500
+    r = _mp(client, "/data/tag/", {"modelName": "m1"}, {"file": ("tag.json", json.dumps(tags).encode(), "application/json")}, h)
+    assert r.json() == {"message": "success"}
+    pk = _mp(client, "/data/list/", {"file_type": "zip", "file_class": "picture"},
+             {"file": ("d.zip", zb, "application/zip")}, h).json()["data_id"]
+    ops = [{"operationName": "左右翻转", "overlap": True},
+           {"operationName": "对比度亮度调整", "value1": 1.2, "value2": 5, "overlap": "true"}]
+    r = client.post("/preprocess/", json={"dataId": pk, "modelName": "m1", "operations": ops}, headers=h)
+    assert r.json() == {"message": "success"}, r.text
+    mdir = client.settings.model_dir(1, "m1")
+    newtags = json.load(open(os.path.join(mdir, "tag.json")))
+    assert len(newtags) == 60 * 3    # originals + one copy per op (batch mode)
+    cfg = {"iter": 40, "learning_rate": 0.05, "ratio": 0.8, "loss_name": "entropy",
+           "optimizer_name": "AdamOptimizer", "net_type": "CNN",
+           "options": {"log_every": 10, "ckpt_every": 20, "batch_size": 16},
+           "net_config": {"middle_layer": [{"layer": "conv", "filter": [3, 3, 4]},
+                                           {"layer": "active", "active_func": "relu"},
+                                           {"layer": "pool"},
+                                           {"layer": "connect", "hidden": 16}], "output_layer": {}}}
+    r = client.post("/construct/construction/m1/file/", json=cfg, headers=h)
+    assert r.status_code == 200, r.text
+    jid = r.json()["job"]
+    assert client.app.state.jobs.wait(jid, 300) == "done"
+    res = client.get("/runtime/train/m1/40/", headers=h).json()
+    assert len(res["every_result"]) == 4 and 0.0 <= float(res["final_accuracy"]) <= 1.0
+    assert client.get("/construct/config/", headers=h).json() == ["m1"]
+    assert client.get("/construct/detail/m1/", headers=h).json()["iter"] == 40
+    assert client.get("/construct/detail/zz/", headers=h).status_code == 404
+    models = client.get("/models/", headers=h).json()
+    assert models[0]["name"] == "m1" and models[0]["state"] == "done"
+    assert client.get("/models/m1/", headers=h).json()["job"]["state"] == "done"
+    assert "m1" in client.get("/models/compare/", params={"models": "m1"}, headers=h).json()
+    assert len(client.get("/generation/run/details/", params={"modelName": "m1"}, headers=h).json()["metrics"]) >= 4
+    assert client.get("/generation/run/runtime/", params={"modelName": "m1"}, headers=h).json()["state"] == "done"
+    img = _png(ds.images[0].reshape(28, 28))
+    r = _mp(client, "/construct/inference/m1/", {}, {"file": ("q.png", img, "image/png")}, h)
+    out = r.json()
+    assert out["result"] == "success" and out["message"] in list("0123456789")
+    r = _mp(client, "/construct/inference/none/", {}, {"file": ("q.png", img, "image/png")}, h)
+    assert r.json()["result"] == "fail"
+    node = client.get("/runtime/kubernetes/", headers=h).json()
+    assert {"Conditions", "Capacity", "Allocatable", "System Info", "Non-terminated Pods"} <= set(node)
+    assert client.delete("/models/m1/", headers=h).json() == {"message": "success"}
+    assert client.get("/models/", headers=h).json() == []
+
+
+def test_construct_rejects_bad_config(client):
+    h = _auth(client)
+    r = client.post("/construct/construction/m2/file/", json={"iter": 5, "net_config": {"middle_layer": [{"layer": "conv"}]}}, headers=h)
+    assert r.status_code == 400
+    r = client.post("/construct/construction/m2/ftp/", json={"iter": 5, "net_config": {"middle_layer": []}}, headers=h)
+    assert r.status_code == 400
