@@ -72,12 +72,25 @@ def load(path: str, map_location="cpu") -> Dict[str, Any]:
     return obj
 
 
+def full_slots(eng) -> torch.Tensor:
+    """Optimizer slots for the WHOLE flat buffer.  Under the sharded "ps" strategy each
+    rank owns a slice, so this is a collective (every rank must call it)."""
+    if eng.sync.strategy == "ps" and eng.ctx.enabled and eng.slots.numel():
+        import torch.distributed as dist
+        full = torch.empty(eng.slots.shape[0], eng.flat.numel(), device=eng.slots.device)
+        for i in range(eng.slots.shape[0]):
+            dist.all_gather_into_tensor(full[i], eng.slots[i].contiguous())
+        return full
+    return eng.slots
+
+
 def engine_state(eng) -> Dict[str, Any]:
-    """Everything needed to resume an engine exactly where it stopped."""
+    """Everything needed to resume an engine exactly where it stopped.  Collective under
+    the "ps" strategy: call on every rank, write on the chief."""
     st = eng.model.export_state()
     return {
         "model": st,
-        "slots": eng.slots.detach().cpu(),
+        "slots": full_slots(eng).detach().cpu(),
         "opt_id": int(eng.opt_id),
         "dstep": int(eng.dstep.item()),
         "host_step": int(eng.host_step),
@@ -88,8 +101,13 @@ def engine_state(eng) -> Dict[str, Any]:
 
 def restore_engine(eng, obj: Dict[str, Any]) -> None:
     eng.model.import_state(obj["model"])
-    if int(obj.get("opt_id", eng.opt_id)) == eng.opt_id and obj["slots"].shape == eng.slots.shape:
-        eng.slots.copy_(obj["slots"].to(eng.slots.device))
+    slots = obj["slots"]
+    if int(obj.get("opt_id", eng.opt_id)) == eng.opt_id and slots.shape[0] == eng.slots.shape[0]:
+        lo, hi = eng.sync.shard_range()
+        if slots.shape[1:] == eng.slots.shape[1:]:
+            eng.slots.copy_(slots.to(eng.slots.device))
+        elif slots.dim() == 2 and slots.shape[1] >= hi:      # full slots -> this rank's shard
+            eng.slots.copy_(slots[:, lo:hi].to(eng.slots.device))
     eng.dstep.fill_(int(obj.get("dstep", obj["step"])))
     eng.host_step = int(obj.get("host_step", obj["step"]))
     # re-seed the batch stream deterministically for the resumed position

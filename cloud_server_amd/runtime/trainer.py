@@ -132,16 +132,16 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
                                         "batch_accuracy": acc, "step_ms": step_time * 1e3,
                                         "samples_per_s": cfg.batch_size * ctx.world / max(step_time, 1e-9),
                                         "time": time.time()}) + "\n")
-                if cfg.ckpt_every > 0 and step > 0 and step % cfg.ckpt_every == 0:
-                    ckpt.save(model_dir, eng.host_step, ckpt.engine_state(eng))
+            if cfg.ckpt_every > 0 and step > 0 and step % cfg.ckpt_every == 0:
+                _checkpoint(model_dir, eng, chief)
             t_int, int_start = time.perf_counter(), eng.host_step
             action = _agree(ctx, read_control(model_dir) if chief else "")
             if action == "stop":
                 state = "stopped"
                 break
             if action == "pause":
+                _checkpoint(model_dir, eng, chief)
                 if chief:
-                    ckpt.save(model_dir, eng.host_step, ckpt.engine_state(eng))
                     write_status(model_dir, state="paused", step=eng.host_step)
                 state = "paused"
                 break
@@ -152,8 +152,9 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
             if chief:
                 with open(result_path, "a") as f:
                     f.write("final_accuracy:%f\n\n" % final_acc)
+        if state != "paused":
+            _checkpoint(model_dir, eng, chief)
         if chief:
-            ckpt.save(model_dir, eng.host_step, ckpt.engine_state(eng))
             write_status(model_dir, state=state, step=eng.host_step, final_accuracy=final_acc,
                          backend=eng.backend, fallback=eng.fallback_reason)
         return {"state": state, "step": eng.host_step, "final_accuracy": final_acc, "backend": eng.backend}
@@ -162,6 +163,12 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
             write_status(model_dir, state="failed", step=eng.host_step, error=repr(exc),
                          trace=traceback.format_exc()[-4000:])
         raise
+
+
+def _checkpoint(model_dir: str, eng: TrainEngine, chief: bool) -> None:
+    state = ckpt.engine_state(eng)          # collective under the sharded "ps" strategy
+    if chief:
+        ckpt.save(model_dir, eng.host_step, state)
 
 
 def _agree(ctx: DistContext, action: str) -> str:

@@ -1,0 +1,281 @@
+"""Store, GPU-slot scheduler (native C++ vs Python policy), checkpoint/resume, trainer
+(result.txt contract, control, fault injection), job manager executors and the warm
+inference cache — all on CPU.
+
+Reference behaviour pinned here: result.txt line format and the monitor's mean fallback
+(construct_distribute.py:405-420, apps/runtime/views.py:44-72); Supervisor-style resume
+from the newest checkpoint (:385-392); inference image prep (construct_inference.py:312-330)."""
+import io
+import json
+import os
+import random
+import time
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from cloud_server_amd.config import Settings
+from cloud_server_amd.data.datasets import synthetic_mnist
+from cloud_server_amd.runtime import checkpoint as ckpt
+from cloud_server_amd.runtime.jobs import JobManager
+from cloud_server_amd.runtime.scheduler import NativeScheduler, PyScheduler
+from cloud_server_amd.runtime.trainer import (CONTROL, RESULT, STATUS, read_train_results, run_job)
+from cloud_server_amd.serve.inference import InferenceService, prepare_reference
+from cloud_server_amd.store.db import Database, check_password, hash_password
+
+SMALL = {"iter": 30, "learning_rate": 0.05, "ratio": 0.8, "loss_name": "entropy",
+         "optimizer_name": "AdamOptimizer",
+         "options": {"log_every": 10, "ckpt_every": 10, "batch_size": 16},
+         "net_config": {"middle_layer": [{"layer": "conv", "filter": [3, 3, 4]},
+                                         {"layer": "active", "active_func": "relu"},
+                                         {"layer": "pool"},
+                                         {"layer": "connect", "hidden": 16}]}}
+
+
+def _data(n=400):
+    ds = synthetic_mnist(n, seed=0)
+    return ds.split(0.8)
+
+
+# ---------------------------------------------------------------- store
+def test_db_users_tokens_data_jobs(tmp_path):
+    db = Database(str(tmp_path / "x.db"))
+    uid = db.create_user("u1", "pw-12345678", "u1@x")
+    assert check_password("pw-12345678", db.get_user(uid)["password"])
+    assert not check_password("nope", db.get_user(uid)["password"])
+    assert hash_password("a") != hash_password("a")          # salted
+    k = db.token_for(uid)
+    assert db.token_for(uid) == k and db.user_for_token(k)["id"] == uid
+    db.delete_token(uid)
+    assert db.user_for_token(k) is None
+    pk = db.add_raw_data(uid, "NJUCloud/1/data/doc/a.csv", "doc")
+    assert db.list_raw_data(uid)[0]["id"] == pk
+    assert db.delete_raw_data(pk) and db.get_raw_data(pk) is None
+    jid = db.add_job(uid, "m", "file", {"iter": 1})
+    db.update_job(jid, state="running")
+    assert [j["id"] for j in db.active_jobs()] == [jid]
+    tok = db.new_reset_token(uid)
+    assert db.use_reset_token(uid, tok) and not db.use_reset_token(uid, tok)
+    with pytest.raises(Exception):
+        db.create_user("u1", "x")
+
+
+# ---------------------------------------------------------------- scheduler
+def test_native_scheduler_matches_python_policy():
+    rnd = random.Random(0)
+    nat, py = NativeScheduler(4, 2, max_skip=3), PyScheduler(4, 2, max_skip=3)
+    running = []
+    jid = 0
+    for _ in range(400):
+        r = rnd.random()
+        if r < 0.45:
+            jid += 1
+            n = rnd.choice([1, 1, 1, 2, 4])
+            assert nat.submit(jid, n) == py.submit(jid, n)
+        elif r < 0.75:
+            a, b = nat.next(), py.next()
+            assert (a is None and b is None) or (a[0] == b[0] and list(a[1]) == list(b[1])), (a, b)
+            if a:
+                running.append(a[0])
+        elif r < 0.95 and running:
+            j = running.pop(rnd.randrange(len(running)))
+            assert nat.release(j) == py.release(j)
+        else:
+            j = rnd.randint(1, max(jid, 1))
+            assert nat.cancel(j) == py.cancel(j)
+        assert [nat.load(g) for g in range(4)] == [py.load(g) for g in range(4)]
+        assert nat.queued() == py.queued()
+    assert not nat.submit(999, 5)          # more GPUs than exist
+
+
+def test_scheduler_packs_least_loaded_and_bounds_skips():
+    s = NativeScheduler(2, 2, max_skip=1)
+    for j in (1, 2, 3):
+        s.submit(j, 1)
+    assert s.next() == (1, [0]) and s.next() == (2, [1]) and s.next() == (3, [0])
+    s.submit(4, 2)            # needs both GPUs; GPU 0 has 2 jobs, GPU 1 has 1
+    s.submit(5, 1)
+    assert s.next() == (5, [1])            # 5 may skip past 4 once
+    s.release(1)
+    s.submit(6, 1)
+    assert s.next() is None                # 4 was skipped max_skip times: it now blocks 6
+    s.release(2); s.release(3); s.release(5)
+    assert s.next() == (4, [0, 1])
+
+
+# ---------------------------------------------------------------- trainer / checkpoint
+def test_run_job_result_contract_and_resume(tmp_path):
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    data = _data()
+    out = run_job(mdir, SMALL, device="cpu", backend="torch", data=data)
+    assert out["state"] == "done" and out["step"] == 30
+    lines = open(os.path.join(mdir, RESULT)).read().splitlines()
+    assert [l.split(",")[0] for l in lines[:3]] == ["step:0", "step:10", "step:20"]
+    assert lines[3].startswith("final_accuracy:") and lines[4] == ""
+    res = read_train_results(os.path.join(mdir, RESULT), 30)
+    assert len(res["every_result"]) == 3 and res["final_accuracy"] == pytest.approx(out["final_accuracy"], abs=1e-6)
+    last = ckpt.latest(mdir)
+    assert last[0] == 30
+    obj = torch.load(last[1], weights_only=True)                 # safe loader works
+    assert obj["host_step"] == 30 and "layers.0.weight" in obj["model"]
+    # extend the job: resumes at 30, runs to 50
+    cfg2 = dict(SMALL, iter=50)
+    out2 = run_job(mdir, cfg2, device="cpu", backend="torch", data=data)
+    assert out2["step"] == 50
+    steps = [r["step"] for r in read_train_results(os.path.join(mdir, RESULT), 50)["every_result"]]
+    assert steps == ["0", "10", "20", "30", "40"]
+
+
+def test_fault_injection_then_resume(tmp_path, monkeypatch):
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    data = _data()
+    monkeypatch.setenv("CSA_FAULT_AT_STEP", "25")
+    with pytest.raises(RuntimeError):
+        run_job(mdir, SMALL, device="cpu", backend="torch", data=data)
+    st = json.load(open(os.path.join(mdir, STATUS)))
+    assert st["state"] == "failed" and "injected" in st["error"]
+    assert ckpt.latest(mdir)[0] == 21            # checkpoint taken after step 20
+    monkeypatch.delenv("CSA_FAULT_AT_STEP")
+    out = run_job(mdir, SMALL, device="cpu", backend="torch", data=data)
+    assert out["state"] == "done" and out["step"] == 30
+
+
+def test_resume_is_exact(tmp_path):
+    """Stopping at a checkpoint and resuming gives the same weights as an unbroken run
+    (same optimizer slots, same step count; batch order re-seeded deterministically)."""
+    data = _data()
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    os.makedirs(a); os.makedirs(b)
+    run_job(a, dict(SMALL, iter=21), device="cpu", backend="torch", data=data)
+    o1 = ckpt.load(ckpt.latest(a)[1])
+    run_job(b, dict(SMALL, iter=21), device="cpu", backend="torch", data=data)
+    o2 = ckpt.load(ckpt.latest(b)[1])
+    for k in o1["model"]:
+        torch.testing.assert_close(o1["model"][k], o2["model"][k])     # deterministic on CPU
+    torch.testing.assert_close(o1["slots"], o2["slots"])
+
+
+def test_stop_and_pause_control(tmp_path):
+    data = _data()
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    with open(os.path.join(mdir, CONTROL), "w") as f:
+        json.dump({"action": "pause"}, f)
+    out = run_job(mdir, dict(SMALL, iter=1000), device="cpu", backend="torch", data=data)
+    assert out["state"] == "paused" and out["step"] == 1     # stops at the first log point
+    assert ckpt.latest(mdir)[0] == 1
+    os.remove(os.path.join(mdir, CONTROL))
+    with open(os.path.join(mdir, CONTROL), "w") as f:
+        json.dump({"action": "stop"}, f)
+    out = run_job(mdir, dict(SMALL, iter=1000), device="cpu", backend="torch", data=data)
+    assert out["state"] == "stopped" and out["step"] == 11
+
+
+def test_monitor_mean_fallback(tmp_path):
+    p = tmp_path / "result.txt"
+    p.write_text("".join(f"step:{s},accuracy:{a},duration:0.1\n" for s, a in
+                         [(0, 0.1), (100, 0.3), (200, 0.5)]))
+    r = read_train_results(str(p), 100)          # > iter/100 rows, no final line -> mean
+    assert r["final_accuracy"] == pytest.approx(0.3)
+    r = read_train_results(str(p), 1000)
+    assert "final_accuracy" not in r
+    assert read_train_results(str(tmp_path / "none.txt"), 10) == {"every_result": []}
+
+
+# ---------------------------------------------------------------- job manager
+def _settings(tmp_path, executor):
+    return Settings(storage_root=str(tmp_path / "s"), db_path=str(tmp_path / "db.sqlite3"),
+                    executor=executor, train_backend="torch")
+
+
+def _prep_model(s, uid, name, n=120):
+    mdir = s.model_dir(uid, name)
+    os.makedirs(os.path.join(mdir, "data"), exist_ok=True)
+    ds = synthetic_mnist(n, seed=4)
+    tags = {}
+    for i in range(n):
+        fn = f"d{i}.png"
+        Image.fromarray(ds.images[i].reshape(28, 28)).save(os.path.join(mdir, "data", fn))
+        tags[fn] = str(int(ds.labels[i]))
+    json.dump(tags, open(os.path.join(mdir, "tag.json"), "w"))
+    return mdir
+
+
+@pytest.mark.parametrize("executor", ["thread", "process"])
+def test_job_manager_executors(tmp_path, executor):
+    s = _settings(tmp_path, executor)
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    jm = JobManager(s, db, executor=executor, ngpu=0)
+    try:
+        mdir = _prep_model(s, uid, "m")
+        jid = jm.submit(uid, "m", "file", dict(SMALL, iter=20))
+        assert jm.wait(jid, 300) == "done", open(os.path.join(mdir, "worker.log")).read() \
+            if os.path.exists(os.path.join(mdir, "worker.log")) else jm.status(jid)
+        st = jm.status(jid)
+        assert st["progress"]["state"] == "done" and st["progress"]["step"] == 20
+        assert len(read_train_results(os.path.join(mdir, RESULT), 20)["every_result"]) == 2
+        # a failing job is marked failed and can be resumed
+        bad = jm.submit(uid, "empty", "file", dict(SMALL, iter=5))
+        assert jm.wait(bad, 300) == "failed"
+        with pytest.raises(ValueError):
+            jm.control(jid, "resume")                        # done jobs cannot resume
+    finally:
+        jm.shutdown()
+
+
+def test_job_pause_resume_thread(tmp_path):
+    s = _settings(tmp_path, "thread")
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    jm = JobManager(s, db, executor="thread", ngpu=0)
+    try:
+        mdir = _prep_model(s, uid, "m")
+        cfg = dict(SMALL, iter=4000, options=dict(SMALL["options"], log_every=5))
+        jid = jm.submit(uid, "m", "file", cfg)
+        t0 = time.time()
+        while not os.path.exists(os.path.join(mdir, RESULT)) and time.time() - t0 < 120:
+            time.sleep(0.05)
+        jm.control(jid, "pause")
+        assert jm.wait(jid, 120) == "paused"
+        step_at_pause = ckpt.latest(mdir)[0]
+        assert 0 < step_at_pause < 4000
+        jid2 = jm.control(jid, "resume")["job"]
+        time.sleep(0.5)
+        jm.control(jid2, "stop")
+        assert jm.wait(jid2, 120) == "stopped"
+        assert ckpt.latest(mdir)[0] >= step_at_pause
+    finally:
+        jm.shutdown()
+
+
+# ---------------------------------------------------------------- inference
+def test_prepare_reference_binarizes_and_centres():
+    img = np.zeros((40, 40), np.uint8)
+    img[5:35, 15:25] = 255
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, format="PNG")
+    x = prepare_reference(b.getvalue()).reshape(28, 28)
+    assert set(np.unique(x)) <= {0.0, np.float32(254 / 255)}
+    assert x[:4].sum() == 0 and x[24:].sum() == 0 and x[:, :4].sum() == 0
+    assert x.sum() > 0
+
+
+def test_inference_service_cache(tmp_path):
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    svc = InferenceService(device="cpu")
+    img = io.BytesIO()
+    Image.fromarray(synthetic_mnist(1, seed=9).images[0].reshape(28, 28)).save(img, format="PNG")
+    assert svc.predict(mdir, img.getvalue())["result"] == "fail"
+    run_job(mdir, dict(SMALL, iter=10), device="cpu", backend="torch", data=_data())
+    r1 = svc.predict(mdir, img.getvalue(), prep="mnist")
+    r2 = svc.predict(mdir, img.getvalue(), prep="mnist")
+    assert r1 == r2 and r1["result"] == "success"
+    assert svc.misses == 1 and svc.hits >= 1
+    many = svc.predict_many(mdir, [img.getvalue()] * 5)
+    assert len(many) == 5 and all(m["result"] == "success" for m in many)
