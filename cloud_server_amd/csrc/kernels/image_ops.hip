@@ -1,0 +1,422 @@
+// Batched image-preprocessing kernels (gfx950 / CDNA4) over uint8 [N, H, W] batches.
+//
+// Reference: apps/preprocess/preprocess.py:18-227 runs one OpenCV call per image per op
+// on the CPU, re-reading and re-writing a JPEG every time (views.py:95-137).  Here the
+// whole labelled set lives on the device as one uint8 tensor and each op is one launch
+// over the batch.  Numerics follow the spec'd NumPy reference (preprocess/ops_ref.py):
+// border modes REFLECT_101 (linear filters, CLAHE padding, NL-means), REPLICATE
+// (median, resize), "ignore outside" (erode/dilate); rounding = rint (half-even) then
+// saturate, done in double where the reference rounds a double, so results are
+// bit-identical except NL-means/resize (float exp / tap order: |diff| <= 1).
+//
+// Layout: most ops use one workgroup (256 threads = 4 waves) per image, the image
+// staged once in LDS; 28x28 digit batches give N workgroups, so a 1k-image batch
+// already fills all 256 CUs several times over.  Elementwise ops are grid-stride.
+#include "common.h"
+
+// Bit-parity with the NumPy reference: no FMA contraction of the double arithmetic here
+// (the library is built with -ffp-contract=fast-honor-pragmas for the training kernels).
+#pragma clang fp contract(off)
+
+namespace csa {
+
+constexpr int IMG_THREADS = 256;
+constexpr int MAX_IMG_PIX = 128 * 128;       // LDS-resident image limit (H*W)
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+__device__ __forceinline__ int clampi(int i, int n) { return i < 0 ? 0 : (i >= n ? n - 1 : i); }
+__device__ __forceinline__ uint8_t sat_rint(double v) {
+  v = rint(v);
+  return (uint8_t)(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
+}
+
+// ------------------------------------------------------------------ flips (P0-P2)
+// mode 0: up-down, 1: left-right, 2: both (the reference "transpose" = cv2.flip(-1))
+__global__ __launch_bounds__(256) void flip_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                   long total, int H, int W, int mode) {
+  const long HW = (long)H * W;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / HW;
+    const int r = (int)(i - n * HW);
+    const int y = r / W, x = r - (r / W) * W;
+    const int sy = (mode == 1) ? y : H - 1 - y;
+    const int sx = (mode == 0) ? x : W - 1 - x;
+    out[i] = in[n * HW + (long)sy * W + sx];
+  }
+}
+
+// ------------------------------------------------------------------ affine intensity (P3/P4)
+// y = x * alpha[n] + beta[n]; saturate (rint+clip) or wrap (trunc mod 256, numpy uint8
+// element assignment in the reference loop).  Per-image alpha/beta let the random
+// variant draw on the host with the reference RNG call order.
+__global__ __launch_bounds__(256) void affine_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                     long total, long HW, const double* __restrict__ alpha,
+                                                     const double* __restrict__ beta, int wrap) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / HW;
+    const double v = (double)in[i] * alpha[n] + beta[n];
+    if (wrap) {
+      long t = (long)trunc(v) % 256;
+      out[i] = (uint8_t)(t < 0 ? t + 256 : t);
+    } else {
+      out[i] = sat_rint(v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ separable filters (P5/P6)
+// Box / Gaussian: rows then columns with REFLECT_101, double accumulation in LDS.
+// Taps at offsets -k/2 .. k-1-k/2 (even box sizes too, as the reference's cv2.blur).
+__global__ __launch_bounds__(IMG_THREADS) void sep_filter_kernel(const uint8_t* __restrict__ in,
+                                                                 uint8_t* __restrict__ out, int H, int W,
+                                                                 const double* __restrict__ taps, int k) {
+  extern __shared__ double s_tmp[];                      // [H*W] row-filtered
+  __shared__ double s_k[32];
+  const long base = (long)blockIdx.x * H * W;
+  const int HW = H * W, r = k / 2;
+  if (threadIdx.x < k) s_k[threadIdx.x] = taps[threadIdx.x];
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) {
+    const int y = p / W, x = p - y * W;
+    double acc = 0.0;
+    for (int i = 0; i < k; ++i) acc += s_k[i] * (double)in[base + (long)y * W + reflect101(x + i - r, W)];
+    s_tmp[p] = acc;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) {
+    const int y = p / W, x = p - y * W;
+    double acc = 0.0;
+    for (int i = 0; i < k; ++i) acc += s_k[i] * s_tmp[reflect101(y + i - r, H) * W + x];
+    out[base + p] = sat_rint(acc);
+  }
+}
+
+// ------------------------------------------------------------------ rank filters (P7, P12, P13)
+// op 0: median (REPLICATE border), 1: erode (min over in-bounds), 2: dilate (max).
+__global__ __launch_bounds__(IMG_THREADS) void rank_filter_kernel(const uint8_t* __restrict__ in,
+                                                                  uint8_t* __restrict__ out, int H, int W,
+                                                                  int k, int op) {
+  extern __shared__ uint8_t s_img[];
+  const long base = (long)blockIdx.x * H * W;
+  const int HW = H * W, r = k / 2;
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) s_img[p] = in[base + p];
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) {
+    const int y = p / W, x = p - y * W;
+    if (op == 0) {
+      // median of k*k (k <= 7): histogram-free rank selection over a register window
+      uint8_t v[49];
+      int n = 0;
+      for (int dy = -r; dy <= r; ++dy)
+        for (int dx = -r; dx <= r; ++dx) v[n++] = s_img[clampi(y + dy, H) * W + clampi(x + dx, W)];
+      const int m = n / 2;
+      int med = 0;
+      for (int i = 0; i < n; ++i) {
+        int lt = 0, le = 0;
+        for (int j = 0; j < n; ++j) { lt += v[j] < v[i]; le += v[j] <= v[i]; }
+        if (lt <= m && m < le) { med = v[i]; break; }
+      }
+      out[base + p] = (uint8_t)med;
+    } else {
+      int acc = op == 1 ? 255 : 0;
+      for (int dy = -r; dy < k - r; ++dy) {            // k x k window at offset -k/2 (even k too)
+        const int yy = y + dy;
+        if (yy < 0 || yy >= H) continue;
+        for (int dx = -r; dx < k - r; ++dx) {
+          const int xx = x + dx;
+          if (xx < 0 || xx >= W) continue;
+          const int s = s_img[yy * W + xx];
+          acc = op == 1 ? min(acc, s) : max(acc, s);
+        }
+      }
+      out[base + p] = (uint8_t)acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ histogram equalisation (P10)
+__global__ __launch_bounds__(IMG_THREADS) void equalize_kernel(const uint8_t* __restrict__ in,
+                                                               uint8_t* __restrict__ out, int HW) {
+  __shared__ unsigned s_hist[256];
+  __shared__ uint8_t s_lut[256];
+  __shared__ int s_copy;
+  const long base = (long)blockIdx.x * HW;
+  s_hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) atomicAdd(&s_hist[in[base + p]], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int first = -1, nz = 0;
+    for (int b = 0; b < 256; ++b)
+      if (s_hist[b]) { nz++; if (first < 0) first = b; }
+    s_copy = (nz <= 1);
+    if (!s_copy) {
+      const unsigned cmin = s_hist[first];
+      const double scale = 255.0 / (double)(HW - (int)cmin);
+      unsigned cdf = 0;
+      for (int b = 0; b < 256; ++b) {
+        cdf += s_hist[b];
+        double v = rint(((double)cdf - (double)cmin) * scale);
+        v = v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v);
+        s_lut[b] = b < first ? 0 : (uint8_t)v;
+      }
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) {
+    const uint8_t v = in[base + p];
+    out[base + p] = s_copy ? v : s_lut[v];
+  }
+}
+
+// ------------------------------------------------------------------ CLAHE (P11)
+// tiles x tiles grid (<= 8x8); tile histograms of the REFLECT_101-padded image in LDS,
+// clip + uniform redistribution + residual stride, cdf LUTs, bilinear blend per pixel.
+constexpr int CLAHE_MAX_TILES = 8;
+__global__ __launch_bounds__(IMG_THREADS) void clahe_kernel(const uint8_t* __restrict__ in,
+                                                            uint8_t* __restrict__ out, int H, int W,
+                                                            int tiles, int clip) {
+  extern __shared__ unsigned s_h[];                      // [tiles*tiles][256] hist, then LUT
+  const long base = (long)blockIdx.x * H * W;
+  const int th = (H + tiles - 1) / tiles, tw = (W + tiles - 1) / tiles;
+  const int PH = th * tiles, PW = tw * tiles, T = tiles * tiles;
+  for (int i = threadIdx.x; i < T * 256; i += IMG_THREADS) s_h[i] = 0;
+  __syncthreads();
+  for (int p = threadIdx.x; p < PH * PW; p += IMG_THREADS) {
+    const int y = p / PW, x = p - y * PW;
+    const uint8_t v = in[base + (long)reflect101(y, H) * W + reflect101(x, W)];
+    atomicAdd(&s_h[((y / th) * tiles + x / tw) * 256 + v], 1u);
+  }
+  __syncthreads();
+  const double lut_scale = 255.0 / (double)(th * tw);
+  for (int t = threadIdx.x; t < T; t += IMG_THREADS) {
+    unsigned* h = s_h + t * 256;
+    if (clip > 0) {
+      long excess = 0;
+      for (int b = 0; b < 256; ++b)
+        if ((int)h[b] > clip) { excess += (int)h[b] - clip; h[b] = clip; }
+      const int add = (int)(excess / 256);
+      int resid = (int)(excess % 256);
+      for (int b = 0; b < 256; ++b) h[b] += add;
+      if (resid) {
+        const int step = max(256 / resid, 1);
+        for (int b = 0; b < 256 && resid > 0; b += step) { h[b] += 1; --resid; }
+      }
+    }
+    unsigned cdf = 0;
+    for (int b = 0; b < 256; ++b) {
+      cdf += h[b];
+      double v = rint((double)cdf * lut_scale);
+      h[b] = (unsigned)(v > 255.0 ? 255.0 : v);         // LUT in place
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < H * W; p += IMG_THREADS) {
+    const int y = p / W, x = p - y * W;
+    const double ys = (y + 0.5) / th - 0.5, xs = (x + 0.5) / tw - 0.5;
+    int y0 = (int)floor(ys), x0 = (int)floor(xs);
+    const double fy = ys - y0, fx = xs - x0;
+    int y1 = min(max(y0 + 1, 0), tiles - 1), x1 = min(max(x0 + 1, 0), tiles - 1);
+    y0 = min(max(y0, 0), tiles - 1);
+    x0 = min(max(x0, 0), tiles - 1);
+    const int v = in[base + p];
+    const double l00 = s_h[(y0 * tiles + x0) * 256 + v], l01 = s_h[(y0 * tiles + x1) * 256 + v];
+    const double l10 = s_h[(y1 * tiles + x0) * 256 + v], l11 = s_h[(y1 * tiles + x1) * 256 + v];
+    const double res = (l00 * (1 - fx) + l01 * fx) * (1 - fy) + (l10 * (1 - fx) + l11 * fx) * fy;
+    out[base + p] = sat_rint(res);
+  }
+}
+
+// ------------------------------------------------------------------ non-local means (P8)
+// w(p,q) = exp(-max(0, d2)/h^2), d2 = mean squared 7x7 template difference (exact int
+// sum), 21x21 search window, REFLECT_101 padding staged once in LDS.
+__global__ __launch_bounds__(IMG_THREADS) void nlmeans_kernel(const uint8_t* __restrict__ in,
+                                                              uint8_t* __restrict__ out, int H, int W,
+                                                              double inv_h2, int tr, int sr) {
+  extern __shared__ uint8_t s_p[];
+  const int pad = tr + sr, PW = W + 2 * pad, PH = H + 2 * pad;
+  const long base = (long)blockIdx.x * H * W;
+  for (int p = threadIdx.x; p < PH * PW; p += IMG_THREADS) {
+    const int y = p / PW, x = p - y * PW;
+    s_p[p] = in[base + (long)reflect101(y - pad, H) * W + reflect101(x - pad, W)];
+  }
+  __syncthreads();
+  const double inv_t2 = 1.0 / (double)((2 * tr + 1) * (2 * tr + 1));
+  for (int p = threadIdx.x; p < H * W; p += IMG_THREADS) {
+    const int y = p / W + pad, x = p - (p / W) * W + pad;
+    double acc = 0.0, wsum = 0.0;
+    for (int dy = -sr; dy <= sr; ++dy) {
+      for (int dx = -sr; dx <= sr; ++dx) {
+        int s = 0;
+        for (int ty = -tr; ty <= tr; ++ty) {
+          const uint8_t* a = s_p + (y + ty) * PW + x - tr;
+          const uint8_t* b = s_p + (y + dy + ty) * PW + x + dx - tr;
+          for (int tx = 0; tx <= 2 * tr; ++tx) {
+            const int d = (int)a[tx] - (int)b[tx];
+            s += d * d;
+          }
+        }
+        const double w = exp(-(double)s * inv_t2 * inv_h2);
+        acc += w * (double)s_p[(y + dy) * PW + x + dx];
+        wsum += w;
+      }
+    }
+    out[base + p] = sat_rint(acc / wsum);
+  }
+}
+
+// ------------------------------------------------------------------ salt & pepper (P9)
+// Coordinates are drawn on the host with the reference RNG order; per image: all salt
+// (255) writes, barrier, then all pepper (0) writes.  Operates in place on ``img``.
+__global__ __launch_bounds__(IMG_THREADS) void salt_pepper_kernel(uint8_t* __restrict__ img, int H, int W,
+                                                                  const int* __restrict__ coords, int m) {
+  const long base = (long)blockIdx.x * H * W;
+  const int* c = coords + (long)blockIdx.x * 4 * m;      // [ys_salt, xs_salt, ys_pep, xs_pep]
+  for (int i = threadIdx.x; i < m; i += IMG_THREADS) img[base + (long)c[i] * W + c[m + i]] = 255;
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += IMG_THREADS) img[base + (long)c[2 * m + i] * W + c[3 * m + i]] = 0;
+}
+
+// ------------------------------------------------------------------ bicubic resize (P14)
+// Separable 4-tap tables (index clamped = REPLICATE, a = -0.75) computed on the host.
+__global__ __launch_bounds__(IMG_THREADS) void resize_kernel(const uint8_t* __restrict__ in,
+                                                             uint8_t* __restrict__ out, int h, int w, int S,
+                                                             const int* __restrict__ iy, const double* __restrict__ wy,
+                                                             const int* __restrict__ ix, const double* __restrict__ wx) {
+  extern __shared__ double s_rows[];                     // [S][w] row pass
+  const long ib = (long)blockIdx.x * h * w, ob = (long)blockIdx.x * S * S;
+  for (int p = threadIdx.x; p < S * w; p += IMG_THREADS) {
+    const int oy = p / w, x = p - oy * w;
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc += (double)in[ib + (long)iy[oy * 4 + t] * w + x] * wy[oy * 4 + t];
+    s_rows[p] = acc;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < S * S; p += IMG_THREADS) {
+    const int oy = p / S, ox = p - oy * S;
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc += s_rows[oy * w + ix[ox * 4 + t]] * wx[ox * 4 + t];
+    out[ob + p] = sat_rint(acc);
+  }
+}
+
+// ------------------------------------------------------------------ inference prep (C28)
+// [N, 20, 20] grayscale (already bicubic-resized by the decoder) -> [N, 784] float:
+// centred in a 28x28 canvas at offset 4, > 150 -> 254 else 0, / 255
+// (construct_inference.py:312-330).
+__global__ __launch_bounds__(256) void infer_prep_kernel(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                                         long total) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / 784;
+    const int r = (int)(i - n * 784), y = r / 28 - 4, x = r % 28 - 4;
+    float v = 0.f;
+    if (y >= 0 && y < 20 && x >= 0 && x < 20) v = in[n * 400 + y * 20 + x] > 150 ? 254.f / 255.f : 0.f;
+    out[i] = v;
+  }
+}
+
+static unsigned grid_for(long total) {
+  long g = (total + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+static bool big_lds(const void* fn) {
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;
+}
+
+}  // namespace csa
+
+using namespace csa;
+
+CSA_API int csa_img_flip(const uint8_t* in, uint8_t* out, int N, int H, int W, int mode, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || mode < 0 || mode > 2 || in == out) return -1;
+  const long total = (long)N * H * W;
+  hipLaunchKernelGGL(flip_kernel, dim3(grid_for(total)), dim3(256), 0, st, in, out, total, H, W, mode);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_affine(const uint8_t* in, uint8_t* out, int N, int H, int W, const double* alpha,
+                           const double* beta, int wrap, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0) return -1;
+  const long total = (long)N * H * W;
+  hipLaunchKernelGGL(affine_kernel, dim3(grid_for(total)), dim3(256), 0, st, in, out, total, (long)H * W,
+                     alpha, beta, wrap);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_sep_filter(const uint8_t* in, uint8_t* out, int N, int H, int W, const double* taps, int k,
+                               hipStream_t st) {
+  if (N <= 0 || H * W > MAX_IMG_PIX / 2 || k < 1 || k > 31 || in == out) return -1;
+  static bool attr = big_lds((const void*)sep_filter_kernel);
+  (void)attr;
+  hipLaunchKernelGGL(sep_filter_kernel, dim3(N), dim3(IMG_THREADS), sizeof(double) * H * W, st, in, out, H, W,
+                     taps, k);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_rank_filter(const uint8_t* in, uint8_t* out, int N, int H, int W, int k, int op,
+                                hipStream_t st) {
+  if (N <= 0 || H * W > MAX_IMG_PIX || k < 1 || op < 0 || op > 2 || in == out) return -1;
+  if (op == 0 && (k > 7 || (k & 1) == 0)) return -1;
+  hipLaunchKernelGGL(rank_filter_kernel, dim3(N), dim3(IMG_THREADS), H * W, st, in, out, H, W, k, op);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_equalize(const uint8_t* in, uint8_t* out, int N, int H, int W, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0) return -1;
+  hipLaunchKernelGGL(equalize_kernel, dim3(N), dim3(IMG_THREADS), 0, st, in, out, H * W);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_clahe(const uint8_t* in, uint8_t* out, int N, int H, int W, int tiles, float clip_limit,
+                          hipStream_t st) {
+  if (N <= 0 || tiles < 1 || tiles > CLAHE_MAX_TILES || H < tiles || W < tiles || in == out) return -1;
+  const int th = (H + tiles - 1) / tiles, tw = (W + tiles - 1) / tiles;
+  const int c0 = (int)((double)clip_limit * th * tw / 256.0);
+  const int clip = clip_limit > 0.f ? (c0 > 1 ? c0 : 1) : 0;
+  static bool attr = big_lds((const void*)clahe_kernel);
+  (void)attr;
+  hipLaunchKernelGGL(clahe_kernel, dim3(N), dim3(IMG_THREADS), sizeof(unsigned) * tiles * tiles * 256, st, in, out,
+                     H, W, tiles, clip);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_nlmeans(const uint8_t* in, uint8_t* out, int N, int H, int W, float h, int template_size,
+                            int search_size, hipStream_t st) {
+  const int tr = template_size / 2, sr = search_size / 2;
+  if (N <= 0 || h <= 0.f || (H + 2 * (tr + sr)) * (W + 2 * (tr + sr)) > MAX_IMG_PIX || in == out) return -1;
+  const int pad = tr + sr;
+  hipLaunchKernelGGL(nlmeans_kernel, dim3(N), dim3(IMG_THREADS), (H + 2 * pad) * (W + 2 * pad), st, in, out, H, W,
+                     1.0 / ((double)h * (double)h), tr, sr);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_salt_pepper(uint8_t* img, int N, int H, int W, const int* coords, int m, hipStream_t st) {
+  if (N <= 0 || m < 0) return -1;
+  if (m == 0) return 0;
+  hipLaunchKernelGGL(salt_pepper_kernel, dim3(N), dim3(IMG_THREADS), 0, st, img, H, W, coords, m);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_resize(const uint8_t* in, uint8_t* out, int N, int h, int w, int S, const int* iy,
+                           const double* wy, const int* ix, const double* wx, hipStream_t st) {
+  if (N <= 0 || S <= 0 || (long)S * w * 8 > 150 * 1024) return -1;
+  static bool attr = big_lds((const void*)resize_kernel);
+  (void)attr;
+  hipLaunchKernelGGL(resize_kernel, dim3(N), dim3(IMG_THREADS), sizeof(double) * S * w, st, in, out, h, w, S, iy, wy,
+                     ix, wx);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_infer_prep(const uint8_t* in, float* out, int N, hipStream_t st) {
+  if (N <= 0) return -1;
+  const long total = (long)N * 784;
+  hipLaunchKernelGGL(infer_prep_kernel, dim3(grid_for(total)), dim3(256), 0, st, in, out, total);
+  return (int)hipGetLastError();
+}

@@ -60,7 +60,7 @@ def _run(cmd: List[str], verbose: bool) -> None:
 def build_kernels(verbose: bool = False, force: bool = False) -> str:
     srcs = _sources("kernels", (".hip",))
     hdrs = _sources("kernels", (".h",))
-    flags = ["-O3", "-fPIC", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=fast",
+    flags = ["-O3", "-fPIC", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=fast-honor-pragmas",
              "-Wno-unused-result"]
     stamp = _hash(srcs + hdrs, " ".join(flags))
     stamp_file = KERNEL_LIB + ".stamp"

@@ -1,0 +1,92 @@
+"""Platform on the MI355X: a training job through the trainer (HIP kernels, HIP graph),
+the job manager's process executor placing a worker on the GPU, the warm inference
+cache on the device, and the reference's 99-image fixture end to end."""
+import json
+import os
+import zipfile
+
+import numpy as np
+import pytest
+import torch
+
+from cloud_server_amd.config import Settings
+from cloud_server_amd.data.datasets import load_user_data, synthetic_mnist
+from cloud_server_amd.models.dsl import SAMPLE_CONFIG
+from cloud_server_amd.runtime import checkpoint as ckpt
+from cloud_server_amd.runtime.trainer import RESULT, read_train_results, run_job
+from cloud_server_amd.serve.inference import InferenceService
+
+pytestmark = pytest.mark.gpu
+FIX = os.path.join(os.path.dirname(__file__), "fixtures")
+
+
+def _cfg(iters, **opts):
+    c = json.loads(json.dumps(SAMPLE_CONFIG))
+    c.update(iter=iters, learning_rate=0.01, optimizer_name="AdamOptimizer")
+    c["options"] = dict(log_every=100, ckpt_every=200, **opts)
+    return c
+
+
+def test_gpu_job_hip_backend_and_inference(tmp_path):
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    ds = synthetic_mnist(6000, seed=0)
+    out = run_job(mdir, _cfg(600), device="cuda:0", backend="hip", data=ds.split(0.9))
+    assert out["backend"] == "hip" and out["state"] == "done" and out["step"] == 600
+    res = read_train_results(os.path.join(mdir, RESULT), 600)
+    assert [r["step"] for r in res["every_result"]] == [str(s) for s in range(0, 600, 100)]
+    assert res["final_accuracy"] > 0.9
+    obj = ckpt.load(ckpt.latest(mdir)[1])
+    assert obj["host_step"] == 600
+    gpu = InferenceService(device="cuda:0")
+    cpu = InferenceService(device="cpu")
+    test = ds.split(0.9)[1]
+    x = test.images[:256].astype(np.float32) / 255.0
+    pg = gpu.predict_arrays(mdir, x)
+    pc = cpu.predict_arrays(mdir, x)
+    assert (pg == pc).mean() > 0.99
+    assert (pg == test.labels[:256]).mean() > 0.9
+
+
+def test_gpu_job_on_reference_fixture(tmp_path):
+    """The reference's 99 labelled digit JPEGs (test-data/) as a user dataset."""
+    mdir = str(tmp_path / "m")
+    os.makedirs(os.path.join(mdir, "data"))
+    with zipfile.ZipFile(os.path.join(FIX, "test-pics.zip")) as z:
+        z.extractall(os.path.join(mdir, "data"))
+    with open(os.path.join(FIX, "tag.json"), "rb") as f, open(os.path.join(mdir, "tag.json"), "wb") as g:
+        g.write(f.read())
+    out = run_job(mdir, _cfg(300), datatype="file", device="cuda:0", backend="hip")
+    assert out["state"] == "done" and out["backend"] == "hip"
+    ds = load_user_data(os.path.join(mdir, "data"), os.path.join(mdir, "tag.json"))
+    svc = InferenceService(device="cuda:0")
+    pred = svc.predict_arrays(mdir, ds.images[:79].astype(np.float32) / 255.0)
+    assert (pred == ds.labels[:79]).mean() > 0.9        # fits its training split
+
+
+def test_job_manager_process_executor_on_gpu(tmp_path):
+    from cloud_server_amd.runtime.jobs import JobManager
+    from cloud_server_amd.store.db import Database
+    from PIL import Image
+    s = Settings(storage_root=str(tmp_path / "s"), db_path=str(tmp_path / "db.sqlite3"),
+                 executor="process", train_backend="hip")
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    jm = JobManager(s, db, executor="process", ngpu=1)
+    try:
+        mdir = s.model_dir(uid, "m")
+        os.makedirs(os.path.join(mdir, "data"))
+        ds = synthetic_mnist(500, seed=3)
+        tags = {}
+        for i in range(500):
+            Image.fromarray(ds.images[i].reshape(28, 28)).save(os.path.join(mdir, "data", f"{i}.png"))
+            tags[f"{i}.png"] = str(int(ds.labels[i]))
+        json.dump(tags, open(os.path.join(mdir, "tag.json"), "w"))
+        jid = jm.submit(uid, "m", "file", _cfg(200))
+        state = jm.wait(jid, 400)
+        log = open(os.path.join(mdir, "worker.log")).read() if os.path.exists(os.path.join(mdir, "worker.log")) else ""
+        assert state == "done", log[-3000:]
+        st = jm.status(jid)
+        assert st["gpu"] == "0" and st["progress"]["backend"] == "hip"
+    finally:
+        jm.shutdown()
