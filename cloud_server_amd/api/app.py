@@ -95,6 +95,15 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
     app = FastAPI(title="cloud_server_amd", version="1.0", lifespan=lifespan)
     app.state.settings, app.state.db, app.state.jobs, app.state.infer = settings, db, jobs, infer
     max_bytes = settings.max_upload_mb << 20
+    if settings.cors_origins:
+        # settings.py:53-82: corsheaders with GET/POST/PUT/PATCH/DELETE/OPTIONS and the
+        # x-requested-with/content-type/accept/origin/authorization/x-csrftoken headers
+        from fastapi.middleware.cors import CORSMiddleware
+        app.add_middleware(CORSMiddleware, allow_origins=settings.cors_origins,
+                           allow_methods=["GET", "POST", "PUT", "PATCH", "DELETE", "OPTIONS"],
+                           allow_headers=["x-requested-with", "content-type", "accept", "origin",
+                                          "authorization", "x-csrftoken"])
+    _install_metrics(app, db)
 
     # ------------------------------------------------------------------ auth helpers
     def current_user(request: Request) -> Optional[Dict[str, Any]]:
@@ -721,7 +730,115 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         shutil.rmtree(settings.model_dir(u["id"], model), ignore_errors=True)
         return J({"message": "success"})
 
+    if settings.enable_demo:
+        _install_demo(app, db, need_user, current_user, form)
     return app
+
+
+def _install_metrics(app: FastAPI, db: Database) -> None:
+    """Prometheus text exposition at /metrics: request counts/latency per route and the
+    job table by state (the reference had print() only)."""
+    try:
+        import prometheus_client as prom
+    except ImportError:       # pragma: no cover
+        return
+    reg = prom.CollectorRegistry()
+    req = prom.Counter("csa_http_requests_total", "HTTP requests", ["method", "route", "status"], registry=reg)
+    lat = prom.Histogram("csa_http_request_seconds", "HTTP request latency", ["route"], registry=reg)
+    jobs_g = prom.Gauge("csa_jobs", "training jobs by state", ["state"], registry=reg)
+
+    @app.middleware("http")
+    async def _count(request: Request, call_next):
+        t0 = time.perf_counter()
+        resp = await call_next(request)
+        route = request.scope.get("route")
+        path = getattr(route, "path", "unmatched")
+        req.labels(request.method, path, str(resp.status_code)).inc()
+        lat.labels(path).observe(time.perf_counter() - t0)
+        return resp
+
+    @app.get("/metrics")
+    async def metrics():
+        counts: Dict[str, int] = {}
+        for (st,) in db.conn().execute("SELECT state FROM jobs").fetchall():
+            counts[st] = counts.get(st, 0) + 1
+        for st in ("queued", "running", "paused", "stopped", "failed", "done"):
+            jobs_g.labels(st).set(counts.get(st, 0))
+        return Response(prom.generate_latest(reg), media_type=prom.CONTENT_TYPE_LATEST)
+
+
+def _install_demo(app: FastAPI, db: Database, need_user, current_user, form) -> None:
+    """The reference's scaffolding "Bills" app (demo/*.py; its routes are commented out
+    in CloudServer/urls.py:25, so it is off unless CSA_ENABLE_DEMO=1).  Same paths:
+    GET/POST /demo/, GET /demo/search/?name=, GET/PUT/DELETE /demo/<pk>/ with the
+    owner-or-read-only rule of demo/permission.py:5-26."""
+
+    def bill_json(b):
+        return {k: b[k] for k in ("id", "goods", "price", "amount", "description", "owner")}
+
+    def parse(f, partial=False):
+        out = {}
+        try:
+            if "goods" in f or not partial:
+                g = str(f.get("goods", "")).strip()
+                if not g or len(g) > 100:
+                    raise ValueError("goods")
+                out["goods"] = g
+            if "price" in f or not partial:
+                out["price"] = float(f["price"])
+            if "amount" in f:
+                out["amount"] = int(f["amount"])
+            if "description" in f:
+                out["description"] = str(f["description"])[:100]
+        except (KeyError, TypeError, ValueError) as exc:
+            raise ValueError(str(exc))
+        return out
+
+    @app.get("/demo/")
+    async def bills_list(request: Request):
+        return J([bill_json(b) for b in db.list_bills()])
+
+    @app.post("/demo/")
+    async def bills_create(request: Request):
+        u, e = need_user(request)
+        if e:
+            return e
+        f, _, e = await form(request)
+        if e:
+            return e
+        try:
+            fields = parse(f)
+        except ValueError as exc:
+            return J({"detail": f"invalid field {exc}"}, 400)
+        return J(bill_json(db.get_bill(db.add_bill(u["id"], **fields))), 201)
+
+    @app.get("/demo/search/")
+    async def bills_search(request: Request):
+        return J([bill_json(b) for b in db.list_bills(request.query_params.get("name", ""))])
+
+    @app.api_route("/demo/{pk}/", methods=["GET", "PUT", "DELETE"])
+    async def bill_detail(pk: int, request: Request):
+        b = db.get_bill(pk)
+        if b is None:
+            return J({"detail": "Not found."}, 404)
+        if request.method == "GET":
+            return J(bill_json(b))
+        u, e = need_user(request)
+        if e:
+            return e
+        if u["id"] != b["owner_id"]:
+            return J({"detail": "You do not have permission to perform this action."}, 403)
+        if request.method == "DELETE":
+            db.delete_bill(pk)
+            return Response(status_code=204)
+        f, _, e = await form(request)
+        if e:
+            return e
+        try:
+            db.update_bill(pk, **parse(f))
+        except ValueError as exc:
+            return J({"detail": f"invalid field {exc}"}, 400)
+        return J(bill_json(db.get_bill(pk)))
 
 
 def _extract_zip(data: bytes, dest: str) -> None:

@@ -15,6 +15,9 @@ local defaults.
 | CSA_TOKEN_TTL_S       | 0 (never expires)               | auth token lifetime                   |
 | CSA_ALLOW_URL_FETCH   | 1                               | allow the ``url`` dataset type        |
 | CSA_MAX_UPLOAD_MB     | 512                             | request body limit                    |
+| CSA_CORS_ORIGINS      | (none)                          | comma list of allowed CORS origins ("*" = any) |
+| CSA_HEARTBEAT_S       | 900                             | a running job silent this long is killed + failed |
+| CSA_ENABLE_DEMO       | 0                               | mount the demo "bills" routes (off, as in the reference) |
 """
 from __future__ import annotations
 
@@ -39,6 +42,10 @@ class Settings:
     max_upload_mb: int = field(default_factory=lambda: int(_env("CSA_MAX_UPLOAD_MB", "512")))
     preprocess_backend: str = field(default_factory=lambda: _env("CSA_PREPROCESS_BACKEND", "auto"))
     train_backend: str = field(default_factory=lambda: _env("CSA_TRAIN_BACKEND", "auto"))
+    cors_origins: List[str] = field(default_factory=lambda: [o.strip() for o in _env("CSA_CORS_ORIGINS", "").split(",")
+                                                             if o.strip()])
+    heartbeat_s: float = field(default_factory=lambda: float(_env("CSA_HEARTBEAT_S", "900")))
+    enable_demo: bool = field(default_factory=lambda: _env("CSA_ENABLE_DEMO", "0") == "1")
 
     def __post_init__(self):
         if not self.db_path:

@@ -99,7 +99,7 @@ def read_idx(path: str) -> np.ndarray:
             raise ValueError(f"{path}: not a uint8 IDX file (magic {magic:#x})")
         ndim = magic & 0xFF
         dims = struct.unpack(">" + "I" * ndim, f.read(4 * ndim))
-        data = np.frombuffer(f.read(), dtype=np.uint8)
+        data = np.frombuffer(f.read(), dtype=np.uint8).copy()   # writable (torch.from_numpy)
     return data.reshape(dims)
 
 

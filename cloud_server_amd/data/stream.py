@@ -39,6 +39,7 @@ class BatchStream:
             raise ValueError("empty dataset")
         self.n, self.batch, self.chunk = n, batch, chunk
         self.rank, self.world = rank, world
+        self.seed = seed
         self.rng = np.random.default_rng(seed)   # identical on every rank -> same permutations
         self.pending = np.zeros(0, np.int64)
         self.rows = torch.zeros(chunk, batch, dtype=torch.int64, device=device)
@@ -58,6 +59,23 @@ class BatchStream:
         allidx = np.concatenate(parts)
         take, self.pending = allidx[:need], allidx[need:]
         return take[self.rank::self.world]
+
+    def seek(self, step: int) -> None:
+        """Position the stream so the next step is global step ``step`` of an unbroken
+        run (exact resume): step s always consumes positions [s*B*W, (s+1)*B*W) of the
+        permutation sequence, so replay the generator and drop what was consumed."""
+        self.rng = np.random.default_rng(self.seed)
+        self.pending = np.zeros(0, np.int64)
+        self.epochs = 0
+        skip = step * self.batch * self.world
+        while skip > 0:
+            p = self.rng.permutation(self.n)
+            self.epochs += 1
+            if skip < len(p):
+                self.pending = p[skip:]
+                break
+            skip -= len(p)
+        self.used = self.chunk            # next before_step() refills from here
 
     def refill(self) -> None:
         idx = self._next_indices(self.chunk * self.batch).reshape(self.chunk, self.batch)

@@ -110,7 +110,5 @@ def restore_engine(eng, obj: Dict[str, Any]) -> None:
             eng.slots.copy_(slots[:, lo:hi].to(eng.slots.device))
     eng.dstep.fill_(int(obj.get("dstep", obj["step"])))
     eng.host_step = int(obj.get("host_step", obj["step"]))
-    # re-seed the batch stream deterministically for the resumed position
-    eng.stream.rng = __import__("numpy").random.default_rng(eng.cfg.seed + 7919 * (eng.host_step + 1))
-    eng.stream.pending = eng.stream.pending[:0]
-    eng.stream.used = eng.stream.chunk
+    # continue the batch sequence exactly where the unbroken run would be
+    eng.stream.seek(eng.host_step)

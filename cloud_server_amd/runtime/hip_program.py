@@ -25,8 +25,9 @@ uses ``TorchProgram`` for that job.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -98,6 +99,56 @@ class HipProgram:
         self.zero_regions: List[torch.Tensor] = []
         self._collect_zero_regions()
         self._zero_now()
+        self._plan_grad_buckets()
+
+    # ------------------------------------------------------------------ DP overlap
+    def _plan_grad_buckets(self) -> None:
+        """Overlap the RCCL gradient all-reduce with the rest of the backward pass.
+
+        The flat buffer holds layers in DSL order with the head last, and backward runs
+        from the head down, so after unit k's backward every parameter of layer index
+        >= unit k's main layer is final: a growing contiguous SUFFIX of ``flat_grad``.
+        (A norm layer's scale/offset grads come from the route kernel of the conv unit
+        BEFORE it, so they join the suffix one unit later — the rule still holds.)
+        Each time the ready suffix has grown by >= ``min_bucket`` bytes it is all-reduced
+        on a side stream (captured into the same HIP graph) while the main stream keeps
+        computing conv gradients; the optimizer waits for the side stream.  With the
+        sample config that is one ~1 MB bucket (head+fc2) launched after fc2, the 8 MB
+        fc1 bucket launched right after fc1's weight gradient, and a small tail."""
+        e = self.e
+        self.overlap = (e.ctx.enabled and e.sync.strategy == "allreduce" and
+                        os.environ.get("CSA_DP_OVERLAP", "1") == "1")
+        self.bucket_at: Dict[object, tuple] = {}
+        if not self.overlap:
+            return
+        self.side = torch.cuda.Stream(e.device)
+        offs = e.model.state.offsets
+        end = e.flat.numel()
+
+        def frontier(layer_index: int) -> int:
+            c = [o for n, o in offs.items()
+                 if n.startswith("head.") or int(n.split(".")[1]) >= layer_index]
+            return min(c) if c else end
+
+        min_elems = int(os.environ.get("CSA_DP_MIN_BUCKET", str(512 << 10))) // 4
+        hi = end
+        points = [("head", frontier(10 ** 9))] + [(k, frontier(self.units[k].layer.index))
+                                                  for k in range(len(self.units) - 1, -1, -1)]
+        for i, (key, f) in enumerate(points):
+            last = i == len(points) - 1
+            lo = 0 if last else f
+            if hi - lo >= min_elems or (last and hi > lo):
+                self.bucket_at[key] = (lo, hi)
+                hi = lo
+
+    def _grad_ready(self, key) -> None:
+        b = self.bucket_at.get(key)
+        if b is None:
+            return
+        cur = torch.cuda.current_stream(self.e.device)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
 
     # ------------------------------------------------------------------ lowering
     def _lower(self) -> None:
@@ -332,6 +383,7 @@ class HipProgram:
             K.ptr(G["head.weight"]), K.ptr(G["head.bias"]), K.ptr(last.dy), None,
             K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(),
             K.ptr(cur), st), "head")
+        self._grad_ready("head")
 
         # ---------------- backward ----------------
         for k in range(len(self.units) - 1, -1, -1):
@@ -400,9 +452,13 @@ class HipProgram:
                     self._rc(lib.csa_conv_dgrad(
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
                         K.ptr(u.x), in_act, in_alpha, *bn, K.ptr(tf.bwd_slab), st), "conv_dgrad")
+            self._grad_ready(k)
 
         # ---------------- gradient sync + optimizer ----------------
-        e.after_backward_sync()
+        if self.overlap:
+            torch.cuda.current_stream(e.device).wait_stream(self.side)
+        else:
+            e.after_backward_sync()
         self._optimizer(st)
 
     def _optimizer(self, st) -> None:

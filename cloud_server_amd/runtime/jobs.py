@@ -22,6 +22,7 @@ import json
 import multiprocessing as mp
 import os
 import queue
+import signal
 import subprocess
 import sys
 import threading
@@ -39,6 +40,7 @@ TERMINAL = ("done", "stopped", "failed", "paused")
 def _launcher_main(req: "mp.Queue", resp: "mp.Queue") -> None:   # pragma: no cover - subprocess
     """Runs in a spawned helper that never initialises HIP: owns every worker Popen."""
     procs: Dict[int, subprocess.Popen] = {}
+    kill_at: Dict[int, float] = {}          # SIGTERM sent; SIGKILL the group after a grace period
     while True:
         try:
             msg = req.get(timeout=0.2)
@@ -54,12 +56,26 @@ def _launcher_main(req: "mp.Queue", resp: "mp.Queue") -> None:   # pragma: no co
             elif kind == "kill":
                 p = procs.get(msg[1])
                 if p is not None and p.poll() is None:
-                    p.terminate()
+                    try:
+                        os.killpg(p.pid, signal.SIGTERM)     # the worker's own session/group
+                    except OSError:
+                        p.terminate()
+                    kill_at[msg[1]] = time.time() + 15.0
             elif kind == "exit":
                 for p in procs.values():
                     if p.poll() is None:
                         p.terminate()
                 return
+        for jid, t in list(kill_at.items()):
+            p = procs.get(jid)
+            if p is None or p.poll() is not None:
+                kill_at.pop(jid, None)
+            elif time.time() > t:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    p.kill()
+                kill_at.pop(jid, None)
         for jid, p in list(procs.items()):
             rc = p.poll()
             if rc is not None:
@@ -183,17 +199,46 @@ class JobManager:
     def _recover(self) -> None:
         """Jobs left running by a previous server instance are marked failed (resumable)."""
         for j in self.db.active_jobs():
-            if j["id"] not in self.running:
+            if j["id"] not in self.running and j["state"] in ("queued", "running"):
                 self.db.update_job(j["id"], state="failed", error="server restarted", finished=time.time())
 
     def _loop(self) -> None:
+        last_watch = 0.0
         while not self._stop.is_set():
             try:
                 self._admit()
                 self._reap()
+                if time.time() - last_watch > 2.0:
+                    last_watch = time.time()
+                    self._watchdog()
             except Exception:   # pragma: no cover - keep the dispatcher alive
                 traceback.print_exc()
             time.sleep(0.05)
+
+    def _watchdog(self) -> None:
+        """Kill + fail a worker whose heartbeat (status.json, written at every log point)
+        is older than ``settings.heartbeat_s`` — a hung collective or kernel, or a dead
+        rank that left its peers blocked."""
+        if self._launcher is None:
+            return
+        limit = float(getattr(self.settings, "heartbeat_s", 0) or 0)
+        if limit <= 0:
+            return
+        now = time.time()
+        with self._lock:
+            items = [(jid, info) for jid, info in self.running.items() if info.get("state") == "running"]
+        for jid, info in items:
+            last = info.get("launched", now)
+            try:
+                with open(os.path.join(info["mdir"], STATUS)) as f:
+                    st = json.load(f)
+                last = max(last, float(st.get("heartbeat", 0)), float(st.get("updated", 0)))
+            except (OSError, ValueError, json.JSONDecodeError):
+                pass
+            if now - last > limit and not info.get("killed"):
+                info["killed"] = True
+                info["kill_reason"] = f"no heartbeat for {now - last:.0f}s"
+                self._req.put(("kill", jid))
 
     def _admit(self) -> None:
         while True:
@@ -244,6 +289,9 @@ class JobManager:
                     "--master-addr", "127.0.0.1", "--master-port", str(port)] + mod[1:]
         else:
             argv = [sys.executable] + mod + ["--device", "cpu" if self.use_cpu else "cuda:0"]
+        env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")   # RCCL errors/timeouts abort the rank
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        info["launched"] = time.time()
         self._req.put(("launch", jid, argv, env, mdir, os.path.join(mdir, "worker.log")))
 
     def _reap(self) -> None:
@@ -269,7 +317,10 @@ class JobManager:
                     state = s
             except (OSError, json.JSONDecodeError):
                 pass
-        self._finish(jid, state, None if state != "failed" else f"worker exit code {rc}")
+        err = None
+        if state == "failed":
+            err = (info or {}).get("kill_reason") or f"worker exit code {rc}"
+        self._finish(jid, state, err)
 
     def _finish(self, jid: int, state: str, error: Optional[str] = None) -> None:
         self.sched.release(jid)

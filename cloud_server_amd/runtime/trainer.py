@@ -101,7 +101,8 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
     last = ckpt.latest(model_dir)
     if last is not None:
         ckpt.restore_engine(eng, ckpt.load(last[1]))
-    fault_at = int(os.environ.get("CSA_FAULT_AT_STEP", "-1"))
+    fault_at = int(os.environ.get("CSA_FAULT_AT_STEP", "-1"))     # raise (crash) at this step
+    hang_at = int(os.environ.get("CSA_HANG_AT_STEP", "-1"))       # stop making progress (watchdog tests)
     result_path = os.path.join(model_dir, RESULT)
     metrics_path = os.path.join(model_dir, METRICS)
     log_every = max(1, cfg.log_every)
@@ -113,6 +114,9 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
             step = eng.host_step
             if step == fault_at:
                 raise RuntimeError(f"injected fault at step {step}")
+            if step == hang_at:
+                while True:
+                    time.sleep(1.0)
             eng.step()
             if step % log_every != 0:
                 continue
@@ -132,6 +136,7 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
                                         "batch_accuracy": acc, "step_ms": step_time * 1e3,
                                         "samples_per_s": cfg.batch_size * ctx.world / max(step_time, 1e-9),
                                         "time": time.time()}) + "\n")
+                write_status(model_dir, step=eng.host_step, heartbeat=time.time())   # watchdog liveness
             if cfg.ckpt_every > 0 and step > 0 and step % cfg.ckpt_every == 0:
                 _checkpoint(model_dir, eng, chief)
             t_int, int_start = time.perf_counter(), eng.host_step

@@ -72,6 +72,15 @@ CREATE TABLE IF NOT EXISTS email_keys (
   user_id INTEGER NOT NULL REFERENCES users(id) ON DELETE CASCADE,
   created REAL NOT NULL
 );
+CREATE TABLE IF NOT EXISTS bills (
+  id INTEGER PRIMARY KEY AUTOINCREMENT,
+  created REAL NOT NULL,
+  goods TEXT NOT NULL,
+  price REAL NOT NULL,
+  amount INTEGER NOT NULL DEFAULT 1,
+  description TEXT NOT NULL DEFAULT 'no description',
+  owner_id INTEGER NOT NULL REFERENCES users(id) ON DELETE CASCADE
+);
 CREATE INDEX IF NOT EXISTS raw_data_owner ON raw_data(owner_id, created_at);
 CREATE INDEX IF NOT EXISTS jobs_owner ON jobs(owner_id, model);
 """
@@ -265,3 +274,40 @@ class Database:
         rows = self.conn().execute(
             "SELECT * FROM jobs WHERE state IN ('queued','running','paused') ORDER BY id").fetchall()
         return [dict(r) for r in rows]
+
+    # ------------------------------------------------------------------ demo bills
+    # (demo/models.py:6-28 — the reference's scaffolding example, kept for parity)
+    def add_bill(self, owner: int, goods: str, price: float, amount: int = 1,
+                 description: str = "no description") -> int:
+        with self.tx() as c:
+            cur = c.execute("INSERT INTO bills(created, goods, price, amount, description, owner_id) "
+                            "VALUES (?,?,?,?,?,?)", (time.time(), goods, price, amount, description, owner))
+            return int(cur.lastrowid)
+
+    def _bill_rows(self, where: str = "", args=()) -> List[Dict[str, Any]]:
+        rows = self.conn().execute(
+            "SELECT b.*, u.username AS owner FROM bills b JOIN users u ON u.id = b.owner_id "
+            f"{where} ORDER BY b.created, b.owner_id", args).fetchall()
+        return [dict(r) for r in rows]
+
+    def list_bills(self, goods_contains: Optional[str] = None) -> List[Dict[str, Any]]:
+        if goods_contains is None:
+            return self._bill_rows()
+        return self._bill_rows("WHERE b.goods LIKE ? ESCAPE '\\'",
+                               ("%" + goods_contains.replace("\\", "\\\\").replace("%", "\\%")
+                                .replace("_", "\\_") + "%",))
+
+    def get_bill(self, pk: int) -> Optional[Dict[str, Any]]:
+        r = self._bill_rows("WHERE b.id=?", (pk,))
+        return r[0] if r else None
+
+    def update_bill(self, pk: int, **fields) -> None:
+        allowed = {k: v for k, v in fields.items() if k in ("goods", "price", "amount", "description")}
+        if allowed:
+            cols = ", ".join(f"{k}=?" for k in allowed)
+            with self.tx() as c:
+                c.execute(f"UPDATE bills SET {cols} WHERE id=?", (*allowed.values(), pk))
+
+    def delete_bill(self, pk: int) -> bool:
+        with self.tx() as c:
+            return c.execute("DELETE FROM bills WHERE id=?", (pk,)).rowcount > 0

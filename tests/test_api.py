@@ -233,3 +233,60 @@ def test_construct_rejects_bad_config(client):
     assert r.status_code == 400
     r = client.post("/construct/construction/m2/ftp/", json={"iter": 5, "net_config": {"middle_layer": []}}, headers=h)
     assert r.status_code == 400
+
+
+def test_metrics_cors_and_demo(tmp_path):
+    s = Settings(storage_root=str(tmp_path / "store"), db_path=str(tmp_path / "db.sqlite3"),
+                 executor="inline", train_backend="torch", cors_origins=["http://ui.example"], enable_demo=True)
+    with TestClient(create_app(s, executor="inline", ngpu=0, inference_device="cpu")) as c:
+        h = _auth(c)
+        hb = _auth(c, "bob")
+        r = c.options("/data/list/", headers={"Origin": "http://ui.example", "Access-Control-Request-Method": "POST",
+                                              "Access-Control-Request-Headers": "authorization"})
+        assert r.headers.get("access-control-allow-origin") == "http://ui.example"
+        m = c.get("/metrics").text
+        assert "csa_http_requests_total" in m and 'csa_jobs{state="running"}' in m
+        # demo bills: list/create/search/detail with owner-or-read-only
+        assert c.post("/demo/", json={"goods": "apple", "price": 2.5}).status_code == 401
+        b = c.post("/demo/", json={"goods": "apple", "price": 2.5, "amount": 3}, headers=h).json()
+        assert b["owner"] == "alice" and b["amount"] == 3
+        c.post("/demo/", json={"goods": "pear", "price": 1}, headers=hb)
+        assert [x["goods"] for x in c.get("/demo/").json()] == ["apple", "pear"]
+        assert [x["goods"] for x in c.get("/demo/search/", params={"name": "pp"}).json()] == ["apple"]
+        assert c.get(f"/demo/{b['id']}/").json()["price"] == 2.5
+        assert c.put(f"/demo/{b['id']}/", json={"goods": "apple", "price": 3}, headers=hb).status_code == 403
+        assert c.put(f"/demo/{b['id']}/", json={"goods": "apple", "price": 3}, headers=h).json()["price"] == 3
+        assert c.delete(f"/demo/{b['id']}/", headers=h).status_code == 204
+        assert c.get(f"/demo/{b['id']}/").status_code == 404
+
+
+def test_url_dataset_and_url_training(client, tmp_path):
+    """datatype=url: ';'-separated URLs downloaded into the dataset (file:// here — no
+    network), then the MNIST-idx training variant (construct_distribute_url.py)."""
+    from cloud_server_amd.data.datasets import write_idx
+    src = tmp_path / "mnist"
+    src.mkdir()
+    tr, te = synthetic_mnist(300, seed=5), synthetic_mnist(100, seed=6)
+    import gzip
+    for stem, arr in [("train-images-idx3-ubyte", tr.images.reshape(-1, 28, 28)),
+                      ("train-labels-idx1-ubyte", tr.labels.astype(np.uint8)),
+                      ("t10k-images-idx3-ubyte", te.images.reshape(-1, 28, 28)),
+                      ("t10k-labels-idx1-ubyte", te.labels.astype(np.uint8))]:
+        write_idx(str(src / stem), arr)
+        with open(src / stem, "rb") as f, gzip.open(str(src / (stem + ".gz")), "wb") as g:
+            g.write(f.read())
+        os.remove(src / stem)
+    urls = ";".join(f"file://{src}/{n}" for n in sorted(os.listdir(src)))
+    h = _auth(client)
+    pk = _mp(client, "/data/list/", {"file_type": "url", "file_class": "picture", "url": urls}, {}, h).json()["data_id"]
+    tree = json.dumps(client.get(f"/data/{pk}/", headers=h).json())
+    assert "t10k-images-idx3-ubyte.gz" in tree
+    client.post("/data/create/", json={"modelName": "mu"}, headers=h)
+    assert client.post("/preprocess/", json={"dataId": pk, "modelName": "mu", "operations": []},
+                       headers=h).json() == {"message": "success"}
+    cfg = {"iter": 20, "learning_rate": 0.01, "optimizer_name": "AdamOptimizer", "options": {"log_every": 10},
+           "net_config": {"middle_layer": [{"layer": "connect", "hidden": 32}]}}
+    jid = client.post("/construct/construction/mu/url/", json=cfg, headers=h).json()["job"]
+    assert client.app.state.jobs.wait(jid, 300) == "done"
+    res = client.get("/runtime/train/mu/20/", headers=h).json()
+    assert len(res["every_result"]) == 2 and "final_accuracy" in res

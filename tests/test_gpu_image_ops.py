@@ -107,7 +107,7 @@ def test_pipeline_gpu_equals_cpu(tmp_path):
         d = tmp_path / be
         with zipfile.ZipFile(os.path.join(FIX, "test-pics.zip")) as z:
             z.extractall(d / "data")
-        shutil.copy(os.path.join(FIX, "tag.json"), d / "tag.json")
+        shutil.copyfile(os.path.join(FIX, "tag.json"), d / "tag.json")
         tags = pipeline.run(str(d / "data"), str(d / "tag.json"), ops, backend=be, seed=5)
         res[be] = (tags, {n: pipeline._read(str(d / "data" / n)) for n in tags})
     assert res["cpu"][0] == res["gpu"][0] and len(res["cpu"][0]) == 99 * 4

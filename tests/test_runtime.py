@@ -146,14 +146,16 @@ def test_fault_injection_then_resume(tmp_path, monkeypatch):
 
 def test_resume_is_exact(tmp_path):
     """Stopping at a checkpoint and resuming gives the same weights as an unbroken run
-    (same optimizer slots, same step count; batch order re-seeded deterministically)."""
+    (same optimizer slots and step count; the batch stream seeks to the same position)."""
     data = _data()
     a, b = str(tmp_path / "a"), str(tmp_path / "b")
     os.makedirs(a); os.makedirs(b)
-    run_job(a, dict(SMALL, iter=21), device="cpu", backend="torch", data=data)
+    run_job(a, dict(SMALL, iter=33), device="cpu", backend="torch", data=data)
     o1 = ckpt.load(ckpt.latest(a)[1])
-    run_job(b, dict(SMALL, iter=21), device="cpu", backend="torch", data=data)
+    run_job(b, dict(SMALL, iter=14), device="cpu", backend="torch", data=data)    # resumed part crosses an epoch
+    run_job(b, dict(SMALL, iter=33), device="cpu", backend="torch", data=data)
     o2 = ckpt.load(ckpt.latest(b)[1])
+    assert o1["host_step"] == o2["host_step"] == 33
     for k in o1["model"]:
         torch.testing.assert_close(o1["model"][k], o2["model"][k])     # deterministic on CPU
     torch.testing.assert_close(o1["slots"], o2["slots"])
@@ -279,3 +281,19 @@ def test_inference_service_cache(tmp_path):
     assert svc.misses == 1 and svc.hits >= 1
     many = svc.predict_many(mdir, [img.getvalue()] * 5)
     assert len(many) == 5 and all(m["result"] == "success" for m in many)
+
+
+def test_watchdog_kills_hung_worker(tmp_path, monkeypatch):
+    s = _settings(tmp_path, "process")
+    s.heartbeat_s = 4.0
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    monkeypatch.setenv("CSA_HANG_AT_STEP", "15")
+    jm = JobManager(s, db, executor="process", ngpu=0)
+    try:
+        _prep_model(s, uid, "m")
+        jid = jm.submit(uid, "m", "file", dict(SMALL, iter=100))
+        assert jm.wait(jid, 240) == "failed"
+        assert "heartbeat" in db.get_job(jid)["error"]
+    finally:
+        jm.shutdown()
