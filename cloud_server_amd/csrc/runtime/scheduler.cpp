@@ -12,7 +12,8 @@
 //     `ngpus` distinct GPUs, one rank per GPU),
 //   * placement = least-loaded GPUs first (ties -> lowest id), FIFO admission with
 //     head-of-line skipping limited by `max_skip` so a wide job is not starved forever,
-//   * the scheduler is thread-safe (one mutex) and allocation-free on the hot path.
+//   * the scheduler is thread-safe (one mutex); tests/native/ stress it under ASan/UBSan
+//     and ThreadSanitizer.
 //
 // The Python job manager (runtime/scheduler.py) wraps this library and falls back to a
 // pure-Python implementation of the same policy if the .so is unavailable.

@@ -4,7 +4,7 @@
   through ctypes from ``ops.fused``.  Launchers take a ``hipStream_t`` and never
   allocate or synchronise, so they are captured into HIP graphs by the engine.
 * ``libcsa_runtime.so`` — host-side C++ runtime pieces (``csrc/runtime/*.cpp``): the
-  GPU-slot job scheduler and the result-log parser used by the job manager.
+  GPU-slot job scheduler used by the job manager.
 
 Objects are rebuilt only when a source/header hash changes (stamp file next to the .so),
 so ``build()`` on an up-to-date tree is instant.  Built ``.so`` files are git-ignored but
