@@ -116,6 +116,9 @@ class HipProgram:
         sample config that is one ~1 MB bucket (head+fc2) launched after fc2, the 8 MB
         fc1 bucket launched right after fc1's weight gradient, and a small tail."""
         e = self.e
+        self.wsplit = os.environ.get("CSA_WGRAD_STREAM", "1") == "1"
+        if self.wsplit:
+            self.wstream = torch.cuda.Stream(e.device)
         self.overlap = (e.ctx.enabled and e.sync.strategy == "allreduce" and
                         os.environ.get("CSA_DP_OVERLAP", "1") == "1")
         self.bucket_at: Dict[object, tuple] = {}
@@ -141,12 +144,24 @@ class HipProgram:
                 self.bucket_at[key] = (lo, hi)
                 hi = lo
 
+    def _fork_wgrad(self, st):
+        """Weight gradients are off the critical path (nothing in this step reads them
+        before the optimizer), so they go to a second stream forked from the main one
+        and overlap the next dgrad/route kernels; the main stream joins before the
+        optimizer.  Returns the stream handle to launch on."""
+        if not self.wsplit:
+            return st
+        self.wstream.wait_stream(torch.cuda.current_stream(self.e.device))
+        return self.wstream.cuda_stream
+
     def _grad_ready(self, key) -> None:
         b = self.bucket_at.get(key)
         if b is None:
             return
         cur = torch.cuda.current_stream(self.e.device)
         self.side.wait_stream(cur)
+        if self.wsplit:
+            self.side.wait_stream(self.wstream)
         with torch.cuda.stream(self.side):
             self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
 
@@ -400,14 +415,15 @@ class HipProgram:
                         K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
                         K.ptr(xf), in_act, in_alpha, *self._bn_args_c(tf), K.ptr(tf.bwd_slab), st),
                         "slabs:dense_dgrad")
+                ws = self._fork_wgrad(st)
                 if u.xt is not None:
                     self._rc(lib.csa_dense_wgrad(
                         K.ptr(u.xt), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
-                        B, fin, fout, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, 1.0, st), "dense_wgrad")
+                        B, fin, fout, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, 1.0, ws), "dense_wgrad")
                 else:
                     self._rc(lib.csa_dense_wgrad(
                         K.ptr(u.x), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
-                        B, fin, fout, *self._bn_args_c(tf), in_act, in_alpha, 1.0, st), "dense_wgrad")
+                        B, fin, fout, *self._bn_args_c(tf), in_act, in_alpha, 1.0, ws), "dense_wgrad")
             else:
                 # output side: (BN backward of the NEXT transform) + act backward + pool routing
                 next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
@@ -442,12 +458,13 @@ class HipProgram:
                 sp = lp.spec
                 h, w = lp.in_shape.hw
                 oh, ow = lp.out_shape.hw
+                ws = self._fork_wgrad(st)
                 self._rc(lib.csa_conv_wgrad(
                     None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
                     K.ptr(dc), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]) if sp.bias else None,
                     B, h, w, lp.in_shape.c, sp.kh, sp.kw, sp.stride[0], sp.stride[1], lp.pads[0], lp.pads[2],
                     oh, ow, sp.cout, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], in_act, in_alpha,
-                    K.ptr(cur) if raw else None, st), "conv_wgrad")
+                    K.ptr(cur) if raw else None, ws), "conv_wgrad")
                 if prev is not None:
                     self._rc(lib.csa_conv_dgrad(
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
@@ -455,8 +472,11 @@ class HipProgram:
             self._grad_ready(k)
 
         # ---------------- gradient sync + optimizer ----------------
+        main = torch.cuda.current_stream(e.device)
+        if self.wsplit:
+            main.wait_stream(self.wstream)
         if self.overlap:
-            torch.cuda.current_stream(e.device).wait_stream(self.side)
+            main.wait_stream(self.side)
         else:
             e.after_backward_sync()
         self._optimizer(st)
