@@ -13,9 +13,10 @@
 //     loads and the inner loop is v_fma_f32 with an SGPR operand;
 //   * fused epilogues: bias, activation, max-pool (argmax kept as uint8 for backward)
 //     and the BatchNorm partial statistics of the output (per-workgroup slab).
-// Weight gradients are an implicit GEMM on MFMA (gemm.hip, csa_conv_wgrad).
+// Weight gradients: a direct LDS-staged reduction kernel (conv_wgrad_kernel).
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace csa {
 
@@ -379,6 +380,233 @@ static int groups(int c) { return (c + CB_T - 1) / CB_T; }
 
 // Rows per band: one pass of the 256 lanes over (pixel, channel-group) pairs, and the
 // staged input rows within STAGE_FLOATS.
+// -----------------------------------------------------------------------------------
+// Conv weight gradient:  dW[i,j,ci,co] = sum_{b,oy,ox} xin[b, oy*SH-PT+i, ox*SW-PL+j, ci]
+// * dc[b,oy,ox,co],  db[co] = sum dc[b,oy,ox,co]  — a GEMM with a huge reduction
+// dimension (pixels: 39,200 for the sample) and a tiny output (taps x Cout: 40 x 20).
+// One workgroup per (image, band of output rows):
+//   * stages the band's input tile ZERO-PADDED (SAME padding materialised, so no bounds
+//     checks in the inner loop) with the forward input transform (uint8 /255 for the
+//     first layer, BN-apply + activation otherwise) and the band's dc rows
+//     (channel-padded to a multiple of 16) in LDS — one batched round trip;
+//   * runs v_mfma_f32_16x16x4_f32 over (tap-row tiles of 16) x (Cout tiles of 16) with
+//     the band's pixels as K, split across the 4 waves; A (im2col of the LDS tile) and
+//     B (dc) are read straight from LDS with per-lane precomputed offsets;
+//   * folds the 4 waves' partial tiles in LDS and issues one atomicAdd per output into
+//     stripe (workgroup % S) of dW/db ([S][taps*Cout], [S][Cout]; zeroed by the
+//     optimizer, which sums the stripes when it applies the update).  Atomics to one
+//     128-B line serialise at ~1 ns each: 350 workgroups x 800 outputs on the sample
+//     conv2 cost 14 us unstriped.  S = 1 (data parallel: the all-reduce needs the plain
+//     gradient) accumulates straight into the flat gradient.
+// The tap row == KH*KW*Cin is the ones row (bias gradient).
+// 16x16x4 map: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15], D[4*(l>>4)+r][l&15].
+// -----------------------------------------------------------------------------------
+typedef float wg_f32x4 __attribute__((ext_vector_type(4)));
+
+struct ConvWgradArgs {
+  ConvGeom g;
+  int nbands, band_rows;
+  int tile_rows, tile_w;        // zero-padded input tile: rows x (Wp * Cin) floats
+  int c16;                      // dc channel stride in LDS (Cout rounded up to 16)
+  int mtiles, ntiles, ntaps;    // ntaps = KH*KW*Cin (+1 if bias); 16x16 output tiles
+  const float* x; const uint8_t* img; const int64_t* idx; const int64_t* cursor;
+  BNRef in_bn; int in_bn_on; int in_act; float in_alpha;
+  const float* dc; float* dw; float* db; int stripes;
+};
+
+template <bool U8>
+__global__ __launch_bounds__(CONV_THREADS) void conv_wgrad_kernel(ConvWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  const ConvGeom& g = a.g;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x % a.nbands;
+  const int r0 = band * a.band_rows, r1 = min(g.OH, r0 + a.band_rows);
+  const int nrows = r1 - r0;
+  const int ty0 = r0 * g.SH - g.PT;                 // image row of tile row 0
+  const int tw = a.tile_w;                          // floats per tile row (Wp * Cin)
+  const int ntile = a.tile_rows * tw;
+  float* s_x = smem;
+  float* s_dc = smem + ((ntile + 3) & ~3);
+  const int npix = nrows * g.OW;
+  const int kpad = (npix + 15) & ~15;               // pixels padded: 4 waves x k-steps of 4
+  float* s_part = s_dc + kpad * a.c16;              // [4 waves][8 tiles][16][16]
+
+  // ---- staging: the band's dc rows and the in-image rows of the input tile are each
+  // ONE contiguous global range; both are loaded as float4 (uint8x4 for the first layer)
+  // in a single batch — every load of a thread in flight before the first LDS store —
+  // and scattered into the padded LDS layouts, whose padding is zero-filled separately.
+  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * g.B : a.idx;
+  const int iy0 = max(0, ty0), iy1 = min(g.H, ty0 + a.tile_rows);
+  const int irow = g.W * g.Cin;                     // floats per image row
+  const int nx = max(0, iy1 - iy0) * irow;          // input elements to load
+  const int nd = npix * g.Cout;                     // dc elements to load
+  const long xoff = ((long)b * g.H + iy0) * irow;
+  const long doff = ((long)b * g.OH + r0) * g.OW * g.Cout;
+  // zero-fill: whole tile + whole dc area (cheap LDS stores; overwritten below)
+  for (int e = threadIdx.x; e < ntile; e += CONV_THREADS) s_x[e] = 0.f;
+  for (int e = threadIdx.x; e < kpad * a.c16; e += CONV_THREADS) s_dc[e] = 0.f;
+  if (!U8 && a.in_bn_on) bn_reduce_to_lds(a.in_bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
+  __syncthreads();
+  {
+    const long ioff = U8 ? idx[b] * (long)(g.H * irow) + (long)iy0 * irow : xoff;
+    const bool v4 = ((ioff | nx | doff | nd) & 3) == 0;
+    const int sx = v4 ? 4 : 1;
+    const int nxv = (nx + sx - 1) / sx, ndv = (nd + sx - 1) / sx, ntot = nxv + ndv;
+    const uint8_t* isrc = U8 ? a.img + ioff : nullptr;
+    const float* xsrc = U8 ? nullptr : a.x + xoff;
+    const float* dsrc = a.dc + doff;
+    const FastDiv dirow(irow), dcout(g.Cout), dcin(g.Cin);
+    const int xcol0 = g.PL * g.Cin, trow0 = iy0 - ty0;
+    constexpr int U = 8;
+    for (int base = 0; base < ntot; base += CONV_THREADS * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * CONV_THREADS + threadIdx.x;
+        const bool isx = i < nxv;
+        const int j = isx ? i : min(i - nxv, ndv - 1);
+        if (v4) {
+          if (isx) {
+            if (U8) {
+              const uchar4 q = reinterpret_cast<const uchar4*>(isrc)[j];
+              v[u] = make_float4(q.x, q.y, q.z, q.w);
+            } else {
+              v[u] = reinterpret_cast<const float4*>(xsrc)[j];
+            }
+          } else {
+            v[u] = reinterpret_cast<const float4*>(dsrc)[max(j, 0)];
+          }
+        } else {
+          const float t = isx ? (U8 ? (float)isrc[j] : xsrc[j]) : dsrc[max(j, 0)];
+          v[u] = make_float4(t, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * CONV_THREADS + threadIdx.x;
+        if (i >= ntot) continue;
+        const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        const bool isx = i < nxv;
+        const int e0 = (isx ? i : i - nxv) * sx;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= sx) break;
+          const int e = e0 + q;
+          if (isx) {
+            if (e >= nx) break;
+            int r, c;
+            dirow.divmod(e, r, c);
+            float t = vv[q];
+            if (U8) {
+              t *= (1.0f / 255.0f);
+            } else {
+              if (a.in_bn_on) {
+                int xq, ci;
+                dcin.divmod(c, xq, ci);
+                t = t * s_bn[256 + ci] + s_bn[384 + ci];
+              }
+              t = act_fwd(t, a.in_act, a.in_alpha);
+            }
+            s_x[(trow0 + r) * tw + xcol0 + c] = t;
+          } else {
+            if (e >= nd) break;
+            int pix, c;
+            dcout.divmod(e, pix, c);
+            s_dc[pix * a.c16 + c] = vv[q];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- MFMA: rows = taps (i, j, ci | bias), cols = Cout, K = band pixels (wave-split).
+  // Output tiles (16 taps x 16 channels) are processed in blocks of up to 8.
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int ntiles = a.mtiles * a.ntiles;
+  const int ncombo = g.KH * g.KW * g.Cin;
+  const int kq = kpad / 4;                          // pixels per wave (multiple of 4)
+  for (int t0 = 0; t0 < ntiles; t0 += 8) {
+    const int nt_blk = min(8, ntiles - t0);
+    // per-lane A row offset of each tile's tap: >= 0 tile offset, -1 zero row, -2 bias row
+    int tapoff[8], bcol[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int tt = t0 + t;
+      const int mt = tt / a.ntiles, nt = tt - mt * a.ntiles;
+      const int tap = mt * 16 + lr;
+      int off = -1;
+      if (t < nt_blk && tap < a.ntaps) {
+        if (tap >= ncombo) off = -2;
+        else {
+          const int ci = tap % g.Cin, ij = tap / g.Cin;
+          const int i = ij / g.KW, j = ij - i * g.KW;
+          off = i * tw + j * g.Cin + ci;
+        }
+      }
+      tapoff[t] = off;
+      bcol[t] = nt * 16 + lr;
+    }
+    wg_f32x4 acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = wg_f32x4{0.f, 0.f, 0.f, 0.f};
+    // this lane's pixel walks k = wave*kq + lk, +4 per step: (oy, ox) advanced
+    // incrementally (no division in the loop); two k-steps per iteration so the next
+    // step's LDS operand reads are in flight under this step's MFMAs
+    int p = wave * kq + lk;
+    int oyl = p / g.OW, ox = p - (p / g.OW) * g.OW;
+    const int pend = (wave + 1) * kq;
+    const int xstep = 4 * g.SW * g.Cin, ystep = g.SH * tw - g.OW * g.SW * g.Cin;
+    int pixoff = oyl * g.SH * tw + ox * g.SW * g.Cin;
+#pragma unroll 2
+    for (; p < pend; p += 4) {
+      const bool okp = p < npix;
+      const float* drow = s_dc + p * a.c16;         // zero beyond npix / Cout
+      float av[8], bv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        if (t >= nt_blk) break;
+        const int to = tapoff[t];
+        const float x = s_x[okp ? pixoff + (to > 0 ? to : 0) : 0];
+        av[t] = (to >= 0 && okp) ? x : ((to == -2 && okp) ? 1.f : 0.f);
+        bv[t] = drow[bcol[t]];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        if (t >= nt_blk) break;
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc[t], 0, 0, 0);
+      }
+      ox += 4;
+      pixoff += xstep;
+      while (ox >= g.OW) { ox -= g.OW; pixoff += ystep; }
+    }
+    // fold the 4 waves' tiles in LDS, one atomic per output
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t < nt_blk) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s_part[(wave * 8 + t) * 256 + (4 * lk + r) * 16 + lr] = acc[t][r];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nt_blk * 256; e += CONV_THREADS) {
+      const int t = e >> 8, rr = (e >> 4) & 15, cc = e & 15;
+      const int tt = t0 + t;
+      const int mt = tt / a.ntiles, nt = tt - mt * a.ntiles;
+      const int tap = mt * 16 + rr, co = nt * 16 + cc;
+      if (tap >= a.ntaps || co >= g.Cout) continue;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += s_part[(w * 8 + t) * 256 + (e & 255)];
+      const int sidx = blockIdx.x % a.stripes;
+      if (tap >= ncombo) atomicAdd(&a.db[sidx * g.Cout + co], v);
+      else atomicAdd(&a.dw[(long)sidx * ncombo * g.Cout + tap * g.Cout + co], v);
+    }
+    __syncthreads();                                // s_part reused by the next block
+  }
+}
+
 static void fwd_bands(const ConvGeom& g, const PoolGeom& p, int& nbands, int& rows, int& rows_in) {
   const int out_rows = p.on ? p.OH : g.OH, out_w = p.on ? p.OW : g.OW;
   const int ppp = CONV_THREADS / groups(g.Cout);
@@ -500,5 +728,57 @@ CSA_API int csa_conv_dgrad(const float* dc, const float* w, float* dx, const int
   (void)attr;
   dim3 grid((unsigned)(a.g.B * a.nbands));
   hipLaunchKernelGGL((conv_dgrad_kernel<CB_T>), grid, dim3(CONV_THREADS), shm, st, a);
+  return (int)hipGetLastError();
+}
+
+// dW/db (+)= conv weight gradient, accumulated with atomics into `stripes` copies
+// (dW: [stripes][KH*KW*Cin*Cout], db: [stripes][Cout]); the caller zeroes them.
+// Input = x (fp32 NHWC, forward input transform BN/act applied on the fly) or the
+// uint8 dataset rows img[idx[b] (+ cursor * B)] / 255 for the first layer.
+CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* idx, const float* dOut,
+                           float* dW, float* db, int stripes, int B, int H, int W, int Cin, int KH, int KW, int SH,
+                           int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
+                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                           const float* bn_offset, int in_act, float in_alpha, const int64_t* cursor,
+                           hipStream_t st) {
+  ConvWgradArgs a{};
+  a.g = ConvGeom{B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout};
+  a.ntaps = KH * KW * Cin + (db ? 1 : 0);
+  a.mtiles = (a.ntaps + 15) / 16;
+  a.ntiles = (Cout + 15) / 16;
+  if (Cin > 128 || (!x && !img)) return -1;
+  a.x = x; a.img = img; a.idx = idx; a.cursor = cursor; a.dc = dOut; a.dw = dW; a.db = db;
+  a.stripes = stripes < 1 ? 1 : stripes;
+  a.in_bn = BNRef{bn_slab, bn_nslab, Cin, bn_count, bn_eps, bn_scale, bn_offset};
+  a.in_bn_on = bn_slab != nullptr && !img;
+  a.in_act = img ? 0 : in_act; a.in_alpha = in_alpha;
+  a.c16 = a.ntiles * 16;
+  a.tile_w = ((OW - 1) * SW + KW) * Cin;
+  auto tile_rows = [&](int r) { return (r - 1) * SH + KH; };
+  auto lds = [&](int r) {
+    const size_t kpad = ((size_t)r * OW + 15) & ~(size_t)15;
+    return (((size_t)tile_rows(r) * a.tile_w + 3) / 4 * 4 + kpad * a.c16 +
+            4 * 8 * 256) * sizeof(float);
+  };
+  // Bands: the batch is cut into ~`target` workgroups.  Each ends in one atomicAdd per
+  // output and atomics to one 128-B line serialise, so fewer, larger bands win until
+  // the per-wave pixel loop dominates (CSA_WGRAD_TARGET overrides for tuning).
+  static const int target = [] {
+    const char* e = getenv("CSA_WGRAD_TARGET");
+    return e ? std::max(1, atoi(e)) : 700;
+  }();
+  const int per_img = std::max(1, (target + B - 1) / B);
+  int rows = std::max(1, (OH + per_img - 1) / per_img);
+  while (rows > 1 && lds(rows) > 150 * 1024) --rows;
+  if (lds(rows) > 150 * 1024) return -2;
+  a.band_rows = rows;
+  a.tile_rows = tile_rows(rows);
+  a.nbands = (OH + rows - 1) / rows;
+  static bool attr = set_lds_attr((const void*)conv_wgrad_kernel<true>) &&
+                     set_lds_attr((const void*)conv_wgrad_kernel<false>);
+  (void)attr;
+  dim3 grid((unsigned)(B * a.nbands));
+  if (img) hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(CONV_THREADS), lds(rows), st, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(CONV_THREADS), lds(rows), st, a);
   return (int)hipGetLastError();
 }

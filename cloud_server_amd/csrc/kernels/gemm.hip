@@ -7,9 +7,9 @@
 //   * uses the exact-f32 MFMA v_mfma_f32_32x32x2_f32 (one 32x32 accumulator per wave),
 //   * splits K across the 4 waves of a workgroup (WK) and across workgroups (split-K),
 //     so every shape launches ~1000 waves (one per SIMD) even at M = 50,
-//   * builds operands through loader functors: row-major, transposed, im2col (conv
-//     weight-gradient as an implicit GEMM) and a fused BatchNorm-apply + activation
-//     prologue, so normalised / activated tensors are never materialised in HBM,
+//   * builds operands through loader functors: row-major, transposed and a fused
+//     BatchNorm-apply + activation prologue (conv weight gradients moved to a direct
+//     reduction kernel in conv.hip),
 //   * ends in epilogue functors: store, split-K atomic add, bias, and the fused
 //     activation-backward + BatchNorm-backward partial statistics.
 //
@@ -26,7 +26,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int KC = 64;        // K chunk staged per iteration (32 MFMAs); most waves need 1-2
 constexpr int LDS_PAD = 33;   // row stride of the 32-wide staging tiles (conflict-free)
 constexpr int MAXC = 128;     // max BatchNorm channels handled in LDS
-constexpr int KTAB = 512;     // max K slice per workgroup for table-driven loaders (im2col)
 
 // LDS tables shared by loaders/epilogues: [mean | rstd | a | b] x MAXC
 struct BNTables { const float *mean, *rstd, *a, *b; };
@@ -50,7 +49,6 @@ struct LoadRowMajor {          // elem(r, c) = p[r * ld + c]
     const int cc = min(c, cols - 4);
     return *reinterpret_cast<const float4*>(p + (long)rr * ld + cc);
   }
-  __device__ void prepare(int*, int, int, int, int) {}
   __device__ void bind(const BNTables&) {}
   __device__ float raw(int r, int c) const {
     const bool ok = r < rows && c < cols;
@@ -69,7 +67,6 @@ struct LoadColMajor {          // elem(r, c) = p[c * ld + r]
     const int cc = c < cols ? c : 0;
     return *reinterpret_cast<const float4*>(p + (long)cc * ld + rr);
   }
-  __device__ void prepare(int*, int, int, int, int) {}
   __device__ void bind(const BNTables&) {}
   __device__ float raw(int r, int c) const {
     const bool ok = r < rows && c < cols;
@@ -93,7 +90,6 @@ struct LoadBNAct {
     f = min(f, feat - 4);
     return *reinterpret_cast<const float4*>(x + (long)m * ld + f);
   }
-  __device__ void prepare(int*, int, int, int, int) {}
   __device__ void bind(const BNTables& t) { ta = t.a; tb = t.b; }
   __device__ float raw(int r, int c) const {
     const int m = ROWS_ARE_BATCH ? r : c, f = ROWS_ARE_BATCH ? c : r;
@@ -105,81 +101,6 @@ struct LoadBNAct {
     if (m >= batch) return 0.f;
     if (f >= feat) return (ones_row && f == feat) ? 1.f : 0.f;
     if (has_bn) { int q, ch; C.divmod(f, q, ch); v = v * ta[ch] + tb[ch]; }
-    return act_fwd(v, act, alpha);
-  }
-};
-
-// im2col^T for conv weight gradients: elem(r = kconv, c = p), kconv = (i, j, ci),
-// p = (b, oy, ox) over the conv OUTPUT pixels; reads the conv input (NHWC fp32, or the
-// raw uint8 dataset gathered through idx for the first layer).  Row kconv == KH*KW*Cin
-// is the ones row (bias gradient).  The input may carry a BN-apply + act transform.
-template <bool U8>
-struct LoadIm2colT {
-  const float* x; const uint8_t* img; const int64_t* idx;
-  int B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, ones_row, has_bn, act; float alpha;
-  FastDiv dCin, dKW, dOW, dOH;
-  const float* ta; const float* tb;
-  const int64_t* cursor;   // if set: idx += cursor[0] * B (resolved in-kernel by bind)
-  static constexpr bool KCONTIG = false;
-  static constexpr bool VEC4 = false;
-  __device__ float4 raw4(int, int) const { return float4{0.f, 0.f, 0.f, 0.f}; }
-  __device__ void bind(const BNTables& t) {
-    ta = t.a; tb = t.b;
-    if (U8 && cursor) { idx += cursor[0] * B; cursor = nullptr; }
-  }
-  // Per-workgroup tables (built once by prepare(), then 2 LDS reads per element instead
-  // of four runtime divisions):
-  //   col c in [klo, khi): {base offset of pixel's image, (oy*SH-PT) << 16 | (ox*SW-PL)}
-  //   row r in [rlo, rhi): {(i*W + j)*Cin + ci, i << 16 | j}, ci in the low bits of a 3rd
-  int* tcol; int* trow; int klo, rlo;
-  __device__ void prepare(int* tab, int rlo_, int rhi, int klo_, int khi) {
-    tcol = tab; trow = tab + 2 * KTAB; klo = klo_; rlo = rlo_;
-    const int kc = KH * KW * Cin, P = B * OH * OW, HWC = H * W * Cin;
-    for (int c = klo + (int)threadIdx.x; c < khi; c += blockDim.x) {
-      int t2, ox, b, oy;
-      dOW.divmod(min(c, P - 1), t2, ox);
-      dOH.divmod(t2, b, oy);
-      const long base = U8 ? idx[b] * (long)HWC : (long)b * HWC;
-      tcol[2 * (c - klo)] = (int)base;
-      tcol[2 * (c - klo) + 1] = ((oy * SH - PT) << 16) | ((ox * SW - PL) & 0xffff);
-    }
-    for (int r = rlo + (int)threadIdx.x; r < rhi; r += blockDim.x) {
-      int t, ci, i, j;
-      dCin.divmod(min(r, kc - 1), t, ci);
-      dKW.divmod(t, i, j);
-      trow[3 * (r - rlo)] = (i * W + j) * Cin + ci;
-      trow[3 * (r - rlo) + 1] = (i << 16) | j;
-      trow[3 * (r - rlo) + 2] = ci;
-    }
-  }
-  __device__ long offset(int r, int c, int& ci, bool& ok) const {
-    const int kc = KH * KW * Cin, P = B * OH * OW;
-    const int cb = tcol[2 * (c - klo)], cyx = tcol[2 * (c - klo) + 1];
-    const int* rt = trow + 3 * (r - rlo);
-    const int ro = rt[0], rij = rt[1];
-    ci = rt[2];
-    const int y = (cyx >> 16) + (rij >> 16);
-    const int x = (short)(cyx & 0xffff) + (rij & 0xffff);
-    ok = (c < P) && (r < kc) && y >= 0 && y < H && x >= 0 && x < W;
-    const int pix = ((cyx >> 16) * W + (short)(cyx & 0xffff)) * Cin + ro;
-    return (long)cb + (ok ? pix : 0);
-  }
-  __device__ float raw(int r, int c) const {
-    int ci;
-    bool ok;
-    const long o = offset(r, c, ci, ok);
-    if (U8) return (float)img[o];
-    return x[o];
-  }
-  __device__ float post(float v, int r, int c) const {
-    const int kc = KH * KW * Cin;
-    if (r >= kc) return (ones_row && r == kc && c < B * OH * OW) ? 1.f : 0.f;
-    int ci;
-    bool ok;
-    (void)offset(r, c, ci, ok);
-    if (!ok) return 0.f;
-    if (U8) return v * (1.0f / 255.0f);
-    if (has_bn) v = v * ta[ci] + tb[ci];
     return act_fwd(v, act, alpha);
   }
 };
@@ -304,7 +225,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
   __shared__ float s_stage[4][2][KC * LDS_PAD];   // per-wave tiles; reused for the WK reduction
   __shared__ float s_bn[4 * MAXC];
   __shared__ float s_acc[2 * MAXC];
-  __shared__ int s_tab[2 * KTAB + 3 * 64];
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN);
@@ -334,12 +254,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
   Stage<LB> stB;
   stA.init(lane);
   stB.init(lane);
-  {  // loader tables for this workgroup's rows / K slice
-    const int rlo = blockIdx.y * 32 * WM, rhi = rlo + 32 * WM;
-    const int klo = blockIdx.z * k_per_split, khi = min(K, klo + k_per_split);
-    la.prepare(s_tab, rlo, rhi, klo, khi);
-    __syncthreads();
-  }
   GEMM_STAMP(1);
   // first chunk's operand loads go out BEFORE the BN-slab reduction, so the two
   // memory round trips overlap
@@ -559,38 +473,3 @@ CSA_API int csa_dense_wgrad(const float* X, const float* dY, float* dW, float* d
   });
 }
 
-// Conv weight gradient as implicit GEMM:  dW[(i,j,ci)][co] = sum_p im2col(x)[p][(i,j,ci)] dOut[p][co]
-// x: fp32 NHWC [B,H,W,Cin] (optionally through bn+act) or, if img != null, the raw uint8
-// dataset gathered through idx.  dOut: [B,OH,OW,Cout].  Always atomic (caller zeroes).
-CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* idx, const float* dOut,
-                           float* dW, float* db, int B, int H, int W, int Cin, int KH, int KW, int SH,
-                           int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
-                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                           const float* bn_offset, int in_act, float in_alpha, const int64_t* cursor,
-                           hipStream_t st) {
-  if (bn_slab && Cin > MAXC) return -1;
-  const int kc = KH * KW * Cin;
-  const int Mg = kc + (db ? 1 : 0);
-  const int P = B * OH * OW;
-  Plan p = plan_gemm(Mg, Cout, P, true);
-  while (p.kps > KTAB) {   // the im2col tables cover one K slice per workgroup
-    p.splits *= 2;
-    p.kps = ((P + p.splits - 1) / p.splits + 3) / 4 * 4;
-  }
-  // conv wgrad is always accumulated with atomics (split-K over pixels)
-  BNRef bn = make_bn(bn_slab, bn_nslab, Cin, bn_count, bn_eps, bn_scale, bn_offset);
-  EpiStore epi{dW, (long)Cout, kc, Cout, nullptr, 1, db, 1.f};
-  return dispatch2(Cout % 4 == 0 && Cout >= 4, false, [&](auto vb, auto) {
-  LoadColMajor<decltype(vb)::value> lb{dOut, (long)Cout, Cout, P};  // B(k=p, co) = dOut[p][co]
-  if (img) {
-    LoadIm2colT<true> la{nullptr, img, idx, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW,
-                         db != nullptr, 0, 0, 0.f, FastDiv(Cin), FastDiv(KW), FastDiv(OW), FastDiv(OH),
-                         nullptr, nullptr, cursor};
-    return launch_gemm(p, la, lb, epi, Mg, Cout, P, bn, 0, nullptr, 0, st);
-  }
-  LoadIm2colT<false> la{x, nullptr, nullptr, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW,
-                        db != nullptr, bn_slab != nullptr, in_act, in_alpha, FastDiv(Cin), FastDiv(KW),
-                        FastDiv(OW), FastDiv(OH), nullptr, nullptr, nullptr};
-  return launch_gemm(p, la, lb, epi, Mg, Cout, P, bn, bn_slab != nullptr, nullptr, 0, st);
-  });
-}

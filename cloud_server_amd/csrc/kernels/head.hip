@@ -1,23 +1,16 @@
-// Fused classifier head + loss + head backward + step bookkeeping (one workgroup).
+// Fused classifier head + loss + head backward + step bookkeeping.
 //
 // Reference: the fixed 10-way head (construct_distribute.py:252-264), the loss
 // (softmax-xent 'entropy' or 'mse', :285-298), the accuracy op (:381-382) and the
-// global_step increment done by minimize() (:372-373).  At B = 50 the whole head is
-// ~0.8 MFLOP, less than one launch's fixed cost, so ONE 1024-thread workgroup does it:
-//   stage T(h) (T = optional activation of the head input; rows padded to K+1 floats so
-//   MFMA operand reads are bank-conflict free) and Wh in LDS,
-//   logits = T(h) @ Wh + bh      — f32 MFMA 32x32x2, K split over the 16 waves,
-//   loss, dlogits (scaled by grad_scale = 1/world), #correct,
-//   dWh = T(h)^T dlogits, dbh    — MFMA, one 32-row tile of Wh per wave,
-//   dh  = (dlogits @ Wh^T) * T'  — MFMA, two 32x32 tiles per wave,
+// global_step increment done by minimize() (:372-373).  At B = 50 the head is ~0.8 MFLOP:
+// latency, not math.  The main path (head_rows_kernel) spreads the batch over
+// ceil(M/16) workgroups that each do every phase for their rows with 16x16x4 f32 MFMA
+// (10 classes pad to 16 columns), accumulate dWh/dbh with atomics and hand the metric
+// bookkeeping to the last arriving workgroup:
 //   ring_loss[step % R] = loss, ring_correct[step % R] = #correct, step += 1
-// so metrics never force a host sync inside the training loop.  (A VALU version with
-// both dot-product operands in LDS was LDS-bandwidth bound at ~38 µs.)
-//
-// MFMA 32x32x2 f32 operand map: A lane l = A[l&31][l>>5], B lane l = B[l>>5][l&31],
-// D reg r of lane l = D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].
+// so metrics never force a host sync inside the training loop.  A VALU fallback
+// (head_generic_kernel) covers K % 4 != 0 or inputs too wide for LDS.
 #include "common.h"
-#include <cstdlib>
 
 namespace csa {
 
@@ -26,8 +19,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int HT = 1024;
 constexpr int NW = HT / 64;
 constexpr int NCLS = 10;
-constexpr int MPAD = 64;                  // batch rows handled by the MFMA path
-constexpr size_t HEAD_LDS_MAX = 160 * 1024;
+constexpr size_t HEAD_LDS_MAX = 150 * 1024;
 
 struct HeadArgs {
   const float* h; int M, K; int in_act; float in_alpha;
@@ -40,11 +32,8 @@ struct HeadArgs {
   float* dw; float* db; float* dh;         // grads (dh may be null)
   float* logits_out;                       // optional [M][10]
   int64_t* step; float* ring_loss; int* ring_correct; int ring;
-  long long* dbg;                          // optional s_memtime stamps (diagnostics)
 };
 
-#define HEAD_STAMP(i) \
-  do { if (a.dbg && threadIdx.x == 0) a.dbg[i] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
 
 __device__ __forceinline__ int drow(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
@@ -109,49 +98,58 @@ __device__ __forceinline__ void head_loss(const HeadArgs& a, const int64_t* idx,
   }
 }
 
-// M <= 64 and M*(K+1) + 10K floats fit in LDS: the MFMA path (v_mfma_f32_16x16x4_f32:
-// 10 classes pad to 16 columns instead of 32).  16x16x4 map: A lane l = A[l&15][l>>4],
-// B lane l = B[l>>4][l&15], D reg r of lane l = D[4*(l>>4) + r][l&15].
+// Row-group MFMA path (K % 4 == 0 and 16 rows of T(h) + Wh fit in LDS): one 256-thread
+// workgroup per 16 batch rows, so the batch's head runs on ceil(M/16) CUs in parallel
+// instead of serialising every phase inside one workgroup (21 µs -> see profiles/).
+// Per workgroup: stage T(h) rows + Wh (one batched round trip), logits with
+// v_mfma_f32_16x16x4_f32 (4 waves = 4 K quarters, partials folded in LDS), loss /
+// dlogits / #correct for its rows, dh rows (plain stores), and its partial dWh / dbh
+// (atomicAdd; the optimizer zeroes them every step).  The step bookkeeping is done by
+// the LAST workgroup to arrive (agent-scope acq_rel counter, cdna_hip_programming.md
+// §6 G16): it reads the batch loss / #correct accumulated with atomics, writes the
+// metric ring, advances the step counter and re-zeroes the workspace for the next step.
+// 16x16x4 map: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
+// D reg r of lane l = D[4*(l>>4) + r][l&15].
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int RT = 256;           // threads per row-group workgroup
+constexpr int RG = 16;            // batch rows per workgroup
 
-__global__ __launch_bounds__(HT) void head_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(RT) void head_rows_kernel(HeadArgs a, int* ws) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int M = a.M, K = a.K, KP = K + 1;
-  float* s_log = smem;                     // [64][10] logits, then dlogits (rows >= M zero)
-  float* s_red = s_log + MPAD * NCLS;      // [16]
-  int* s_cor = (int*)(s_red + 16);
-  float* s_part = s_red + 32;              // [16 waves][16 rows][16 cols] logits partials
-  float* s_w = s_part + NW * 256;          // [K][10]
-  float* s_h = s_w + K * NCLS;             // [M][K+1]  T(h)
+  const int g = blockIdx.x, m0 = g * RG, mrows = min(RG, M - m0);
+  float* s_log = smem;                     // [16][10] logits, then dlogits (rows >= mrows zero)
+  float* s_part = s_log + RG * NCLS;       // [4 waves][16][16]
+  float* s_red = s_part + 4 * 256;         // [8]
+  float* s_w = s_red + 8;                  // [K][10]
+  float* s_h = s_w + K * NCLS;             // [16][K+1]  T(h) rows
+  __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
-  HEAD_STAMP(0);
-  // labels / bias early: their latency hides under the staging
   int my_label = 0;
-  if (tid < M) my_label = (int)a.labels[idx[tid]];
-
-  for (int i = tid; i < MPAD * NCLS; i += HT) s_log[i] = 0.f;
-  if (tid == 0) *s_cor = 0;
-  stage_to_lds<4>(s_w, a.w, K * NCLS, [](float v, int) { return v; });
-  {  // T(h) into padded rows: float4 loads, all of a thread's loads in flight together
+  if (tid < mrows) my_label = (int)a.labels[idx[m0 + tid]];
+  {  // Wh and the 16 rows of T(h): every load of a thread in flight together
     const int act = a.in_act;
     const float alpha = a.in_alpha;
-    const int n4 = (M * K) >> 2;            // K % 4 == 0 on this path
-    const int K4 = K >> 2;
+    const int K4 = K >> 2, nw4 = (K * NCLS) >> 2, nh4 = mrows * K4;
+    const float4* w4 = reinterpret_cast<const float4*>(a.w);
+    const float4* h4 = reinterpret_cast<const float4*>(a.h + (long)m0 * K);
     const FastDiv dk4(K4);
-    for (int base = 0; base < n4; base += HT * 8) {
+    for (int base = 0; base < nw4 + nh4; base += RT * 8) {
       float4 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int i = base + u * HT + tid;
-        v[u] = reinterpret_cast<const float4*>(a.h)[i < n4 ? i : 0];
+        const int i = base + u * RT + tid;
+        v[u] = i < nw4 ? w4[i] : h4[(i - nw4 < nh4) ? i - nw4 : 0];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int i = base + u * HT + tid;
-        if (i < n4) {
+        const int i = base + u * RT + tid;
+        if (i < nw4) {
+          reinterpret_cast<float4*>(s_w)[i] = v[u];
+        } else if (i - nw4 < nh4) {
           int m, k4;
-          dk4.divmod(i, m, k4);
+          dk4.divmod(i - nw4, m, k4);
           float* d = s_h + m * KP + 4 * k4;
           d[0] = act_fwd(v[u].x, act, alpha);
           d[1] = act_fwd(v[u].y, act, alpha);
@@ -162,16 +160,13 @@ __global__ __launch_bounds__(HT) void head_mfma_kernel(HeadArgs a) {
     }
   }
   __syncthreads();
-  HEAD_STAMP(1);
 
-  // ---- 1) logits: wave = (16-row M tile mt, K quarter kq); partials in LDS ----
-  {
-    const int mt = wave & 3, kq = wave >> 2;
-    const int r = lane & 15, hk = lane >> 4;
+  const int r = lane & 15, hk = lane >> 4;
+  {  // ---- logits partials: wave = K quarter ----
     const int kper = ((K + 3) / 4 + 3) & ~3;
-    const int kb = kq * kper, ke = min(K, kb + kper);
-    const int m = min(mt * 16 + r, M - 1);
-    const bool okm = mt * 16 + r < M, okj = r < NCLS;
+    const int kb = wave * kper, ke = min(K, kb + kper);
+    const int m = min(r, mrows - 1);
+    const bool okm = r < mrows, okj = r < NCLS;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int k = kb; k < ke; k += 4) {
       const int kk = k + hk;
@@ -187,77 +182,135 @@ __global__ __launch_bounds__(HT) void head_mfma_kernel(HeadArgs a) {
     for (int i = 0; i < 4; ++i) part[(4 * hk + i) * 16 + r] = acc[i];
   }
   __syncthreads();
-  for (int e = tid; e < MPAD * NCLS; e += HT) {   // reduce the 4 K quarters
-    const int row = e / NCLS, j = e % NCLS, mt = row >> 4, rr = row & 15;
+  if (tid < RG * NCLS) {
+    const int row = tid / NCLS, j = tid % NCLS;
     float v = 0.f;
 #pragma unroll
-    for (int kq = 0; kq < 4; ++kq) v += s_part[(kq * 4 + mt) * 256 + rr * 16 + j];
-    s_log[e] = row < M ? v : 0.f;
+    for (int q = 0; q < 4; ++q) v += s_part[q * 256 + row * 16 + j];
+    s_log[tid] = row < mrows ? v : 0.f;
   }
   __syncthreads();
-  HEAD_STAMP(2);
 
-  // ---- 2) loss / dlogits / accuracy / bookkeeping ----
-  head_loss(a, idx, s_log, s_red, s_cor, my_label);
-  __syncthreads();
-  HEAD_STAMP(3);
-
-  // ---- 3) dWh[k][j] = sum_m T(h)[m][k] dl[m][j]: 16-row k tiles over the waves ----
-  {
-    const int r = lane & 15, hk = lane >> 4;
-    for (int kt = wave; kt * 16 < K; kt += NW) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int k = kt * 16 + r;
-      const int kc = min(k, K - 1);
-      for (int m = 0; m < M; m += 4) {
-        const int mm = m + hk;                     // s_log rows >= M are zero
-        const float hv = s_h[min(mm, M - 1) * KP + kc];
-        const float lv = s_log[mm * NCLS + (r < NCLS ? r : 0)];
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, r < NCLS ? lv : 0.f, acc, 0, 0, 0);
-      }
-      if (r < NCLS) {
+  // ---- loss / dlogits / #correct for this group's rows (one lane per row) ----
+  float lsum = 0.f;
+  int cor = 0;
+  if (tid < mrows) {
+    const int y = my_label;
+    float* row = s_log + tid * NCLS;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kr = kt * 16 + 4 * hk + i;
-          if (kr < K) a.dw[kr * NCLS + r] = acc[i];
-        }
+    for (int j = 0; j < NCLS; ++j) row[j] += a.b[j];
+    float mx = row[0];
+    int am = 0;
+#pragma unroll
+    for (int j = 1; j < NCLS; ++j)
+      if (row[j] > mx) { mx = row[j]; am = j; }
+    cor = (am == y);
+    if (a.logits_out) {
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) a.logits_out[(long)(m0 + tid) * NCLS + j] = row[j];
+    }
+    if (a.loss == 0) {
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) se += __expf(row[j] - mx);
+      const float lse = mx + __logf(se);
+      lsum = lse - row[y];
+      const float inv = a.grad_scale / (float)M;
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) row[j] = (__expf(row[j] - lse) - (j == y ? 1.f : 0.f)) * inv;
+    } else {
+      const float inv = 2.f * a.grad_scale / (float)(M * NCLS);
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) {
+        const float d = row[j] - (j == y ? 1.f : 0.f);
+        lsum += d * d;
+        row[j] = d * inv;
       }
     }
   }
-  HEAD_STAMP(4);
+  if (wave == 0) {
+    lsum = wave_sum(lsum);
+    const unsigned long long ball = __ballot(cor != 0);
+    if (lane == 0) {
+      atomicAdd(reinterpret_cast<float*>(ws + 1), lsum);
+      atomicAdd(ws + 2, __popcll(ball));
+    }
+  }
+  __syncthreads();
+  if (tid < NCLS) {   // dbh partial
+    float acc = 0.f;
+    for (int m = 0; m < mrows; ++m) acc += s_log[m * NCLS + tid];
+    atomicAdd(&a.db[tid], acc);
+  }
 
-  // ---- 4) dh[m][k] = (sum_j dl[m][j] Wh[k][j]) * T'(h): (16-row m, 16-col k) tiles ----
+  // ---- dWh partial[k][j] = sum_{rows} T(h)[m][k] dl[m][j]: 16-k tiles over the waves ----
+  for (int kt = wave; kt * 16 < K; kt += 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int kc = min(kt * 16 + r, K - 1);
+#pragma unroll
+    for (int m = 0; m < RG; m += 4) {
+      const int mm = m + hk;                       // s_log rows >= mrows are zero
+      const float hv = s_h[min(mm, mrows - 1) * KP + kc];
+      const float lv = s_log[mm * NCLS + (r < NCLS ? r : 0)];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, r < NCLS ? lv : 0.f, acc, 0, 0, 0);
+    }
+    if (r < NCLS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kr = kt * 16 + 4 * hk + i;
+        if (kr < K) atomicAdd(&a.dw[kr * NCLS + r], acc[i]);
+      }
+    }
+  }
+
+  // ---- dh rows[m][k] = (sum_j dl[m][j] Wh[k][j]) * T'(h): 16-col k tiles over the waves ----
   if (a.dh) {
-    const int r = lane & 15, hk = lane >> 4;
-    const int nkt = (K + 15) / 16;
-    const int nmt = (M + 15) / 16;
-    for (int t = wave; t < nmt * nkt; t += NW) {
-      const int mt = t / nkt, kt = t % nkt;
+    for (int kt = wave; kt * 16 < K; kt += 4) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int m = mt * 16 + r, k = kt * 16 + r;
+      const int k = kt * 16 + r;
 #pragma unroll
       for (int j = 0; j < 12; j += 4) {            // 10 classes -> 3 k-steps of 4
         const int jj = j + hk;
         const bool okj = jj < NCLS;
-        const float lv = s_log[m * NCLS + (okj ? jj : 0)];    // m < 64: rows >= M zero
+        const float lv = s_log[r * NCLS + (okj ? jj : 0)];
         const float wv = s_w[min(k, K - 1) * NCLS + (okj ? jj : 0)];
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(okj ? lv : 0.f, (okj && k < K) ? wv : 0.f, acc, 0, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int mr = mt * 16 + 4 * hk + i;
-        if (mr < M && k < K) {
-          float g = acc[i];
+        const int mr = 4 * hk + i;
+        if (mr < mrows && k < K) {
+          float gv = acc[i];
           if (a.in_act) {  // post-activation value decides every supported derivative
             const float y = s_h[mr * KP + k];
-            g = act_bwd(g, y, y, a.in_act, a.in_alpha);
+            gv = act_bwd(gv, y, y, a.in_act, a.in_alpha);
           }
-          a.dh[(long)mr * K + k] = g;
+          a.dh[(long)(m0 + mr) * K + k] = gv;
         }
       }
     }
   }
-  HEAD_STAMP(5);
+
+  // ---- last workgroup: metric ring + step counter, re-arm the workspace ----
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(ws, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old == (int)gridDim.x - 1);
+  }
+  __syncthreads();
+  if (s_last && tid == 0) {
+    const float tot = __hip_atomic_load(reinterpret_cast<float*>(ws + 1), __ATOMIC_ACQUIRE,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    const int ncor = __hip_atomic_load(ws + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t st = *a.step;
+    const int pos = (int)(st % a.ring);
+    a.ring_loss[pos] = (a.loss == 0) ? tot / M : tot / (M * NCLS);
+    a.ring_correct[pos] = ncor;
+    *a.step = st + 1;
+    __hip_atomic_store(reinterpret_cast<float*>(ws + 1), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ws + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ws, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.
@@ -317,19 +370,21 @@ CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, c
                      const float* b, const int64_t* labels, const int64_t* idx, int loss,
                      float grad_scale, float* dw, float* db, float* dh, float* logits_out,
                      int64_t* step, float* ring_loss, int* ring_correct, int ring,
-                     const int64_t* cursor, hipStream_t st) {
+                     const int64_t* cursor, int* ws, hipStream_t st) {
   if (M <= 0 || M > 4096) return -1;
   HeadArgs a{h, M, K, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dw, db, dh,
-             logits_out, step, ring_loss, ring_correct, ring, nullptr};
-  if (const char* e = getenv("CSA_HEAD_DBG")) a.dbg = (long long*)strtoull(e, nullptr, 0);
-  const size_t mfma_lds =
-      ((size_t)MPAD * NCLS + 32 + NW * 256 + (size_t)K * NCLS + (size_t)M * (K + 1)) * sizeof(float);
-  if (M <= MPAD && K % 4 == 0 && mfma_lds <= HEAD_LDS_MAX) {
-    static bool attr_set = hipFuncSetAttribute((const void*)head_mfma_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)HEAD_LDS_MAX) == hipSuccess;
-    (void)attr_set;
-    hipLaunchKernelGGL(head_mfma_kernel, dim3(1), dim3(HT), mfma_lds, st, a);
+             logits_out, step, ring_loss, ring_correct, ring};
+  // dW/db are ACCUMULATED (the caller zeroes them every step); ws = int[4] zeroed once
+  const size_t rows_lds =
+      ((size_t)RG * NCLS + 4 * 256 + 8 + (size_t)K * NCLS + (size_t)RG * (K + 1)) * sizeof(float);
+  if (K % 4 == 0 && rows_lds <= HEAD_LDS_MAX && ws) {
+    if (rows_lds > 64 * 1024) {
+      static bool attr_set = hipFuncSetAttribute((const void*)head_rows_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)HEAD_LDS_MAX) == hipSuccess;
+      if (!attr_set) return -3;
+    }
+    hipLaunchKernelGGL(head_rows_kernel, dim3((M + RG - 1) / RG), dim3(RT), rows_lds, st, a, ws);
   } else {
     const size_t base = ((size_t)M * NCLS + 32) * sizeof(float);
     hipLaunchKernelGGL(head_generic_kernel, dim3(1), dim3(HT), base, st, a);

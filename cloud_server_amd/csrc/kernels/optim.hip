@@ -8,7 +8,10 @@
 //
 // Side jobs folded into the same launch (each would otherwise be its own tiny launch):
 //   * zero the split-K / atomic accumulators the NEXT step's kernels add into,
-//   * update BatchNorm running statistics from this step's forward partial slabs.
+//   * fold striped gradient accumulators: a conv weight gradient is accumulated by
+//     hundreds of workgroups into S stripes (S x fewer atomics per cache line, see
+//     conv.hip); the update of those parameters reads g = sum of the S stripes,
+//   * advance the batch-stream cursor.
 #include "common.h"
 
 namespace csa {
@@ -16,21 +19,64 @@ namespace csa {
 enum Opt : int { OPT_SGD = 0, OPT_ADAGRAD = 1, OPT_ADAM = 2, OPT_ADADELTA = 3 };
 
 constexpr int MAXZ = 16;
-constexpr int MAXBN = 8;
+constexpr int MAXF = 8;
 
 struct ZeroList { float* p[MAXZ]; long n[MAXZ]; int count; };
 
-struct BNRun {
-  const float* slab; int nslab; int C; float count; float* rmean; float* rvar; float momentum;
-};
-struct BNRunList { BNRun r[MAXBN]; int count; };
+// g[off + e] = sum_s src[s * ld + e] for e < n (flat-buffer offsets; off % 4 == 0);
+// the stripes are re-zeroed by the thread that folds them (their only reader)
+struct Fold { long off, n, ld; float* src; int S; };
+struct FoldList { Fold f[MAXF]; int count; long lo, hi; };
 
 struct OptArgs {
   int opt; float* w; const float* g; float* s0; float* s1; long n;
+  float* gz;                       // if set (== g): each thread zeroes the gradient it read
   float lr; const int64_t* step;   // 1-based step AFTER the head kernel's increment
-  ZeroList z; BNRunList bn;
+  ZeroList z; FoldList fold;
   int64_t* cursor;                 // batch-stream cursor: += 1 at the end of the step
 };
+
+constexpr int MAXS = 16;   // stripes per folded gradient
+
+__device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g) {
+  float gs[4] = {g.x, g.y, g.z, g.w};
+  for (int k = 0; k < fl.count; ++k) {
+    const Fold& f = fl.f[k];
+    if (e + 3 < f.off || e >= f.off + f.n) continue;
+    const long i0 = e - f.off;
+    if (i0 >= 0 && i0 + 4 <= f.n && (f.ld & 3) == 0) {
+      // whole float4 inside the segment: all stripes' loads in flight together
+      float4 v[MAXS];
+#pragma unroll
+      for (int s2 = 0; s2 < MAXS; ++s2)
+        v[s2] = s2 < f.S ? *reinterpret_cast<const float4*>(f.src + s2 * f.ld + i0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int s2 = 0; s2 < MAXS; ++s2) {
+        acc.x += v[s2].x; acc.y += v[s2].y; acc.z += v[s2].z; acc.w += v[s2].w;
+        if (s2 < f.S) *reinterpret_cast<float4*>(f.src + s2 * f.ld + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      gs[0] = acc.x; gs[1] = acc.y; gs[2] = acc.z; gs[3] = acc.w;
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // segment edge: per element
+      const long i = i0 + j;
+      if (i < 0 || i >= f.n) continue;
+      float v[MAXS];
+#pragma unroll
+      for (int s2 = 0; s2 < MAXS; ++s2) v[s2] = s2 < f.S ? f.src[s2 * f.ld + i] : 0.f;
+      float acc = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < MAXS; ++s2) {
+        acc += v[s2];
+        if (s2 < f.S) f.src[s2 * f.ld + i] = 0.f;
+      }
+      gs[j] = acc;
+    }
+  }
+  return make_float4(gs[0], gs[1], gs[2], gs[3]);
+}
 
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,7 +93,12 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   float4* s14 = (float4*)a.s1;
   for (long i = tid; i < n4; i += nth) {
     float4 w = w4[i];
-    const float4 g = g4[i];
+    float4 g = g4[i];
+    // Zeroing the accumulators the next step adds into must not race with this read:
+    // a zero-list pass over flat-gradient ranges run by OTHER threads could clear an
+    // element before its owner read it, so the owner clears what it read.
+    if (a.gz) reinterpret_cast<float4*>(a.gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i * 4 + 3 >= a.fold.lo && i * 4 < a.fold.hi) g = fold_grad(a.fold, i * 4, g);
     float* wp = (float*)&w;
     const float* gp = (const float*)&g;
     if (a.opt == OPT_SGD) {
@@ -97,45 +148,36 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     for (long i = tid; i < n; i += nth) p[i] = 0.f;
   }
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) *a.cursor += 1;
-  // BN running statistics (one block)
-  if (blockIdx.x == gridDim.x - 1) {
-    for (int r = 0; r < a.bn.count; ++r) {
-      const BNRun& b = a.bn.r[r];
-      for (int c = threadIdx.x; c < b.C; c += blockDim.x) {
-        float s1 = 0.f, s2 = 0.f;
-        for (int i = 0; i < b.nslab; ++i) {
-          s1 += b.slab[(size_t)i * 2 * b.C + c];
-          s2 += b.slab[(size_t)i * 2 * b.C + b.C + c];
-        }
-        const float mean = s1 / b.count;
-        const float var = fmaxf(s2 / b.count - mean * mean, 0.f);
-        b.rmean[c] = (1.f - b.momentum) * b.rmean[c] + b.momentum * mean;
-        b.rvar[c] = (1.f - b.momentum) * b.rvar[c] + b.momentum * var;
-      }
-    }
-  }
 }
 
 }  // namespace csa
 
 using namespace csa;
 
-// zero_ptrs/zero_ns: count <= 16 regions; bn_*: count <= 8 descriptors, arrays of length count.
-CSA_API int csa_optimizer(int opt, float* w, const float* g, float* s0, float* s1, long n, float lr,
-                          const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
-                          int nzero, const float* const* bn_slabs, const int* bn_nslab,
-                          const int* bn_C, const float* bn_count, float* const* bn_rmean,
-                          float* const* bn_rvar, float momentum, int nbn, int64_t* cursor,
+// zero_ptrs/zero_ns: count <= 16 regions; fold_*: count <= 8 striped-gradient descriptors.
+// zero_grad != 0: the update clears g[i] after reading it (g is then an accumulator that
+// must start the next step at zero); zero_ptrs must NOT overlap g or the fold stripes.
+CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, long n, int zero_grad,
+                          float lr, const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
+                          int nzero, const long* fold_off, const long* fold_n, float* const* fold_src,
+                          const int* fold_S, const long* fold_ld, int nfold, int64_t* cursor,
                           hipStream_t st) {
-  if (n % 4 || nzero > MAXZ || nbn > MAXBN) return -1;
+  if (n % 4 || nzero > MAXZ || nfold > MAXF) return -1;
   OptArgs a{};
   a.cursor = cursor;
   a.opt = opt; a.w = w; a.g = g; a.s0 = s0; a.s1 = s1; a.n = n; a.lr = lr; a.step = step;
+  a.gz = zero_grad ? g : nullptr;
   a.z.count = nzero;
   for (int i = 0; i < nzero; ++i) { a.z.p[i] = zero_ptrs[i]; a.z.n[i] = zero_ns[i]; }
-  a.bn.count = nbn;
-  for (int i = 0; i < nbn; ++i)
-    a.bn.r[i] = BNRun{bn_slabs[i], bn_nslab[i], bn_C[i], bn_count[i], bn_rmean[i], bn_rvar[i], momentum};
+  a.fold.count = nfold;
+  a.fold.lo = nfold ? fold_off[0] : 0;
+  a.fold.hi = 0;
+  for (int i = 0; i < nfold; ++i) {
+    if (fold_off[i] % 4 || fold_S[i] > MAXS || fold_S[i] < 1) return -1;
+    a.fold.f[i] = Fold{fold_off[i], fold_n[i], fold_ld[i], fold_src[i], fold_S[i]};
+    a.fold.lo = fold_off[i] < a.fold.lo ? fold_off[i] : a.fold.lo;
+    a.fold.hi = fold_off[i] + fold_n[i] > a.fold.hi ? fold_off[i] + fold_n[i] : a.fold.hi;
+  }
   long n4 = n / 4;
   int blocks = (int)((n4 + 255) / 256);
   if (blocks > 2048) blocks = 2048;

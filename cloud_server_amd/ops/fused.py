@@ -35,15 +35,15 @@ _SIGS = {
     "csa_dense_dgrad_slabs": (I, [I, I, I]),
     "csa_dense_wgrad_splits": (I, [I, I, I]),
     "csa_dense_wgrad": (I, [P, P, P, P, I, I, I, P, I, I, F, F, P, P, I, F, F, P]),
-    "csa_conv_wgrad": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I,
+    "csa_conv_wgrad": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I,
                            P, I, F, F, P, P, I, F, P, P]),
     "csa_conv_fwd_nslab": (I, [P, P]),
     "csa_conv_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, F, F, P, P, I, F, I, F, P, P]),
     "csa_route_bwd": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, I, P, P, P, P, F, P]),
     "csa_conv_dgrad_nslab": (I, [P]),
     "csa_conv_dgrad": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, P]),
-    "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P]),
-    "csa_optimizer": (I, [I, P, P, P, P, L, F, P, P, P, I, P, P, P, P, P, P, F, I, P, P]),
+    "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P, P]),
+    "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
     "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),

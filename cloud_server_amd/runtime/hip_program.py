@@ -82,9 +82,14 @@ class Unit:
     dc: Optional[torch.Tensor] = None       # conv: grad wrt pre-act conv output
     splits_fwd: int = 1
     xt: Optional[torch.Tensor] = None       # dense: materialised act(bn(x)) (BN inputs)
+    wg_stripes: int = 1                     # conv: weight-gradient accumulator stripes
+    dw_acc: Optional[torch.Tensor] = None   # conv: [stripes][taps*Cout] (or the flat-grad view)
+    db_acc: Optional[torch.Tensor] = None   # conv: [stripes][Cout] (or the flat-grad view)
 
 
 class HipProgram:
+    WGRAD_STRIPES = 16
+
     def __init__(self, eng):
         self.e = eng
         self.lib = K.load(required=True)
@@ -116,7 +121,9 @@ class HipProgram:
         sample config that is one ~1 MB bucket (head+fc2) launched after fc2, the 8 MB
         fc1 bucket launched right after fc1's weight gradient, and a small tail."""
         e = self.e
-        self.wsplit = os.environ.get("CSA_WGRAD_STREAM", "1") == "1"
+        # measured on MI355X: the forked stream costs more in cross-queue sync than it
+        # overlaps (207 -> 233 us/step, profiles/r1_ab_wgrad_stream.txt), so it is opt-in
+        self.wsplit = os.environ.get("CSA_WGRAD_STREAM", "0") == "1"
         if self.wsplit:
             self.wstream = torch.cuda.Stream(e.device)
         self.overlap = (e.ctx.enabled and e.sync.strategy == "allreduce" and
@@ -269,8 +276,16 @@ class HipProgram:
         self.idx = None
 
     def _collect_zero_regions(self) -> None:
+        """Accumulators that must start every step at zero.  ``zero_regions`` are cleared
+        by the optimizer's zero-list pass; flat-gradient accumulators are cleared by the
+        update itself (each thread zeroes the gradient it read — a separate pass over the
+        same memory would race with the reads), except under the sharded "ps" strategy,
+        where the update reads the reduce-scattered shard and the flat ranges go to the
+        zero list; conv weight-gradient stripes are cleared by the fold that reads them."""
         B = self.B
-        regs = []
+        regs: List[torch.Tensor] = []
+        flat: List[torch.Tensor] = []
+        self.stripe_bufs: List[torch.Tensor] = []
         for k, u in enumerate(self.units):
             lp = u.layer
             if u.kind == "dense":
@@ -283,28 +298,45 @@ class HipProgram:
                     if self.lib.csa_dense_dgrad_splits(B, fin, fout, int(tfm)) > 1:
                         regs.append(self.units[k - 1].dy)
                 if self.lib.csa_dense_wgrad_splits(B, fin, fout) > 1:
-                    regs.append(self.gviews[f"{lp.name}.weight"].view(-1))
-                    regs.append(self.gviews[f"{lp.name}.bias"])
+                    flat.append(self.gviews[f"{lp.name}.weight"].view(-1))
+                    flat.append(self.gviews[f"{lp.name}.bias"])
             else:
-                regs.append(self.gviews[f"{lp.name}.weight"].view(-1))
-                if lp.spec.bias:
-                    regs.append(self.gviews[f"{lp.name}.bias"])
+                # conv weight gradients: S stripes on one GPU (folded by the optimizer),
+                # accumulated straight into the flat gradient under data parallelism
+                S = 1 if self.e.ctx.enabled else self.WGRAD_STRIPES
+                u.wg_stripes = S
+                nw = self.gviews[f"{lp.name}.weight"].numel()
+                if S > 1:       # zeroed by the optimizer's fold (their only reader)
+                    u.dw_acc = torch.zeros(S, nw, device=self.e.device)
+                    u.db_acc = torch.zeros(S, lp.spec.cout, device=self.e.device) if lp.spec.bias else None
+                    self.stripe_bufs += [t for t in (u.dw_acc, u.db_acc) if t is not None]
+                else:
+                    u.dw_acc = self.gviews[f"{lp.name}.weight"]
+                    u.db_acc = self.gviews[f"{lp.name}.bias"] if lp.spec.bias else None
+                    flat.append(u.dw_acc.view(-1))
+                    if lp.spec.bias:
+                        flat.append(u.db_acc.view(-1))
                 if u.pool is not None:
                     pk, ps = u.pool.spec.kernel, u.pool.spec.stride
                     if tuple(pk) != tuple(ps):
                         regs.append(u.dc.view(-1))
+        # the head accumulates dWh/dbh across its row-group workgroups
+        flat.append(self.e.flat_grad[self.e.model.state.offsets["head.weight"]:])
+        self.head_ws = torch.zeros(4, dtype=torch.int32, device=self.e.device)   # arrival counter + sums
         for u in self.units:
             if u.in_tf.has_bn:
                 regs.append(u.in_tf.slab.view(-1))          # forward stats (atomic rows)
                 if u.kind == "conv":
                     regs.append(u.in_tf.bwd_slab.view(-1))  # conv dgrad folds rows atomically
-        self.zero_regions = regs
-        if len(regs) > 16:
+        self.ps_mode = self.e.sync.strategy == "ps" and self.e.ctx.enabled
+        self.zero_regions = regs + (flat if self.ps_mode else [])
+        if len(self.zero_regions) > 16:
             raise Unsupported("too many accumulator regions")
 
     def _zero_now(self) -> None:
-        for r in self.zero_regions:
+        for r in self.zero_regions + self.stripe_bufs:
             r.zero_()
+        self.e.flat_grad.zero_()
 
     def reset_after_warmup(self) -> None:
         self._zero_now()
@@ -397,7 +429,7 @@ class HipProgram:
             0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
             K.ptr(G["head.weight"]), K.ptr(G["head.bias"]), K.ptr(last.dy), None,
             K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(),
-            K.ptr(cur), st), "head")
+            K.ptr(cur), K.ptr(self.head_ws), st), "head")
         self._grad_ready("head")
 
         # ---------------- backward ----------------
@@ -461,7 +493,7 @@ class HipProgram:
                 ws = self._fork_wgrad(st)
                 self._rc(lib.csa_conv_wgrad(
                     None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
-                    K.ptr(dc), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]) if sp.bias else None,
+                    K.ptr(dc), K.ptr(u.dw_acc), K.ptr(u.db_acc) if sp.bias else None, u.wg_stripes,
                     B, h, w, lp.in_shape.c, sp.kh, sp.kw, sp.stride[0], sp.stride[1], lp.pads[0], lp.pads[2],
                     oh, ow, sp.cout, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], in_act, in_alpha,
                     K.ptr(cur) if raw else None, ws), "conv_wgrad")
@@ -492,17 +524,25 @@ class HipProgram:
         s1 = e.slots[1] if e.slots.shape[0] > 1 else None
         zp = (C.c_void_p * 16)(*[r.data_ptr() for r in self.zero_regions])
         zn = (C.c_long * 16)(*[r.numel() for r in self.zero_regions])
-        bns = []   # BN running statistics are updated by csa_route_bwd (block 0)
-        nb = len(bns)
-        slabs = (C.c_void_p * 8)(*[tf.slab.data_ptr() for tf, _ in bns])
-        nsl = (C.c_int * 8)(*[tf.nslab for tf, _ in bns])
-        cs = (C.c_int * 8)(*[tf.slab.shape[2] for tf, _ in bns])
-        cnt = (C.c_float * 8)(*[tf.count for tf, _ in bns])
-        rm = (C.c_void_p * 8)(*[getattr(self.model, f"bn{tf.norm.index}_mean").data_ptr() for tf, _ in bns])
-        rv = (C.c_void_p * 8)(*[getattr(self.model, f"bn{tf.norm.index}_var").data_ptr() for tf, _ in bns])
+        folds = []          # striped conv weight gradients -> summed inside the update
+        offs = self.model.state.offsets
+        for u in self.units:
+            if u.kind == "conv" and u.wg_stripes > 1:
+                lp = u.layer
+                folds.append((offs[f"{lp.name}.weight"], u.dw_acc.shape[1], u.dw_acc, u.wg_stripes))
+                if u.db_acc is not None:
+                    folds.append((offs[f"{lp.name}.bias"], u.db_acc.shape[1], u.db_acc, u.wg_stripes))
+        if len(folds) > 8:
+            raise Unsupported("more than 8 striped gradients")
+        fo = (C.c_long * 8)(*[f[0] for f in folds])
+        fn = (C.c_long * 8)(*[f[1] for f in folds])
+        fs = (C.c_void_p * 8)(*[f[2].data_ptr() for f in folds])
+        fS = (C.c_int * 8)(*[f[3] for f in folds])
+        fl = (C.c_long * 8)(*[f[1] for f in folds])
         self._rc(lib.csa_optimizer(
-            e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), float(e.lr), K.ptr(e.dstep),
-            zp, zn, len(self.zero_regions), slabs, nsl, cs, cnt, rm, rv, float(self.model.bn_momentum), nb,
+            e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), 0 if self.ps_mode else 1,
+            float(e.lr), K.ptr(e.dstep),
+            zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, len(folds),
             K.ptr(e.stream.cursor), st), "optimizer")
         if e.sync.strategy == "ps" and e.ctx.enabled:
             e.sync.all_gather_params(e.flat)

@@ -98,21 +98,5 @@ def main() -> int:
     return 0
 
 
-def head_stamps():
-    """Phase timestamps of the head kernel (CSA_HEAD_DBG points at a device buffer)."""
-    buf = torch.zeros(8, dtype=torch.int64, device="cuda")
-    os.environ["CSA_HEAD_DBG"] = str(buf.data_ptr())
-    cfg = parse_train_config(dict(SAMPLE_CONFIG, options={"batch_size": 50}))
-    eng = TrainEngine(cfg, synthetic_mnist(600), device="cuda", backend="hip", use_graph=False)
-    for _ in range(5):
-        eng.step()
-    torch.cuda.synchronize()
-    t = buf.tolist()
-    print("head phase cycles (s_memtime, 100MHz ref):", [t[i + 1] - t[i] for i in range(5)])
-    del os.environ["CSA_HEAD_DBG"]
-
-
 if __name__ == "__main__":
-    if os.environ.get("MB_HEAD"):
-        head_stamps()
     sys.exit(main())
