@@ -57,7 +57,8 @@ struct LoadRowMajor {          // elem(r, c) = p[r * ld + c]
   __device__ float post(float v, int r, int c) const { return (r < rows && c < cols) ? v : 0.f; }
 };
 
-template <bool V4 = false>
+// ONES: row r == rows reads as 1 (c < cols) — the bias-gradient row of a weight gradient.
+template <bool V4 = false, bool ONES = false>
 struct LoadColMajor {          // elem(r, c) = p[c * ld + r]
   const float* p; long ld; int rows, cols;
   static constexpr bool KCONTIG = false;
@@ -72,7 +73,10 @@ struct LoadColMajor {          // elem(r, c) = p[c * ld + r]
     const bool ok = r < rows && c < cols;
     return p[ok ? (long)c * ld + r : 0];
   }
-  __device__ float post(float v, int r, int c) const { return (r < rows && c < cols) ? v : 0.f; }
+  __device__ float post(float v, int r, int c) const {
+    if (ONES && r == rows) return c < cols ? 1.f : 0.f;
+    return (r < rows && c < cols) ? v : 0.f;
+  }
 };
 
 // Activation tensor X[m][f] read through an optional BN-apply (channel = f % C) and act.
@@ -112,14 +116,21 @@ struct EpiStore {              // C[m][n] (+)= v (+ bias[n] once); row m == M ->
   float* c; long ldc; int M, N; const float* bias; int atomic; float* extra; float scale;
   static constexpr bool NEEDS_LDS = false;
   __device__ void bind(const BNTables&) {}
-  __device__ void operator()(int m, int n, float v, bool first_split, float*) const {
+  // Global operands of the epilogue are fetched for all 16 elements of a lane BEFORE any
+  // store/atomic is issued: vmcnt counts loads, stores and atomics in issue order, so a
+  // load placed after an atomic waits for that atomic (measured: 16 serial round trips,
+  // ~15k cycles per workgroup, when the bias was read inside the store loop).
+  __device__ float prefetch(int, int n, bool first_split) const {
+    return (bias && first_split) ? bias[n < N ? n : 0] : 0.f;
+  }
+  __device__ void operator()(int m, int n, float v, bool first_split, float*, float aux) const {
     if (n >= N) return;
     float* p;
     if (m < M) p = c + (long)m * ldc + n;
     else if (extra && m == M) p = extra + n;
     else return;
     v *= scale;
-    if (bias && first_split && m < M) v += bias[n];
+    if (bias && first_split && m < M) v += aux;
     if (atomic) atomicAdd(p, v); else *p = v;
   }
 };
@@ -132,9 +143,12 @@ struct EpiActBNBwd {
   BNTables t;
   static constexpr bool NEEDS_LDS = true;
   __device__ void bind(const BNTables& tt) { t = tt; }
-  __device__ void operator()(int m, int f, float g, bool, float* lds_acc) const {
+  __device__ float prefetch(int m, int f, bool) const {   // branch-free clamped load
+    const bool ok = m < M && f < F;
+    return x[ok ? (long)m * ld + f : 0];
+  }
+  __device__ void operator()(int m, int f, float g, bool, float* lds_acc, float xv) const {
     if (m >= M || f >= F) return;
-    float xv = x[(long)m * ld + f];
     int q, ch;
     C.divmod(f, q, ch);
     float z = has_bn ? xv * t.a[ch] + t.b[ch] : xv;
@@ -213,15 +227,37 @@ struct Stage {
 __device__ long long* g_gemm_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
 #define GEMM_STAMP(i)                                                                       \
   do {                                                                                      \
-    if (g_gemm_dbg && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) \
+    if (g_gemm_dbg && threadIdx.x == 0 && tid.x == 0 && tid.y == 0 && tid.z == 0)              \
       g_gemm_dbg[i] = (long long)__builtin_amdgcn_s_memtime();                               \
   } while (0)
+
+// XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs (block b and
+// b + 8 share one L2; MI355X_MICROARCH.md "Workgroup dispatch"), so with the natural order
+// the 16 N-tiles that re-read one split-K slice of the activations, and the 2 M-tiles that
+// re-read one weight tile, land on 8 different XCDs and every re-read goes to HBM/MALL.
+// The 1-D grid is instead mapped so that XCD x owns a contiguous range of tasks ordered
+// (split, N tile, M tile) fastest-last: re-reads hit that XCD's L2.  Speed only — any
+// placement is correct.  The grid is padded to a multiple of 8 (padding blocks exit).
+struct TileId { int x, y, z; bool valid; };
+__device__ __forceinline__ TileId gemm_tile(int X, int Y, int Z) {
+  const int L = blockIdx.x, G = gridDim.x;                 // G % 8 == 0
+  const int t = (L & 7) * (G >> 3) + (L >> 3);
+  TileId id;
+  id.valid = t < X * Y * Z;
+  id.y = t % Y;
+  id.x = (t / Y) % X;
+  id.z = t / (X * Y);
+  return id;
+}
 
 template <int WM, int WN, int WK, class LA, class LB, class EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
                                                        int k_per_split, BNRef bn, int bn_on,
-                                                       float* bn_slab_out, int slab_C) {
+                                                       float* bn_slab_out, int slab_C, int GX,
+                                                       int GY, int GZ) {
   static_assert(WM * WN * WK == 4, "4 waves per workgroup");
+  const TileId tid = gemm_tile(GX, GY, GZ);
+  if (!tid.valid) return;                 // whole workgroup: grid padding
   __shared__ float s_stage[4][2][KC * LDS_PAD];   // per-wave tiles; reused for the WK reduction
   __shared__ float s_bn[4 * MAXC];
   __shared__ float s_acc[2 * MAXC];
@@ -229,15 +265,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN);
   const int wm = wmn / WN, wn = wmn % WN;
-  const int m0 = blockIdx.y * 32 * WM + wm * 32;
-  const int n0 = blockIdx.x * 32 * WN + wn * 32;
+  const int m0 = tid.y * 32 * WM + wm * 32;
+  const int n0 = tid.x * 32 * WN + wn * 32;
   GEMM_STAMP(0);
   const BNTables tabs{s_bn, s_bn + MAXC, s_bn + 2 * MAXC, s_bn + 3 * MAXC};
   la.bind(tabs);
   lb.bind(tabs);
   epi.bind(tabs);
   // K range of this wave (multiples of KC keep every wave's chunks aligned)
-  const int ks0 = blockIdx.z * k_per_split;
+  const int ks0 = tid.z * k_per_split;
   const int ks1 = min(K, ks0 + k_per_split);
   const int klen = max(0, ks1 - ks0);
   const int kw_len = ((klen + WK - 1) / WK + 3) / 4 * 4;
@@ -269,10 +305,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
     if (it < 4) GEMM_STAMP(2 + it);
     ++it;
     stA.commit(la, sa, m0, k, ke);
+    if (it == 1) GEMM_STAMP(10);
     stB.commit(lb, sb, n0, k, ke);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (it == 1) GEMM_STAMP(11);
     if (k + KC < ke) {   // next chunk's global loads fly under the MFMAs
       stA.fetch(la, m0, k + KC, ke);
       stB.fetch(lb, n0, k + KC, ke);
@@ -283,12 +321,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
       float bv = sb[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
+    if (it == 1) GEMM_STAMP(12);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 
   GEMM_STAMP(6);
+  // epilogue operands (bias / forward activations) in flight under the WK reduction
+  const bool first = tid.z == 0;
+  float aux[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+    aux[i] = wk == 0 ? epi.prefetch(m0 + row, n0 + (lane & 31), first) : 0.f;
+  }
+  GEMM_STAMP(8);
   if (WK > 1) {  // intra-workgroup split-K reduction through LDS (each wave's own stage area)
     float* mine = s_stage[wave][0];
     __builtin_amdgcn_wave_barrier();
@@ -303,18 +351,18 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
       }
     }
   }
+  GEMM_STAMP(9);
   if (wk == 0) {
-    const bool first = blockIdx.z == 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-      epi(m0 + row, n0 + (lane & 31), acc[i], first, s_acc);
+      epi(m0 + row, n0 + (lane & 31), acc[i], first, s_acc, aux[i]);
     }
   }
   GEMM_STAMP(7);
   if (EPI::NEEDS_LDS && bn_slab_out) {
     __syncthreads();
-    const int slab_row = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int slab_row = (tid.z * GY + tid.y) * GX + tid.x;
     for (int i = threadIdx.x; i < 2 * slab_C; i += blockDim.x)
       bn_slab_out[(size_t)slab_row * 2 * slab_C + i] = s_acc[(i < slab_C) ? i : (MAXC + i - slab_C)];
   }
@@ -350,11 +398,14 @@ static int grid_slabs(const Plan& p, int M, int N) {
 template <class LA, class LB, class EPI>
 static int launch_gemm(const Plan& p, LA la, LB lb, EPI epi, int M, int N, int K, const BNRef& bn,
                        int bn_on, float* slab_out, int slab_C, hipStream_t st) {
-  dim3 grid((N + 32 * p.wn - 1) / (32 * p.wn), (M + 32 * p.wm - 1) / (32 * p.wm), p.splits);
+  const int GX = (N + 32 * p.wn - 1) / (32 * p.wn), GY = (M + 32 * p.wm - 1) / (32 * p.wm);
+  const int GZ = p.splits;
+  dim3 grid((unsigned)((GX * GY * GZ + 7) / 8 * 8));
 #define CSA_L(WM, WN, WK)                                                                   \
   hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, WK, LA, LB, EPI>), grid, dim3(256), 0, st, la, \
-                     lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C)
+                     lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ)
   if (p.wm == 2 && p.wn == 2) CSA_L(2, 2, 1);
+  else if (p.wm == 2 && p.wn == 1) CSA_L(2, 1, 2);
   else if (p.wm == 1 && p.wn == 2) CSA_L(1, 2, 2);
   else CSA_L(1, 1, 4);
 #undef CSA_L
@@ -404,9 +455,13 @@ CSA_API int csa_dense_fwd(const float* X, const float* W, const float* bias, flo
   BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
   EpiStore epi{Y, (long)N, M, N, bias, p.splits > 1, nullptr, 1.f};
   return dispatch2(K % 4 == 0 && K >= 4, N % 4 == 0 && N >= 4, [&](auto va, auto vb) {
+    LoadColMajor<decltype(vb)::value> lb{W, (long)N, N, K};          // B(k, n) = W[k][n]
+    if (!bn_slab && in_act == ACT_NONE) {   // plain operand: no per-element transform code
+      LoadRowMajor<decltype(va)::value> la{X, (long)K, M, K};
+      return launch_gemm(p, la, lb, epi, M, N, K, bn, 0, nullptr, 0, st);
+    }
     LoadBNAct<true, decltype(va)::value> la{X, (long)K, M, K, FastDiv(bn_C > 0 ? bn_C : 1), in_act,
                                              in_alpha, bn_slab != nullptr, 0, nullptr, nullptr};
-    LoadColMajor<decltype(vb)::value> lb{W, (long)N, N, K};          // B(k, n) = W[k][n]
     return launch_gemm(p, la, lb, epi, M, N, K, bn, bn_slab != nullptr, nullptr, 0, st);
   });
 }
@@ -466,9 +521,17 @@ CSA_API int csa_dense_wgrad(const float* X, const float* dY, float* dW, float* d
   BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
   EpiStore epi{dW, (long)Nout, Kin, Nout, nullptr, p.splits > 1, db, scale};
   return dispatch2(Kin % 4 == 0 && Kin >= 4, Nout % 4 == 0 && Nout >= 4, [&](auto va, auto vb) {
+    LoadColMajor<decltype(vb)::value> lb{dY, (long)Nout, Nout, M};   // B(k=m, n) = dY[m][n]
+    if (!bn_slab && in_act == ACT_NONE) {   // plain operand (+ ones row for the bias gradient)
+      if (db) {
+        LoadColMajor<decltype(va)::value, true> la{X, (long)Kin, Kin, M};   // A(f, m) = X[m][f]
+        return launch_gemm(p, la, lb, epi, Mg, Nout, M, bn, 0, nullptr, 0, st);
+      }
+      LoadColMajor<decltype(va)::value> la{X, (long)Kin, Kin, M};
+      return launch_gemm(p, la, lb, epi, Mg, Nout, M, bn, 0, nullptr, 0, st);
+    }
     LoadBNAct<false, decltype(va)::value> la{X, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), in_act,
                                               in_alpha, bn_slab != nullptr, db != nullptr, nullptr, nullptr};
-    LoadColMajor<decltype(vb)::value> lb{dY, (long)Nout, Nout, M};   // B(k=m, n) = dY[m][n]
     return launch_gemm(p, la, lb, epi, Mg, Nout, M, bn, bn_slab != nullptr, nullptr, 0, st);
   });
 }

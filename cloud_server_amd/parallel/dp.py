@@ -25,6 +25,7 @@ gloo (CPU tests) and RCCL (MI355X).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -45,6 +46,9 @@ class GradSync:
             raise ValueError("ps strategy needs the flat buffer padded to a multiple of world")
         self.shard = numel // ctx.world if ctx.enabled else numel
         self.bucket_elems = max(1, bucket_bytes // 4)
+        # grouped RCCL launches for the multi-tensor lowrank collectives (opt-in: a grouped
+        # collective inside HIP-graph capture crashed capture_end on ROCm 7 / torch 2.10)
+        self.coalesce = ctx.backend == "nccl" and os.environ.get("CSA_COALESCE", "0") == "1"
 
     @property
     def grad_scale(self) -> float:
@@ -93,6 +97,33 @@ class GradSync:
             out.copy_(local)
             return
         dist.all_gather_into_tensor(out, local.contiguous())
+
+    def all_gather_rows_many(self, pairs) -> None:
+        """Several ``all_gather_rows`` issued as ONE grouped RCCL launch where the backend
+        supports coalescing (each separate collective pays its own fixed latency)."""
+        if not self.ctx.enabled:
+            for local, out in pairs:
+                out.copy_(local)
+            return
+        if self.coalesce and len(pairs) > 1:
+            with dist._coalescing_manager(async_ops=False):
+                for local, out in pairs:
+                    dist.all_gather_into_tensor(out, local.contiguous())
+            return
+        for local, out in pairs:
+            dist.all_gather_into_tensor(out, local.contiguous())
+
+    def allreduce_ranges(self, flat: torch.Tensor, ranges) -> None:
+        """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one grouped launch on RCCL)."""
+        if not self.ctx.enabled or not ranges:
+            return
+        if self.coalesce and len(ranges) > 1:
+            with dist._coalescing_manager(async_ops=False):
+                for lo, hi in ranges:
+                    dist.all_reduce(flat[lo:hi])
+            return
+        for lo, hi in ranges:
+            dist.all_reduce(flat[lo:hi])
 
     def broadcast_params(self, flat_param: torch.Tensor) -> None:
         """Initial sync from rank 0 (reference: chief runs init_op, construct_distribute.py:379)."""

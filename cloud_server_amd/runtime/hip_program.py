@@ -101,6 +101,7 @@ class HipProgram:
         self.gviews = eng.model.state.views(eng.flat_grad)
         self._lower()
         self._alloc()
+        self._plan_lowrank()
         self.zero_regions: List[torch.Tensor] = []
         self._collect_zero_regions()
         self._zero_now()
@@ -150,6 +151,77 @@ class HipProgram:
             if hi - lo >= min_elems or (last and hi > lo):
                 self.bucket_at[key] = (lo, hi)
                 hi = lo
+
+    # ------------------------------------------------------------------ DP "lowrank"
+    def _plan_lowrank(self) -> None:
+        """Exact data parallelism for the dense layers without all-reducing their weights.
+
+        A dense weight gradient is ``Σ_ranks T(x_r)ᵀ·dy_r`` — a GEMM whose reduction
+        dimension is the per-rank batch (50).  So instead of an RCCL all-reduce of the
+        [in, out] gradient (8 MB for fc1 of the sample config; ring collectives over xGMI
+        are per-link bound), every rank all-gathers the [B, in] GEMM inputs and the
+        [B, out] output gradients (0.9 MB for fc1) and forms the global gradient locally
+        with K = world·B on a side stream that overlaps the conv backward.  The 1/world
+        mean is already folded into the loss-gradient seed.  Only the small remainder
+        (conv, BatchNorm, head: ~25 KB for the sample config) is all-reduced.  A dense
+        layer whose input goes through a BatchNorm that is not materialised per rank
+        (batch statistics differ between ranks) stays on the all-reduce path."""
+        e = self.e
+        self.lr_units: List[Unit] = []
+        self.lr_ranges: List[tuple] = []
+        if not (e.ctx.enabled and e.sync.strategy == "lowrank"):
+            return
+        W, B, dev = e.ctx.world, self.B, e.device
+        offs = self.model.state.offsets
+        taken = []
+        for u in self.units:
+            if u.kind != "dense" or (u.in_tf.has_bn and u.xt is None):
+                continue
+            fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
+            u.lr_src = u.xt if u.xt is not None else u.x.view(B, fin)
+            u.lr_act = (0, 0.0) if u.xt is not None else (_act_id(u.in_tf.act), _alpha(u.in_tf.act))
+            u.lr_x = torch.zeros(W * B, fin, device=dev)
+            u.lr_dy = torch.zeros(W * B, fout, device=dev)
+            for p in ("weight", "bias"):
+                n = f"{u.layer.name}.{p}"
+                taken.append((offs[n], offs[n] + self.gviews[n].numel()))
+            self.lr_units.append(u)
+        # everything else is all-reduced: the complement of the lowrank weight ranges
+        lo, end = 0, e.flat.numel()
+        for a, b in sorted(taken):
+            if a > lo:
+                self.lr_ranges.append((lo, a))
+            lo = max(lo, b)
+        if lo < end:
+            self.lr_ranges.append((lo, end))
+        if self.lr_units:
+            self.lr_side = torch.cuda.Stream(dev)
+            self.lr_first = min(self.units.index(u) for u in self.lr_units)
+
+    def _lowrank_gather_inputs(self) -> None:
+        """After the forward pass: all-gather the dense GEMM inputs on the side stream
+        (overlaps the head and the dense input-gradient GEMMs)."""
+        if not self.lr_units:
+            return
+        self.lr_side.wait_stream(torch.cuda.current_stream(self.e.device))
+        with torch.cuda.stream(self.lr_side):
+            self.e.sync.all_gather_rows_many([(u.lr_src, u.lr_x) for u in self.lr_units])
+
+    def _lowrank_wgrads(self) -> None:
+        """Once every lowrank unit's output gradient is final: gather them and form the
+        global weight gradients (K = world·B) on the side stream."""
+        lib, W, B, G = self.lib, self.e.ctx.world, self.B, self.gviews
+        self.lr_side.wait_stream(torch.cuda.current_stream(self.e.device))
+        with torch.cuda.stream(self.lr_side):
+            ss = self.lr_side.cuda_stream
+            self.e.sync.all_gather_rows_many([(u.dy.view(B, -1), u.lr_dy) for u in self.lr_units])
+            for u in self.lr_units:
+                lp = u.layer
+                fin, fout = lp.in_shape.numel, lp.spec.hidden
+                self._rc(lib.csa_dense_wgrad(
+                    K.ptr(u.lr_x), K.ptr(u.lr_dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+                    W * B, fin, fout, None, 0, 0, 0.0, 0.0, None, None, u.lr_act[0], u.lr_act[1], 1.0, ss),
+                    "dense_wgrad(lowrank)")
 
     def _fork_wgrad(self, st):
         """Weight gradients are off the critical path (nothing in this step reads them
@@ -420,6 +492,8 @@ class HipProgram:
                         K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
                         B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
 
+        self._lowrank_gather_inputs()
+
         # ---------------- head (loss, head grads, input grad, metrics) ----------------
         last = self.units[-1]
         hin = last.y.view(B, -1)
@@ -447,6 +521,11 @@ class HipProgram:
                         K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
                         K.ptr(xf), in_act, in_alpha, *self._bn_args_c(tf), K.ptr(tf.bwd_slab), st),
                         "slabs:dense_dgrad")
+                if u in self.lr_units:          # global wgrad formed after the gathers
+                    if k == self.lr_first:
+                        self._lowrank_wgrads()
+                    self._grad_ready(k)
+                    continue
                 ws = self._fork_wgrad(st)
                 if u.xt is not None:
                     self._rc(lib.csa_dense_wgrad(
@@ -509,6 +588,10 @@ class HipProgram:
             main.wait_stream(self.wstream)
         if self.overlap:
             main.wait_stream(self.side)
+        elif e.ctx.enabled and e.sync.strategy == "lowrank":
+            e.sync.allreduce_ranges(e.flat_grad, self.lr_ranges)
+            if self.lr_units:
+                main.wait_stream(self.lr_side)
         else:
             e.after_backward_sync()
         self._optimizer(st)

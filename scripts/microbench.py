@@ -58,7 +58,7 @@ def main() -> int:
     total = 0.0
     rows = []
     if os.environ.get("MB_GEMM"):
-        dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+        dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
         for i, (name, fn, args) in enumerate(rec.calls):
             if name in ("csa_dense_fwd", "csa_dense_dgrad", "csa_dense_wgrad", "csa_conv_wgrad"):
                 eng.program.lib.csa_gemm_debug(dbg.data_ptr())
@@ -66,7 +66,11 @@ def main() -> int:
                 torch.cuda.synchronize()
                 eng.program.lib.csa_gemm_debug(None)
                 t = dbg.tolist()
-                print(f"{i:2d} {name:18s} stamps:", [t[j + 1] - t[j] for j in range(7)])
+                last = max(j for j in range(2, 6) if t[j]) if any(t[2:6]) else 1
+                print(f"{i:2d} {name:18s} launch->k0 {t[2] - t[0] if t[2] else -1}  loop {t[6] - t[2] if t[2] else -1}"
+                      f" (iters {[t[j + 1] - t[j] for j in range(2, last)]})  prefetch {t[8] - t[6]}"
+                      f"  wk-reduce {t[9] - t[8]}  epilogue {t[7] - t[9]}  it0: commitA {t[10] - t[2]} commitB {t[11] - t[10]} mfma {t[12] - t[11]}")
+                dbg.zero_()
     for i, (name, fn, args) in enumerate(rec.calls):
         for _ in range(5):
             fn(*args)

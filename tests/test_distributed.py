@@ -69,6 +69,19 @@ def _collectives(rank, world, port, out):
     allrows = torch.zeros(3 * world, 5)
     ga.all_gather_rows(rows, allrows)
     ok &= torch.equal(allrows[3:], torch.ones(3, 5)) and torch.equal(allrows[:3], torch.zeros(3, 5))
+    # lowrank identity: sum_r X_r^T dY_r == X_all^T dY_all with rank-major gathered rows
+    gen = torch.Generator().manual_seed(rank)
+    x, dy = torch.randn(4, 6, generator=gen), torch.randn(4, 3, generator=gen)
+    xa, dya = torch.zeros(4 * world, 6), torch.zeros(4 * world, 3)
+    ga.all_gather_rows_many([(x, xa), (dy, dya)])
+    g_ar = x.t() @ dy
+    dist.all_reduce(g_ar)
+    ok &= torch.allclose(xa.t() @ dya, g_ar, atol=1e-5)
+    flat = torch.arange(12, dtype=torch.float32) * (rank + 1)
+    ga.allreduce_ranges(flat, [(0, 3), (8, 12)])
+    s = float(sum(range(1, world + 1)))
+    ok &= torch.equal(flat[:3], torch.arange(3.0) * s) and torch.equal(flat[8:], torch.arange(8.0, 12.0) * s)
+    ok &= torch.equal(flat[3:8], torch.arange(3.0, 8.0) * (rank + 1))
     out[rank] = bool(ok)
     dist.destroy_process_group()
 

@@ -48,3 +48,24 @@ def test_overlap_buckets_match_single_gpu(pg):
         a.step(); b.step()
     torch.cuda.synchronize()
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
+
+
+def test_lowrank_strategy_matches_single_gpu(pg):
+    """``lowrank`` DP: dense weight gradients from all-gathered GEMM inputs / output
+    gradients (K = world·B) on a side stream, the rest all-reduced — captured in the HIP
+    graph; world 1 must reproduce the single-GPU step."""
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdamOptimizer", learning_rate=1e-3))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy="lowrank")
+    assert a.backend == "hip", a.fallback_reason
+    names = [u.layer.name for u in a.program.lr_units]
+    assert len(names) == 2, names                      # fc1 (materialised BN input) and fc2
+    covered = sum(hi - lo for lo, hi in a.program.lr_ranges)
+    dense = sum(a.program.gviews[f"{n}.{p}"].numel() for n in names for p in ("weight", "bias"))
+    assert covered < a.flat.numel() - dense + 64 * 8   # only the remainder is all-reduced
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for _ in range(20):
+        a.step(); b.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
