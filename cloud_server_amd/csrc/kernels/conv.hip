@@ -17,10 +17,18 @@
 #include "common.h"
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace csa {
 
 constexpr int CONV_THREADS = 256;
+
+__device__ long long* g_conv_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
+#define CONV_STAMP(i)                                                                       \
+  do {                                                                                      \
+    if (g_conv_dbg && threadIdx.x == 0 && blockIdx.x == 0)                                  \
+      g_conv_dbg[i] = (long long)__builtin_amdgcn_s_memtime();                               \
+  } while (0)
 
 struct ConvGeom {
   int B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout;
@@ -372,6 +380,228 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs 
   }
 }
 
+
+// -----------------------------------------------------------------------------------
+// Conv forward as an implicit GEMM on v_mfma_f32_16x16x4_f32 (the VALU kernel above is
+// the fallback).  Rows = output pixels, K = taps (i, j, ci), columns = Cout.  The band's
+// input tile is staged ZERO-PADDED in LDS (with the input transform applied once per
+// element), the weights as a [K][Cout16] panel and a per-tap offset table, so an A
+// operand is ONE ds_read at (pixel base + tap offset) and the inner loop is branch-free.
+// With the fused 2x2 / stride-2 max-pool, the 16 rows of a tile are 4 pooled pixels x
+// their 4 window positions in the order that the MFMA D layout hands to one lane
+// (lane l holds rows 4*(l>>4)..+3 of column l&15): max + argmax stay in registers.
+// Bias, activation, pooled store, argmax and the BN partial statistics are fused.
+// 16x16x4 map: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15], D[4*(l>>4)+r][l&15].
+// -----------------------------------------------------------------------------------
+typedef float cf32x4 __attribute__((ext_vector_type(4)));
+
+struct ConvMfmaArgs {
+  ConvGeom g;
+  int pool_on;                  // 2x2 / stride 2 / no padding pool fused
+  int OHo, OWo;                 // unit-output geometry (pooled if pool_on)
+  int nbands, band_rows;        // unit-output rows per band
+  int tile_rows, tile_w;        // staged zero-padded input tile: rows x (Wp * Cin) floats
+  int kpad, c16;                // K rounded up to 4, Cout rounded up to 16
+  const float* x; const uint8_t* img; const int64_t* idx; const int64_t* cursor;
+  BNRef in_bn; int in_bn_on; int in_act; float in_alpha;
+  const float* w; const float* bias; int out_act; float out_alpha;
+  float* y; uint8_t* argmax; float* stat_slab; int nslab;
+};
+
+template <bool U8, bool POOL>
+__global__ __launch_bounds__(CONV_THREADS) void conv_fwd_mfma_kernel(ConvMfmaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  __shared__ float s_stat[2 * 128];
+  const ConvGeom& g = a.g;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x % a.nbands;
+  const int OWo = a.OWo;
+  const int r0 = band * a.band_rows, r1 = min(a.OHo, r0 + a.band_rows);
+  const int c0 = POOL ? 2 * r0 : r0;                // first conv-output row of the band
+  const int ty0 = c0 * g.SH - g.PT;                 // image row of tile row 0
+  const int tw = a.tile_w, ntile = a.tile_rows * tw;
+  float* s_x = smem;
+  float* s_w = smem + ((ntile + 3) & ~3);
+  int* s_koff = reinterpret_cast<int*>(s_w + a.kpad * a.c16);
+  const int K = g.KH * g.KW * g.Cin;
+  const int tid = threadIdx.x;
+
+  // ---- staging.  The band's input rows are ONE contiguous global range: the first
+  // batch of their loads is issued before anything else, so its round trip overlaps the
+  // LDS zero-fill, the weight panel / tap table and the BN table reduction.
+  const int iy0 = max(0, ty0), iy1 = min(g.H, ty0 + a.tile_rows);
+  const int irow = g.W * g.Cin;
+  const int nx = max(0, iy1 - iy0) * irow;
+  constexpr int U = 8;
+  using T = typename std::conditional<U8, uint8_t, float>::type;
+  const T* src;
+  if (U8) {
+    const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * g.B : a.idx;
+    src = reinterpret_cast<const T*>(a.img + idx[b] * (long)(g.H * irow) + (long)iy0 * irow);
+  } else {
+    src = reinterpret_cast<const T*>(a.x + ((long)b * g.H + iy0) * irow);
+  }
+  CONV_STAMP(0);
+  T v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { const int e = u * CONV_THREADS + tid; v[u] = src[e < nx ? e : 0]; }
+  CONV_STAMP(1);
+
+  for (int e = tid; e < ntile; e += CONV_THREADS) s_x[e] = 0.f;
+  const FastDiv dc16(a.c16);
+  for (int e = tid; e < a.kpad * a.c16; e += CONV_THREADS) {
+    int k, co;
+    dc16.divmod(e, k, co);
+    s_w[e] = (k < K && co < g.Cout) ? a.w[k * g.Cout + co] : 0.f;
+  }
+  for (int k = tid; k < a.kpad; k += CONV_THREADS) {
+    int off = 0;
+    if (k < K) {
+      const int ci = k % g.Cin, ij = k / g.Cin, i = ij / g.KW, j = ij - i * g.KW;
+      off = i * tw + j * g.Cin + ci;
+    }
+    s_koff[k] = off;
+  }
+  for (int i = tid; i < 2 * g.Cout; i += CONV_THREADS) s_stat[i] = 0.f;
+  if (!U8 && a.in_bn_on) bn_reduce_to_lds(a.in_bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
+  CONV_STAMP(2);
+  __syncthreads();
+  CONV_STAMP(3);
+  {  // scatter into the zero-padded rows (transform applied once per element)
+    float* dst0 = s_x + (iy0 - ty0) * tw + g.PL * g.Cin;
+    const int cmax = min(irow, tw - g.PL * g.Cin);   // VALID: columns past the last tap unused
+    const FastDiv drow(irow), dcin(g.Cin);
+    const int bn_on = a.in_bn_on, act = a.in_act;
+    const float alpha = a.in_alpha;
+    for (int base = 0; base < nx; base += CONV_THREADS * U) {
+      if (base > 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) { const int e = base + u * CONV_THREADS + tid; v[u] = src[e < nx ? e : 0]; }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * CONV_THREADS + tid;
+        if (e >= nx) continue;
+        int r, c;
+        drow.divmod(e, r, c);
+        if (c >= cmax) continue;
+        float t;
+        if (U8) {
+          t = (float)v[u] * (1.0f / 255.0f);
+        } else {
+          t = (float)v[u];
+          if (bn_on) { int q, ci; dcin.divmod(c, q, ci); t = t * s_bn[256 + ci] + s_bn[384 + ci]; }
+          t = act_fwd(t, act, alpha);
+        }
+        dst0[r * tw + c] = t;
+      }
+    }
+  }
+  __syncthreads();
+  CONV_STAMP(4);
+
+  // ---- MFMA over (row tiles) x (Cout tiles), K = taps ----
+  const int lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int ntn = a.c16 >> 4;
+  const int nunit = (r1 - r0) * OWo;                // unit-output pixels of the band
+  const int nmt = POOL ? (nunit + 3) >> 2 : (nunit + 15) >> 4;
+  const int ksteps = a.kpad >> 2;
+  float bias[8], bsum[8], bsq[8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) {
+    const int co = nt * 16 + lr;
+    bias[nt] = (nt < ntn && a.bias && co < g.Cout) ? a.bias[co] : 0.f;
+    bsum[nt] = 0.f;
+    bsq[nt] = 0.f;
+  }
+  for (int mt = wave; mt < nmt; mt += 4) {
+    // this lane's A row (pixel lr of the tile)
+    int cy, cx;
+    bool okr;
+    if (POOL) {
+      const int pp = mt * 4 + (lr >> 2), pos = lr & 3;
+      okr = pp < nunit;
+      const int ppc = okr ? pp : 0;
+      cy = 2 * (r0 + ppc / OWo) + (pos >> 1);
+      cx = 2 * (ppc % OWo) + (pos & 1);
+      okr = okr && cy < g.OH && cx < g.OW;
+    } else {
+      const int p = mt * 16 + lr;
+      okr = p < nunit;
+      const int pc = okr ? p : 0;
+      cy = r0 + pc / OWo;
+      cx = pc % OWo;
+    }
+    const int pixbase = okr ? (cy - c0) * g.SH * tw + cx * g.SW * g.Cin : 0;
+    cf32x4 acc[8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) acc[nt] = cf32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < ksteps; ++s2) {
+      const int k = 4 * s2 + lk;
+      const float av = s_x[pixbase + s_koff[k]];
+      const float* wrow = s_w + k * a.c16 + lr;
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+        if (nt < ntn) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wrow[nt * 16], acc[nt], 0, 0, 0);
+    }
+    if (mt == 0) CONV_STAMP(5);
+    // ---- epilogue: lane holds rows 4*lk .. 4*lk+3 of column lr ----
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      if (nt >= ntn) break;
+      const int co = nt * 16 + lr;
+      if (co >= g.Cout) continue;
+      if (POOL) {
+        const int pp = mt * 4 + lk;
+        if (pp >= nunit) continue;
+        const int py = r0 + pp / OWo, px = pp % OWo;
+        float out = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cyy = 2 * py + (r >> 1), cxx = 2 * px + (r & 1);
+          if (cyy >= g.OH || cxx >= g.OW) continue;
+          const float v = act_fwd(acc[nt][r] + bias[nt], a.out_act, a.out_alpha);
+          if (v > out) { out = v; am = r; }
+        }
+        const long o = (((long)b * a.OHo + py) * OWo + px) * g.Cout + co;
+        a.y[o] = out;
+        if (a.argmax) a.argmax[o] = (uint8_t)am;
+        bsum[nt] += out;
+        bsq[nt] += out * out;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = mt * 16 + 4 * lk + r;
+          if (p >= nunit) continue;
+          const float v = act_fwd(acc[nt][r] + bias[nt], a.out_act, a.out_alpha);
+          const int oy = r0 + p / OWo, ox = p % OWo;
+          a.y[(((long)b * a.OHo + oy) * OWo + ox) * g.Cout + co] = v;
+          bsum[nt] += v;
+          bsq[nt] += v * v;
+        }
+      }
+    }
+  }
+  if (a.stat_slab) {
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      if (nt >= ntn) break;
+      float s1 = bsum[nt], s2 = bsq[nt];
+      s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+      const int co = nt * 16 + lr;
+      if (lk == 0 && co < g.Cout) { atomicAdd(&s_stat[co], s1); atomicAdd(&s_stat[g.Cout + co], s2); }
+    }
+    CONV_STAMP(6);
+    __syncthreads();
+    float* row = a.stat_slab + (size_t)(blockIdx.x % a.nslab) * 2 * g.Cout;
+    for (int i = tid; i < 2 * g.Cout; i += CONV_THREADS) atomicAdd(&row[i], s_stat[i]);
+  }
+  CONV_STAMP(7);
+}
+
 constexpr int CB_T = 4;                  // channels per lane
 constexpr int STAGE_FLOATS = 12288;      // 48 KiB of staged rows per workgroup
 constexpr int SLAB_ROWS = 32;            // BN partial-slab rows (atomically folded)
@@ -507,7 +737,7 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_wgrad_kernel(ConvWgradArgs 
               }
               t = act_fwd(t, a.in_act, a.in_alpha);
             }
-            s_x[(trow0 + r) * tw + xcol0 + c] = t;
+            if (c < tw - xcol0) s_x[(trow0 + r) * tw + xcol0 + c] = t;   // VALID: unused tail
           } else {
             if (e >= nd) break;
             int pix, c;
@@ -637,9 +867,64 @@ static bool set_lds_attr(const void* fn) {
   return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;
 }
 
+
+// Launch the MFMA conv forward when the shape is inside its family; false = use the VALU
+// kernel.  Bands: ~CSA_CONV_TARGET (700) workgroups over the batch.
+static bool conv_fwd_mfma(const ConvFwdArgs& f, hipStream_t st) {
+  static const int enabled = [] { const char* e = getenv("CSA_CONV_MFMA"); return e ? atoi(e) : 1; }();
+  static const int target = [] { const char* e = getenv("CSA_CONV_TARGET"); return e ? std::max(1, atoi(e)) : 700; }();
+  if (!enabled) return false;
+  const ConvGeom& g = f.g;
+  const PoolGeom& p = f.pool;
+  const bool pool = p.on != 0;
+  if (pool && !(p.KH == 2 && p.KW == 2 && p.SH == 2 && p.SW == 2 && p.PT == 0 && p.PL == 0)) return false;
+  if (g.Cout > 128) return false;
+  ConvMfmaArgs a{};
+  a.g = g; a.pool_on = pool;
+  a.OHo = pool ? p.OH : g.OH; a.OWo = pool ? p.OW : g.OW;
+  const int K = g.KH * g.KW * g.Cin;
+  a.kpad = (K + 3) & ~3;
+  a.c16 = (g.Cout + 15) & ~15;
+  a.tile_w = ((g.OW - 1) * g.SW + g.KW) * g.Cin;
+  const int per_img = std::max(1, (target + g.B - 1) / g.B);
+  int rows = std::max(1, (a.OHo + per_img - 1) / per_img);
+  auto tile_rows = [&](int r) { return ((pool ? 2 * r : r) - 1) * g.SH + g.KH; };
+  auto lds = [&](int r) {
+    return ((((size_t)tile_rows(r) * a.tile_w + 3) & ~(size_t)3) + (size_t)a.kpad * a.c16 + a.kpad) * sizeof(float);
+  };
+  while (rows > 1 && lds(rows) > 150 * 1024) --rows;
+  if (lds(rows) > 150 * 1024) return false;
+  a.band_rows = rows;
+  a.tile_rows = tile_rows(rows);
+  a.nbands = (a.OHo + rows - 1) / rows;
+  a.x = f.x; a.img = f.img; a.idx = f.idx; a.cursor = f.cursor;
+  a.in_bn = f.in_bn; a.in_bn_on = f.in_bn_on; a.in_act = f.in_act; a.in_alpha = f.in_alpha;
+  a.w = f.w; a.bias = f.bias; a.out_act = f.out_act; a.out_alpha = f.out_alpha;
+  a.y = f.y; a.argmax = f.argmax; a.stat_slab = f.stat_slab; a.nslab = f.nslab;
+  static bool attr = set_lds_attr((const void*)conv_fwd_mfma_kernel<true, true>) &&
+                     set_lds_attr((const void*)conv_fwd_mfma_kernel<true, false>) &&
+                     set_lds_attr((const void*)conv_fwd_mfma_kernel<false, true>) &&
+                     set_lds_attr((const void*)conv_fwd_mfma_kernel<false, false>);
+  (void)attr;
+  dim3 grid((unsigned)(g.B * a.nbands));
+  const size_t shm = lds(rows);
+  if (f.img) {
+    if (pool) hipLaunchKernelGGL((conv_fwd_mfma_kernel<true, true>), grid, dim3(CONV_THREADS), shm, st, a);
+    else hipLaunchKernelGGL((conv_fwd_mfma_kernel<true, false>), grid, dim3(CONV_THREADS), shm, st, a);
+  } else {
+    if (pool) hipLaunchKernelGGL((conv_fwd_mfma_kernel<false, true>), grid, dim3(CONV_THREADS), shm, st, a);
+    else hipLaunchKernelGGL((conv_fwd_mfma_kernel<false, false>), grid, dim3(CONV_THREADS), shm, st, a);
+  }
+  return true;
+}
+
 }  // namespace csa
 
 using namespace csa;
+
+CSA_API int csa_conv_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_conv_dbg), &p, sizeof(p));
+}
 
 // Number of BN partial-slab rows a csa_conv_fwd launch writes (the slab must be zeroed
 // before every launch: rows are accumulated with atomics).
@@ -667,6 +952,7 @@ CSA_API int csa_conv_fwd(const float* x, const uint8_t* img, const int64_t* idx,
   a.in_act = in_act; a.in_alpha = in_alpha;
   a.w = w; a.bias = bias; a.out_act = out_act; a.out_alpha = out_alpha;
   a.y = y; a.argmax = argmax; a.stat_slab = stat_slab; a.nslab = SLAB_ROWS;
+  if (conv_fwd_mfma(a, st)) return (int)hipGetLastError();
   fwd_bands(a.g, a.pool, a.nbands, a.band_rows, a.band_rows_in);
   const size_t nin = ((size_t)a.band_rows_in * a.g.W * a.g.Cin + 3) & ~(size_t)3;
   const size_t shm = (nin + (size_t)a.g.KH * a.g.KW * a.g.Cin * a.g.Cout) * sizeof(float);

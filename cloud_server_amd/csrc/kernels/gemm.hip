@@ -123,6 +123,7 @@ struct EpiStore {              // C[m][n] (+)= v (+ bias[n] once); row m == M ->
   __device__ float prefetch(int, int n, bool first_split) const {
     return (bias && first_split) ? bias[n < N ? n : 0] : 0.f;
   }
+  __device__ void flush(int, float*) {}
   __device__ void operator()(int m, int n, float v, bool first_split, float*, float aux) const {
     if (n >= N) return;
     float* p;
@@ -147,7 +148,11 @@ struct EpiActBNBwd {
     const bool ok = m < M && f < F;
     return x[ok ? (long)m * ld + f : 0];
   }
-  __device__ void operator()(int m, int f, float g, bool, float* lds_acc, float xv) const {
+  // A lane's 16 elements share one column f (the MFMA D layout varies only the row), so
+  // the BN-backward sums are kept in registers and flushed with ONE pair of LDS atomics
+  // per lane (per-element LDS float atomics on 20 channels serialised: ~8k cycles).
+  float sd = 0.f, sdx = 0.f;
+  __device__ void operator()(int m, int f, float g, bool, float*, float xv) {
     if (m >= M || f >= F) return;
     int q, ch;
     C.divmod(f, q, ch);
@@ -156,10 +161,16 @@ struct EpiActBNBwd {
     float d = act_bwd(g, z, y, act, alpha);
     dz[(long)m * ld + f] = d;
     if (has_bn) {
-      float xhat = (xv - t.mean[ch]) * t.rstd[ch];
-      atomicAdd(&lds_acc[ch], d);
-      atomicAdd(&lds_acc[MAXC + ch], d * xhat);
+      sd += d;
+      sdx += d * (xv - t.mean[ch]) * t.rstd[ch];
     }
+  }
+  __device__ void flush(int f, float* lds_acc) {
+    if (!has_bn || f >= F) return;
+    int q, ch;
+    C.divmod(f, q, ch);
+    atomicAdd(&lds_acc[ch], sd);
+    atomicAdd(&lds_acc[MAXC + ch], sdx);
   }
 };
 
@@ -239,8 +250,7 @@ __device__ long long* g_gemm_dbg = nullptr;   // diagnostics: s_memtime stamps o
 // (split, N tile, M tile) fastest-last: re-reads hit that XCD's L2.  Speed only — any
 // placement is correct.  The grid is padded to a multiple of 8 (padding blocks exit).
 struct TileId { int x, y, z; bool valid; };
-__device__ __forceinline__ TileId gemm_tile(int X, int Y, int Z) {
-  const int L = blockIdx.x, G = gridDim.x;                 // G % 8 == 0
+__device__ __forceinline__ TileId gemm_tile(int X, int Y, int Z, int L, int G) {   // G % 8 == 0
   const int t = (L & 7) * (G >> 3) + (L >> 3);
   TileId id;
   id.valid = t < X * Y * Z;
@@ -250,17 +260,23 @@ __device__ __forceinline__ TileId gemm_tile(int X, int Y, int Z) {
   return id;
 }
 
+// LDS arena of one GEMM workgroup: per-wave staging tiles (reused for the WK reduction),
+// BN tables, epilogue accumulators.  One static array per kernel, passed to the body, so
+// a kernel that hosts two GEMM bodies (gemm_pair_kernel) still allocates it once.
+constexpr int GEMM_LDS_FLOATS = 4 * 2 * KC * LDS_PAD + 4 * MAXC + 2 * MAXC;
+
 template <int WM, int WN, int WK, class LA, class LB, class EPI>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
-                                                       int k_per_split, BNRef bn, int bn_on,
-                                                       float* bn_slab_out, int slab_C, int GX,
-                                                       int GY, int GZ) {
+__device__ __forceinline__ void gemm_body(LA la, LB lb, EPI epi, int M, int N, int K,
+                                          int k_per_split, const BNRef& bn, int bn_on,
+                                          float* bn_slab_out, int slab_C, int GX, int GY, int GZ,
+                                          int bid, int nblk, float* lds) {
   static_assert(WM * WN * WK == 4, "4 waves per workgroup");
-  const TileId tid = gemm_tile(GX, GY, GZ);
+  const TileId tid = gemm_tile(GX, GY, GZ, bid, nblk);
   if (!tid.valid) return;                 // whole workgroup: grid padding
-  __shared__ float s_stage[4][2][KC * LDS_PAD];   // per-wave tiles; reused for the WK reduction
-  __shared__ float s_bn[4 * MAXC];
-  __shared__ float s_acc[2 * MAXC];
+  typedef float StageT[2][KC * LDS_PAD];
+  StageT* s_stage = reinterpret_cast<StageT*>(lds);
+  float* s_bn = lds + 4 * 2 * KC * LDS_PAD;
+  float* s_acc = s_bn + 4 * MAXC;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN);
@@ -358,6 +374,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
       int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
       epi(m0 + row, n0 + (lane & 31), acc[i], first, s_acc, aux[i]);
     }
+    epi.flush(n0 + (lane & 31), s_acc);
   }
   GEMM_STAMP(7);
   if (EPI::NEEDS_LDS && bn_slab_out) {
@@ -366,6 +383,37 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EPI epi, in
     for (int i = threadIdx.x; i < 2 * slab_C; i += blockDim.x)
       bn_slab_out[(size_t)slab_row * 2 * slab_C + i] = s_acc[(i < slab_C) ? i : (MAXC + i - slab_C)];
   }
+}
+
+// A GEMM problem bound to its arguments (what one launch — or one half of a pair — runs).
+template <int WM, int WN, int WK, class LA, class LB, class EPI>
+struct GemmProblem {
+  LA la; LB lb; EPI epi; int M, N, K, kps; BNRef bn; int bn_on; float* slab_out; int slab_C;
+  int GX, GY, GZ;
+  __host__ __device__ int nblocks() const { return (GX * GY * GZ + 7) / 8 * 8; }
+  __device__ __forceinline__ void run(int bid, float* lds) const {
+    gemm_body<WM, WN, WK>(la, lb, epi, M, N, K, kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ, bid,
+                          nblocks(), lds);
+  }
+};
+
+template <class P>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(P p) {
+  __shared__ float lds[GEMM_LDS_FLOATS];
+  p.run(blockIdx.x, lds);
+}
+
+// Horizontal fusion: two independent GEMMs (a dense layer's input gradient and weight
+// gradient) in ONE launch — blocks [0, n1) run the first, the rest the second.  HIP-graph
+// branches on a second stream measured slower than serial launches on this runtime
+// (profiles/r1_ab_wgrad_stream.txt); one grid overlaps the two for free and removes a
+// kernel boundary.  n1 is a multiple of 8, so each half keeps its XCD-aware tile order.
+template <class P1, class P2>
+__global__ __launch_bounds__(256) void gemm_pair_kernel(P1 p1, P2 p2) {
+  __shared__ float lds[GEMM_LDS_FLOATS];
+  const int n1 = p1.nblocks();
+  if ((int)blockIdx.x < n1) p1.run(blockIdx.x, lds);
+  else p2.run(blockIdx.x - n1, lds);
 }
 
 // Wave layout + split-K so that one launch has ~1024 waves (one per SIMD on 256 CUs).
@@ -395,22 +443,30 @@ static int grid_slabs(const Plan& p, int M, int N) {
   return ((N + 32 * p.wn - 1) / (32 * p.wn)) * ((M + 32 * p.wm - 1) / (32 * p.wm)) * p.splits;
 }
 
+// Bind a plan's wave layout into a GemmProblem type and hand it to f.
+template <class LA, class LB, class EPI, class F>
+static int with_problem(const Plan& p, LA la, LB lb, EPI epi, int M, int N, int K, const BNRef& bn,
+                        int bn_on, float* slab_out, int slab_C, F f) {
+  const int GX = (N + 32 * p.wn - 1) / (32 * p.wn), GY = (M + 32 * p.wm - 1) / (32 * p.wm);
+  const int GZ = p.splits;
+#define CSA_P(WM, WN, WK) \
+  return f(GemmProblem<WM, WN, WK, LA, LB, EPI>{la, lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ})
+  if (p.wm == 2 && p.wn == 2) CSA_P(2, 2, 1);
+  if (p.wm == 1 && p.wn == 2) CSA_P(1, 2, 2);
+  CSA_P(1, 1, 4);
+#undef CSA_P
+}
+
 template <class LA, class LB, class EPI>
 static int launch_gemm(const Plan& p, LA la, LB lb, EPI epi, int M, int N, int K, const BNRef& bn,
                        int bn_on, float* slab_out, int slab_C, hipStream_t st) {
-  const int GX = (N + 32 * p.wn - 1) / (32 * p.wn), GY = (M + 32 * p.wm - 1) / (32 * p.wm);
-  const int GZ = p.splits;
-  dim3 grid((unsigned)((GX * GY * GZ + 7) / 8 * 8));
-#define CSA_L(WM, WN, WK)                                                                   \
-  hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, WK, LA, LB, EPI>), grid, dim3(256), 0, st, la, \
-                     lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ)
-  if (p.wm == 2 && p.wn == 2) CSA_L(2, 2, 1);
-  else if (p.wm == 2 && p.wn == 1) CSA_L(2, 1, 2);
-  else if (p.wm == 1 && p.wn == 2) CSA_L(1, 2, 2);
-  else CSA_L(1, 1, 4);
-#undef CSA_L
-  return (int)hipGetLastError();
+  return with_problem(p, la, lb, epi, M, N, K, bn, bn_on, slab_out, slab_C, [&](auto prob) {
+    hipLaunchKernelGGL((gemm_f32_kernel<decltype(prob)>), dim3((unsigned)prob.nblocks()), dim3(256), 0,
+                       st, prob);
+    return (int)hipGetLastError();
+  });
 }
+
 
 // Call f(std::integral_constant<bool, a>, std::integral_constant<bool, b>) — picks the
 // float4 loader instantiations when the operands' strides allow it.
@@ -536,3 +592,53 @@ CSA_API int csa_dense_wgrad(const float* X, const float* dY, float* dW, float* d
   });
 }
 
+
+// Dense layer backward in ONE launch (gemm_pair_kernel): the input gradient dX (with the
+// forward input transform's backward in its epilogue, as csa_dense_dgrad) and the weight
+// gradient dW/db of an untransformed / materialised input Xw (as csa_dense_wgrad).
+// Returns the dgrad BN-slab row count (>= 1), 0 when the shape is outside the fused family
+// (the caller then launches the two GEMMs separately), or a negative error.
+CSA_API int csa_dense_bwd(const float* dY, const float* W, float* dX, int M, int Kin, int Nout,
+                          const float* x_fwd, int act, float alpha, const float* bn_slab,
+                          int bn_nslab, int bn_C, float bn_count, float bn_eps,
+                          const float* bn_scale, const float* bn_offset, float* bwd_slab,
+                          const float* Xw, float* dW, float* db, float scale, hipStream_t st) {
+  if (Nout % 4 || Kin % 4 || Nout < 4 || Kin < 4) return 0;
+  if (bn_slab && bn_C > MAXC) return -1;
+  const bool transform = (act != ACT_NONE) || (bn_slab != nullptr);
+  const Plan pd = plan_gemm(M, Kin, Nout, !transform);
+  if (!(pd.wm == 1 && pd.wn == 1 && pd.wk == 4)) return 0;
+  const int Mg = Kin + (db ? 1 : 0);
+  const Plan pw = plan_gemm(Mg, Nout, M, true);
+  const BNRef bn = make_bn(bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset);
+  const LoadRowMajor<true> la{dY, (long)Nout, M, Nout};     // A(m, k=n) = dY[m][n]
+  const LoadRowMajor<true> lb{W, (long)Nout, Kin, Nout};    // B(k=n, j) = W[j][n]
+  const LoadColMajor<true> lbw{dY, (long)Nout, Nout, M};    // B(k=m, n) = dY[m][n]
+  const EpiStore ew{dW, (long)Nout, Kin, Nout, nullptr, pw.splits > 1, db, scale};
+  const int GX = (Kin + 31) / 32, GY = (M + 31) / 32;
+  auto go = [&](auto ed, int bn_on, float* so, int sc) {
+    using ED = decltype(ed);
+    const GemmProblem<1, 1, 4, LoadRowMajor<true>, LoadRowMajor<true>, ED> a{
+        la, lb, ed, M, Kin, Nout, pd.kps, bn, bn_on, so, sc, GX, GY, pd.splits};
+    auto launch = [&](auto law) {
+      return with_problem(pw, law, lbw, ew, Mg, Nout, M, BNRef{}, 0, nullptr, 0, [&](auto b) {
+        hipLaunchKernelGGL((gemm_pair_kernel<decltype(a), decltype(b)>),
+                           dim3((unsigned)(a.nblocks() + b.nblocks())), dim3(256), 0, st, a, b);
+        return (int)hipGetLastError();
+      });
+    };
+    if (db) return launch(LoadColMajor<true, true>{Xw, (long)Kin, Kin, M});   // A(f, m) = Xw[m][f]
+    return launch(LoadColMajor<true>{Xw, (long)Kin, Kin, M});
+  };
+  int rc;
+  if (transform) {
+    EpiActBNBwd ed{dX, (long)Kin, M, Kin, FastDiv(bn_C > 0 ? bn_C : 1), x_fwd, act, alpha,
+                   bn_slab != nullptr, BNTables{}};
+    rc = go(ed, bn_slab != nullptr, bn_slab ? bwd_slab : nullptr, bn_C);
+  } else {
+    EpiStore ed{dX, (long)Kin, M, Kin, nullptr, pd.splits > 1, nullptr, 1.f};
+    rc = go(ed, 0, nullptr, 0);
+  }
+  if (rc) return -rc;
+  return grid_slabs(pd, M, Kin);
+}

@@ -34,6 +34,7 @@ _SIGS = {
     "csa_dense_dgrad_splits": (I, [I, I, I, I]),
     "csa_dense_dgrad_slabs": (I, [I, I, I]),
     "csa_dense_wgrad_splits": (I, [I, I, I]),
+    "csa_dense_bwd": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, P, P, F, P]),
     "csa_dense_wgrad": (I, [P, P, P, P, I, I, I, P, I, I, F, F, P, P, I, F, F, P]),
     "csa_conv_wgrad": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I,
                            P, I, F, F, P, P, I, F, P, P]),
@@ -46,6 +47,7 @@ _SIGS = {
     "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
+    "csa_conv_debug": (I, [P]),
     "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),
 }
 

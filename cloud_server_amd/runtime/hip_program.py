@@ -515,6 +515,10 @@ class HipProgram:
             prev = self.units[k - 1] if k > 0 else None
             if u.kind == "dense":
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if (prev is not None and u not in self.lr_units and not self.wsplit
+                        and self._dense_bwd_fused(u, prev, st)):
+                    self._grad_ready(k)          # dgrad + wgrad in one launch
+                    continue
                 if prev is not None:
                     xf = u.x.view(B, -1)
                     self._rc(lib.csa_dense_dgrad(
@@ -595,6 +599,27 @@ class HipProgram:
         else:
             e.after_backward_sync()
         self._optimizer(st)
+
+    def _dense_bwd_fused(self, u: Unit, prev: Unit, st) -> bool:
+        """Input gradient + weight gradient of a dense unit as ONE launch
+        (``csa_dense_bwd``) when its weight-gradient operand needs no transform (a
+        materialised BN/act input, or an identity transform).  False: not applicable."""
+        if os.environ.get("CSA_DENSE_PAIR", "1") != "1":
+            return False
+        tf, lp, B = u.in_tf, u.layer, self.B
+        if u.xt is None and (tf.has_bn or tf.act is not None):
+            return False
+        V, G = self.views, self.gviews
+        fin, fout = lp.in_shape.numel, lp.spec.hidden
+        xw = u.xt if u.xt is not None else u.x.view(B, -1)
+        rc = self.lib.csa_dense_bwd(
+            K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
+            K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
+            K.ptr(tf.bwd_slab), K.ptr(xw), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+            1.0, st)
+        if rc < 0:
+            raise RuntimeError(f"dense_bwd failed: {rc}")
+        return rc > 0
 
     def _optimizer(self, st) -> None:
         e, lib = self.e, self.lib

@@ -71,6 +71,18 @@ def main() -> int:
                       f" (iters {[t[j + 1] - t[j] for j in range(2, last)]})  prefetch {t[8] - t[6]}"
                       f"  wk-reduce {t[9] - t[8]}  epilogue {t[7] - t[9]}  it0: commitA {t[10] - t[2]} commitB {t[11] - t[10]} mfma {t[12] - t[11]}")
                 dbg.zero_()
+    if os.environ.get("MB_CONV"):
+        dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name == "csa_conv_fwd":
+                for _ in range(3):
+                    dbg.zero_()
+                    eng.program.lib.csa_conv_debug(dbg.data_ptr())
+                    fn(*args)
+                    torch.cuda.synchronize()
+                    eng.program.lib.csa_conv_debug(None)
+                t = dbg.tolist()
+                print(f"{i:2d} {name:18s} conv stamps:", [t[j + 1] - t[j] for j in range(7)])
     for i, (name, fn, args) in enumerate(rec.calls):
         for _ in range(5):
             fn(*args)
