@@ -278,13 +278,11 @@ struct ConvDgradArgs {
 };
 
 template <int CB>
-__global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs a) {
-  // dynamic LDS: dc rows of the band [rows][OW][Cout] then weights [(i,j,ci)][Cout]
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float s_bn[4 * 128 + 2 * 128];
-  __shared__ float s_stat[2 * 128];
+__device__ __forceinline__ void conv_dgrad_body(const ConvDgradArgs& a, int bid, float* smem,
+                                                float* s_bn, float* s_stat) {
+  // smem (dynamic): dc rows of the band [rows][OW][Cout] then weights [(i,j,ci)][Cout]
   const ConvGeom& g = a.g;
-  const int b = blockIdx.x / a.nbands, band = blockIdx.x % a.nbands;
+  const int b = bid / a.nbands, band = bid % a.nbands;
   const int G = (g.Cin + CB - 1) / CB;
   const int y0 = band * a.band_rows, y1 = min(g.H, y0 + a.band_rows);
   // dc rows that touch input rows [y0, y1): oy*SH - PT + i in [y0, y1)
@@ -375,9 +373,17 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs 
     for (int c = 0; c < CB; ++c)
       if (c < nci) { atomicAdd(&s_stat[ci0 + c], dsum[c]); atomicAdd(&s_stat[g.Cin + ci0 + c], dxs[c]); }
     __syncthreads();
-    float* row = a.bwd_slab + (size_t)(blockIdx.x % a.nslab) * 2 * g.Cin;
+    float* row = a.bwd_slab + (size_t)(bid % a.nslab) * 2 * g.Cin;
     for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) atomicAdd(&row[i], s_stat[i]);
   }
+}
+
+template <int CB>
+__global__ __launch_bounds__(CONV_THREADS) void conv_dgrad_kernel(ConvDgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  __shared__ float s_stat[2 * 128];
+  conv_dgrad_body<CB>(a, blockIdx.x, smem, s_bn, s_stat);
 }
 
 
@@ -645,11 +651,10 @@ struct ConvWgradArgs {
 };
 
 template <bool U8>
-__global__ __launch_bounds__(CONV_THREADS) void conv_wgrad_kernel(ConvWgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float s_bn[4 * 128 + 2 * 128];
+__device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid, float* smem,
+                                                float* s_bn) {
   const ConvGeom& g = a.g;
-  const int b = blockIdx.x / a.nbands, band = blockIdx.x % a.nbands;
+  const int b = bid / a.nbands, band = bid % a.nbands;
   const int r0 = band * a.band_rows, r1 = min(g.OH, r0 + a.band_rows);
   const int nrows = r1 - r0;
   const int ty0 = r0 * g.SH - g.PT;                 // image row of tile row 0
@@ -829,12 +834,31 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_wgrad_kernel(ConvWgradArgs 
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) v += s_part[(w * 8 + t) * 256 + (e & 255)];
-      const int sidx = blockIdx.x % a.stripes;
+      const int sidx = bid % a.stripes;
       if (tap >= ncombo) atomicAdd(&a.db[sidx * g.Cout + co], v);
       else atomicAdd(&a.dw[(long)sidx * ncombo * g.Cout + tap * g.Cout + co], v);
     }
     __syncthreads();                                // s_part reused by the next block
   }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(CONV_THREADS) void conv_wgrad_kernel(ConvWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  conv_wgrad_body<U8>(a, blockIdx.x, smem, s_bn);
+}
+
+// A conv unit's input gradient and weight gradient (independent: both read dc) in ONE
+// launch — blocks [0, nd) run the dgrad body, the rest the wgrad body (see
+// gemm_pair_kernel in gemm.hip for why this beats a forked graph branch).
+__global__ __launch_bounds__(CONV_THREADS) void conv_bwd_pair_kernel(ConvDgradArgs d, ConvWgradArgs w,
+                                                                     int nd) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  __shared__ float s_stat[2 * 128];
+  if ((int)blockIdx.x < nd) conv_dgrad_body<CB_T>(d, blockIdx.x, smem, s_bn, s_stat);
+  else conv_wgrad_body<false>(w, blockIdx.x - nd, smem, s_bn);
 }
 
 static void fwd_bands(const ConvGeom& g, const PoolGeom& p, int& nbands, int& rows, int& rows_in) {
@@ -995,11 +1019,11 @@ CSA_API int csa_conv_dgrad_nslab(const int* geom) {
   return SLAB_ROWS;
 }
 
-CSA_API int csa_conv_dgrad(const float* dc, const float* w, float* dx, const int* geom,
-                           const float* x_fwd, int in_act, float in_alpha, const float* bn_slab,
-                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                           const float* bn_offset, float* bwd_slab, hipStream_t st) {
-  ConvDgradArgs a{};
+static int dgrad_args(const float* dc, const float* w, float* dx, const int* geom, const float* x_fwd,
+                      int in_act, float in_alpha, const float* bn_slab, int bn_nslab, float bn_count,
+                      float bn_eps, const float* bn_scale, const float* bn_offset, float* bwd_slab,
+                      ConvDgradArgs& a, size_t& shm) {
+  a = ConvDgradArgs{};
   a.g = geom_from(geom);
   if (a.g.Cin > 128 || a.g.Cout > 128) return -1;
   a.dc = dc; a.w = w; a.dx = dx; a.x_fwd = x_fwd; a.in_act = in_act; a.in_alpha = in_alpha;
@@ -1008,8 +1032,19 @@ CSA_API int csa_conv_dgrad(const float* dc, const float* w, float* dx, const int
   a.bwd_slab = bwd_slab; a.nslab = SLAB_ROWS;
   dgrad_bands(a.g, a.nbands, a.band_rows, a.band_rows_in);
   const size_t nd = ((size_t)a.band_rows_in * a.g.OW * a.g.Cout + 3) & ~(size_t)3;
-  const size_t shm = (nd + (size_t)a.g.KH * a.g.KW * a.g.Cin * a.g.Cout) * sizeof(float);
-  if (shm > 150 * 1024) return -2;
+  shm = (nd + (size_t)a.g.KH * a.g.KW * a.g.Cin * a.g.Cout) * sizeof(float);
+  return shm > 150 * 1024 ? -2 : 0;
+}
+
+CSA_API int csa_conv_dgrad(const float* dc, const float* w, float* dx, const int* geom,
+                           const float* x_fwd, int in_act, float in_alpha, const float* bn_slab,
+                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                           const float* bn_offset, float* bwd_slab, hipStream_t st) {
+  ConvDgradArgs a;
+  size_t shm;
+  const int rc = dgrad_args(dc, w, dx, geom, x_fwd, in_act, in_alpha, bn_slab, bn_nslab, bn_count, bn_eps,
+                            bn_scale, bn_offset, bwd_slab, a, shm);
+  if (rc) return rc;
   static bool attr = set_lds_attr((const void*)conv_dgrad_kernel<CB_T>);
   (void)attr;
   dim3 grid((unsigned)(a.g.B * a.nbands));
@@ -1017,17 +1052,13 @@ CSA_API int csa_conv_dgrad(const float* dc, const float* w, float* dx, const int
   return (int)hipGetLastError();
 }
 
-// dW/db (+)= conv weight gradient, accumulated with atomics into `stripes` copies
-// (dW: [stripes][KH*KW*Cin*Cout], db: [stripes][Cout]); the caller zeroes them.
-// Input = x (fp32 NHWC, forward input transform BN/act applied on the fly) or the
-// uint8 dataset rows img[idx[b] (+ cursor * B)] / 255 for the first layer.
-CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* idx, const float* dOut,
-                           float* dW, float* db, int stripes, int B, int H, int W, int Cin, int KH, int KW, int SH,
-                           int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
-                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                           const float* bn_offset, int in_act, float in_alpha, const int64_t* cursor,
-                           hipStream_t st) {
-  ConvWgradArgs a{};
+static int wgrad_args(const float* x, const uint8_t* img, const int64_t* idx, const float* dOut,
+                      float* dW, float* db, int stripes, int B, int H, int W, int Cin, int KH, int KW,
+                      int SH, int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
+                      int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                      const float* bn_offset, int in_act, float in_alpha, const int64_t* cursor,
+                      ConvWgradArgs& a, size_t& shm) {
+  a = ConvWgradArgs{};
   a.g = ConvGeom{B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout};
   a.ntaps = KH * KW * Cin + (db ? 1 : 0);
   a.mtiles = (a.ntaps + 15) / 16;
@@ -1060,11 +1091,56 @@ CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* id
   a.band_rows = rows;
   a.tile_rows = tile_rows(rows);
   a.nbands = (OH + rows - 1) / rows;
+  shm = lds(rows);
+  return 0;
+}
+
+// dW/db (+)= conv weight gradient, accumulated with atomics into `stripes` copies
+// (dW: [stripes][KH*KW*Cin*Cout], db: [stripes][Cout]); the caller zeroes them.
+// Input = x (fp32 NHWC, forward input transform BN/act applied on the fly) or the
+// uint8 dataset rows img[idx[b] (+ cursor * B)] / 255 for the first layer.
+CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* idx, const float* dOut,
+                           float* dW, float* db, int stripes, int B, int H, int W, int Cin, int KH, int KW, int SH,
+                           int SW, int PT, int PL, int OH, int OW, int Cout, const float* bn_slab,
+                           int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                           const float* bn_offset, int in_act, float in_alpha, const int64_t* cursor,
+                           hipStream_t st) {
+  ConvWgradArgs a;
+  size_t shm;
+  const int rc = wgrad_args(x, img, idx, dOut, dW, db, stripes, B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH,
+                            OW, Cout, bn_slab, bn_nslab, bn_count, bn_eps, bn_scale, bn_offset, in_act,
+                            in_alpha, cursor, a, shm);
+  if (rc) return rc;
   static bool attr = set_lds_attr((const void*)conv_wgrad_kernel<true>) &&
                      set_lds_attr((const void*)conv_wgrad_kernel<false>);
   (void)attr;
   dim3 grid((unsigned)(B * a.nbands));
-  if (img) hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(CONV_THREADS), lds(rows), st, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(CONV_THREADS), lds(rows), st, a);
+  if (img) hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(CONV_THREADS), shm, st, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(CONV_THREADS), shm, st, a);
+  return (int)hipGetLastError();
+}
+
+// Conv unit backward in ONE launch: input gradient (as csa_conv_dgrad) + weight gradient
+// of a non-first layer (as csa_conv_wgrad with x, never the uint8 images).
+CSA_API int csa_conv_bwd(const float* dc, const float* w, float* dx, const int* geom, const float* x_fwd,
+                         int in_act, float in_alpha, const float* bn_slab, int bn_nslab, float bn_count,
+                         float bn_eps, const float* bn_scale, const float* bn_offset, float* bwd_slab,
+                         float* dW, float* db, int stripes, hipStream_t st) {
+  ConvDgradArgs d;
+  ConvWgradArgs wg;
+  size_t shm_d, shm_w;
+  int rc = dgrad_args(dc, w, dx, geom, x_fwd, in_act, in_alpha, bn_slab, bn_nslab, bn_count, bn_eps,
+                      bn_scale, bn_offset, bwd_slab, d, shm_d);
+  if (rc) return rc;
+  const ConvGeom& g = d.g;
+  rc = wgrad_args(x_fwd, nullptr, nullptr, dc, dW, db, stripes, g.B, g.H, g.W, g.Cin, g.KH, g.KW, g.SH, g.SW,
+                  g.PT, g.PL, g.OH, g.OW, g.Cout, bn_slab, bn_nslab, bn_count, bn_eps, bn_scale, bn_offset,
+                  in_act, in_alpha, nullptr, wg, shm_w);
+  if (rc) return rc;
+  static bool attr = set_lds_attr((const void*)conv_bwd_pair_kernel);
+  (void)attr;
+  const int nd = g.B * d.nbands;
+  dim3 grid((unsigned)(nd + g.B * wg.nbands));
+  hipLaunchKernelGGL(conv_bwd_pair_kernel, grid, dim3(CONV_THREADS), std::max(shm_d, shm_w), st, d, wg, nd);
   return (int)hipGetLastError();
 }

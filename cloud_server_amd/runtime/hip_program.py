@@ -573,6 +573,14 @@ class HipProgram:
                 sp = lp.spec
                 h, w = lp.in_shape.hw
                 oh, ow = lp.out_shape.hw
+                if prev is not None and not self.wsplit and os.environ.get("CSA_CONV_PAIR", "1") == "1":
+                    # input gradient + weight gradient in one launch
+                    self._rc(lib.csa_conv_bwd(
+                        K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
+                        K.ptr(u.x), in_act, in_alpha, *bn, K.ptr(tf.bwd_slab),
+                        K.ptr(u.dw_acc), K.ptr(u.db_acc) if sp.bias else None, u.wg_stripes, st), "conv_bwd")
+                    self._grad_ready(k)
+                    continue
                 ws = self._fork_wgrad(st)
                 self._rc(lib.csa_conv_wgrad(
                     None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
