@@ -211,6 +211,14 @@ struct RouteArgs {
 __global__ __launch_bounds__(256) void route_bwd_kernel(RouteArgs a) {
   __shared__ float s_bn[4 * 128];
   __shared__ float s_s[2 * 128];
+  // this lane's element loads go out first: their round trip overlaps the BN-slab
+  // reductions below (clamped index, so the loads are unconditional)
+  const long n = (long)a.B * a.h * a.w * a.C;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long ec = e < n ? e : 0;
+  float g = a.dz[ec];
+  const float yv = a.y[ec];
+  const int am = a.pool_on ? (int)a.argmax[ec] : 0;
   if (a.bn_on) {
     bn_reduce_to_lds(a.bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_s);
     __syncthreads();
@@ -228,12 +236,8 @@ __global__ __launch_bounds__(256) void route_bwd_kernel(RouteArgs a) {
       }
   }
   __syncthreads();
-  const long n = (long)a.B * a.h * a.w * a.C;
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int c = (int)(e % a.C);
-  float g = a.dz[e];
-  const float yv = a.y[e];
   if (a.bn_on) {
     const float inv_n = 1.0f / a.bn.count;
     const float xhat = (yv - s_bn[c]) * s_bn[128 + c];
@@ -244,7 +248,6 @@ __global__ __launch_bounds__(256) void route_bwd_kernel(RouteArgs a) {
   if (!a.pool_on) { a.dc[e] = g; return; }
   const long pix = e / a.C;
   const int px = (int)(pix % a.w), py = (int)((pix / a.w) % a.h), b = (int)(pix / ((long)a.w * a.h));
-  const int am = a.argmax[e];
   // non-overlapping windows (kernel == stride): this lane owns its whole window and
   // writes it with plain stores (zeros included); otherwise atomics into a zeroed dc.
   const int ky = am / a.PKW, kx = am % a.PKW;
@@ -686,52 +689,48 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid,
     const long ioff = U8 ? idx[b] * (long)(g.H * irow) + (long)iy0 * irow : xoff;
     const bool v4 = ((ioff | nx | doff | nd) & 3) == 0;
     const int sx = v4 ? 4 : 1;
-    const int nxv = (nx + sx - 1) / sx, ndv = (nd + sx - 1) / sx, ntot = nxv + ndv;
+    const int nxv = (nx + sx - 1) / sx, ndv = (nd + sx - 1) / sx, nmax = max(nxv, ndv);
     const uint8_t* isrc = U8 ? a.img + ioff : nullptr;
     const float* xsrc = U8 ? nullptr : a.x + xoff;
     const float* dsrc = a.dc + doff;
     const FastDiv dirow(irow), dcout(g.Cout), dcin(g.Cin);
     const int xcol0 = g.PL * g.Cin, trow0 = iy0 - ty0;
-    constexpr int U = 8;
-    for (int base = 0; base < ntot; base += CONV_THREADS * U) {
-      float4 v[U];
+    constexpr int U = 4;
+    // Input and dc loads go to two separate register arrays with clamped indices: a
+    // per-element "input or dc" select between two loads made hipcc branch around every
+    // load and wait for it before issuing the next (8 serial round trips per thread).
+    for (int base = 0; base < nmax; base += CONV_THREADS * U) {
+      float4 vx[U], vd[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = base + u * CONV_THREADS + threadIdx.x;
-        const bool isx = i < nxv;
-        const int j = isx ? i : min(i - nxv, ndv - 1);
+        const int jx = min(i, max(nxv - 1, 0)), jd = min(i, max(ndv - 1, 0));
         if (v4) {
-          if (isx) {
-            if (U8) {
-              const uchar4 q = reinterpret_cast<const uchar4*>(isrc)[j];
-              v[u] = make_float4(q.x, q.y, q.z, q.w);
-            } else {
-              v[u] = reinterpret_cast<const float4*>(xsrc)[j];
-            }
+          if (U8) {
+            const uchar4 q = reinterpret_cast<const uchar4*>(isrc)[jx];
+            vx[u] = make_float4(q.x, q.y, q.z, q.w);
           } else {
-            v[u] = reinterpret_cast<const float4*>(dsrc)[max(j, 0)];
+            vx[u] = reinterpret_cast<const float4*>(xsrc)[jx];
           }
+          vd[u] = reinterpret_cast<const float4*>(dsrc)[jd];
         } else {
-          const float t = isx ? (U8 ? (float)isrc[j] : xsrc[j]) : dsrc[max(j, 0)];
-          v[u] = make_float4(t, 0.f, 0.f, 0.f);
+          vx[u] = make_float4(U8 ? (float)isrc[jx] : xsrc[jx], 0.f, 0.f, 0.f);
+          vd[u] = make_float4(dsrc[jd], 0.f, 0.f, 0.f);
         }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = base + u * CONV_THREADS + threadIdx.x;
-        if (i >= ntot) continue;
-        const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-        const bool isx = i < nxv;
-        const int e0 = (isx ? i : i - nxv) * sx;
+        const float xs[4] = {vx[u].x, vx[u].y, vx[u].z, vx[u].w};
+        const float ds[4] = {vd[u].x, vd[u].y, vd[u].z, vd[u].w};
+        if (i < nxv) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q >= sx) break;
-          const int e = e0 + q;
-          if (isx) {
-            if (e >= nx) break;
+          for (int q = 0; q < 4; ++q) {
+            const int e = i * sx + q;
+            if (q >= sx || e >= nx) break;
             int r, c;
             dirow.divmod(e, r, c);
-            float t = vv[q];
+            float t = xs[q];
             if (U8) {
               t *= (1.0f / 255.0f);
             } else {
@@ -743,11 +742,16 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid,
               t = act_fwd(t, a.in_act, a.in_alpha);
             }
             if (c < tw - xcol0) s_x[(trow0 + r) * tw + xcol0 + c] = t;   // VALID: unused tail
-          } else {
-            if (e >= nd) break;
+          }
+        }
+        if (i < ndv) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = i * sx + q;
+            if (q >= sx || e >= nd) break;
             int pix, c;
             dcout.divmod(e, pix, c);
-            s_dc[pix * a.c16 + c] = vv[q];
+            s_dc[pix * a.c16 + c] = ds[q];
           }
         }
       }
@@ -825,6 +829,23 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid,
       }
     }
     __syncthreads();
+    if (ntiles <= 8) {
+      // every output in this block: walk them in memory order so each atomic
+      // wave-instruction covers 256 contiguous bytes of dW (row = tap, Cout wide)
+      const int nout = a.ntaps * g.Cout;
+      const int sidx = bid % a.stripes;
+      for (int o = threadIdx.x; o < nout; o += CONV_THREADS) {
+        const int tap = o / g.Cout, co = o - tap * g.Cout;
+        const int t = (tap >> 4) * a.ntiles + (co >> 4);
+        const int el = (tap & 15) * 16 + (co & 15);
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += s_part[(w * 8 + t) * 256 + el];
+        if (tap >= ncombo) atomicAdd(&a.db[sidx * g.Cout + co], v);
+        else atomicAdd(&a.dw[(long)sidx * ncombo * g.Cout + o], v);
+      }
+      break;                                        // single block: done
+    }
     for (int e = threadIdx.x; e < nt_blk * 256; e += CONV_THREADS) {
       const int t = e >> 8, rr = (e >> 4) & 15, cc = e & 15;
       const int tt = t0 + t;

@@ -113,12 +113,12 @@ class DigitNet(nn.Module):
     """Eager model over a ``FlatState``.  ``forward(x)`` takes NHWC [B,28,28,1] or [B,784]."""
 
     def __init__(self, plan: NetPlan, device="cpu", seed: int = 0, bn_mode: str = "running",
-                 bn_momentum: float = 0.1, pad_multiple: int = 1):
+                 bn_momentum: float = 0.1, pad_multiple: int = 1, dense_last: bool = False):
         super().__init__()
         self.plan = plan
         self.bn_mode = bn_mode
         self.bn_momentum = bn_momentum
-        self.state = FlatState(plan.param_shapes(), device=device, pad_multiple=pad_multiple)
+        self.state = FlatState(plan.param_shapes(dense_last), device=device, pad_multiple=pad_multiple)
         init_params(plan, self.state, seed)
         self.flat = nn.Parameter(self.state.buffer)
         self.state.buffer = self.flat.data
@@ -214,6 +214,7 @@ def loss_fn(name: str, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tens
     return F.cross_entropy(logits, labels.long())
 
 
-def build_model(cfg: TrainConfig, device="cpu", pad_multiple: int = 1) -> DigitNet:
+def build_model(cfg: TrainConfig, device="cpu", pad_multiple: int = 1,
+                dense_last: bool = False) -> DigitNet:
     return DigitNet(cfg.plan(), device=device, seed=cfg.seed, bn_mode=cfg.bn_mode,
-                    pad_multiple=pad_multiple)
+                    pad_multiple=pad_multiple, dense_last=dense_last)

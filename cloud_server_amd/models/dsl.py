@@ -209,13 +209,18 @@ class NetPlan:
     head_in: int
     num_classes: int = NUM_CLASSES
 
-    def param_shapes(self) -> Dict[str, Tuple[int, ...]]:
+    def param_shapes(self, dense_last: bool = False) -> Dict[str, Tuple[int, ...]]:
+        """Named parameter shapes in flat-buffer order: DSL order, head last — or, with
+        ``dense_last``, every non-dense parameter and the head first and the dense layers
+        after them (the "lowrank" DP strategy all-reduces exactly that leading range)."""
         out: Dict[str, Tuple[int, ...]] = {}
+        dense: Dict[str, Tuple[int, ...]] = {}
         for lp in self.layers:
             for k, s in lp.params.items():
-                out[f"{lp.name}.{k}"] = s
+                (dense if dense_last and isinstance(lp.spec, DenseSpec) else out)[f"{lp.name}.{k}"] = s
         out["head.weight"] = (self.head_in, self.num_classes)
         out["head.bias"] = (self.num_classes,)
+        out.update(dense)
         return out
 
     def num_params(self) -> int:

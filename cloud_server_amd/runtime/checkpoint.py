@@ -15,6 +15,7 @@ step counters, the batch-stream position and the model config JSON.  Writes are 
 from __future__ import annotations
 
 import json
+import math
 import os
 import re
 from typing import Any, Dict, Optional, Tuple
@@ -91,6 +92,10 @@ def engine_state(eng) -> Dict[str, Any]:
     return {
         "model": st,
         "slots": full_slots(eng).detach().cpu(),
+        # flat-buffer layout of the slots (it depends on the DP strategy: "lowrank" puts
+        # the dense layers last), so a resume under another strategy can re-map them
+        "layout": [[n, int(o), int(math.prod(eng.model.state.shapes[n]))]
+                   for n, o in eng.model.state.offsets.items()],
         "opt_id": int(eng.opt_id),
         "dstep": int(eng.dstep.item()),
         "host_step": int(eng.host_step),
@@ -102,6 +107,14 @@ def engine_state(eng) -> Dict[str, Any]:
 def restore_engine(eng, obj: Dict[str, Any]) -> None:
     eng.model.import_state(obj["model"])
     slots = obj["slots"]
+    layout = obj.get("layout")
+    cur = eng.model.state.offsets
+    if layout and slots.dim() == 2 and any(cur.get(n) != o for n, o, _ in layout):
+        remap = torch.zeros(slots.shape[0], eng.flat.numel(), dtype=slots.dtype)
+        for n, o, k in layout:
+            if n in cur:
+                remap[:, cur[n]:cur[n] + k] = slots[:, o:o + k]
+        slots = remap
     if int(obj.get("opt_id", eng.opt_id)) == eng.opt_id and slots.shape[0] == eng.slots.shape[0]:
         lo, hi = eng.sync.shard_range()
         if slots.shape[1:] == eng.slots.shape[1:]:

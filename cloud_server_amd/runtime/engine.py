@@ -68,7 +68,8 @@ class TrainEngine:
         self.cfg = cfg
         self.ctx = ctx or DistContext(device=torch.device(device))
         self.device = torch.device(device)
-        self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world)
+        self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world,
+                                           dense_last=strategy == "lowrank")
         self.model.train()
         self.flat = self.model.flat.data
         self.flat_grad = torch.zeros_like(self.flat)

@@ -186,14 +186,19 @@ class HipProgram:
                 n = f"{u.layer.name}.{p}"
                 taken.append((offs[n], offs[n] + self.gviews[n].numel()))
             self.lr_units.append(u)
-        # everything else is all-reduced: the complement of the lowrank weight ranges
-        lo, end = 0, e.flat.numel()
-        for a, b in sorted(taken):
-            if a > lo:
-                self.lr_ranges.append((lo, a))
-            lo = max(lo, b)
-        if lo < end:
-            self.lr_ranges.append((lo, end))
+        # everything else is all-reduced: the other parameters' spans, merged across
+        # alignment padding (with the dense-last flat layout that is ONE leading range)
+        lr_spans = set(taken)
+        spans = sorted((o, o + self.gviews[n].numel()) for n, o in offs.items())
+        open_range = False
+        for a, b in spans:
+            if (a, b) in lr_spans:
+                open_range = False
+            elif open_range:
+                self.lr_ranges[-1] = (self.lr_ranges[-1][0], b)
+            else:
+                self.lr_ranges.append((a, b))
+                open_range = True
         if self.lr_units:
             self.lr_side = torch.cuda.Stream(dev)
             self.lr_first = min(self.units.index(u) for u in self.lr_units)
