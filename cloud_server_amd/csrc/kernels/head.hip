@@ -140,7 +140,10 @@ __global__ __launch_bounds__(RT) void head_rows_kernel(HeadArgs a, int* ws) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int i = base + u * RT + tid;
-        v[u] = i < nw4 ? w4[i] : h4[(i - nw4 < nh4) ? i - nw4 : 0];
+        // select the ADDRESS, then one unconditional load (a select between two loads
+        // made hipcc branch around each and wait for it: 8 serial round trips)
+        const float4* p = i < nw4 ? w4 + i : h4 + ((i - nw4 < nh4) ? i - nw4 : 0);
+        v[u] = *p;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
