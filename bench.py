@@ -32,7 +32,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch", type=int, default=50)
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--strategy", default="allreduce", choices=["allreduce", "ps", "lowrank"])
+    # auto: "lowrank" data parallelism when world > 1 (dense weight gradients from
+    # all-gathered GEMM operands instead of an 8 MB all-reduce; parallel/dp.py), else plain
+    ap.add_argument("--strategy", default="auto", choices=["auto", "allreduce", "ps", "lowrank"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--optimizer", default="AdagradOptimizer")
     args = ap.parse_args()
@@ -45,6 +47,8 @@ def main() -> int:
     from cloud_server_amd.runtime.engine import TrainEngine
 
     ctx = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
+    if args.strategy == "auto":
+        args.strategy = "lowrank" if ctx.world > 1 else "allreduce"
     cfg_json = dict(SAMPLE_CONFIG)
     cfg_json["optimizer_name"] = args.optimizer
     cfg_json["learning_rate"] = 1e-4 if args.optimizer == "AdagradOptimizer" else 0.01
