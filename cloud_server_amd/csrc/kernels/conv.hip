@@ -264,6 +264,77 @@ __global__ __launch_bounds__(256) void route_bwd_kernel(RouteArgs a) {
   }
 }
 
+// Route backward fused into its consumer (the conv unit's input-gradient / weight-gradient
+// pair): the pair's workgroups build the BN tables of the route once each (two tiny slab
+// reductions) and then compute the route value of exactly the conv-output rows they
+// stage, instead of reading a dc tensor a separate route launch wrote.  Non-overlapping
+// pools (kernel == stride, no padding) or no pool.
+struct RouteTables { float* bn; float* ss; };   // bn: [mean|rstd|a|b] x 128, ss: [S1|S2] x 128
+
+__device__ __forceinline__ void route_prologue(const RouteArgs& a, const RouteTables& t, int bid) {
+  if (a.bn_on) {
+    bn_reduce_to_lds(a.bn, t.bn, t.bn + 128, t.bn + 256, t.bn + 384, t.ss);
+    __syncthreads();
+    slab_sum_to_lds(a.bwd_slab, a.bwd_nslab, 2 * a.C, t.ss);
+    if (bid == 0)
+      for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+        a.doffset[c] = t.ss[c];
+        a.dscale[c] = t.ss[a.C + c];
+        if (a.run_mean) {
+          const float mean = t.bn[c];
+          const float var = 1.0f / (t.bn[128 + c] * t.bn[128 + c]) - a.bn.eps;
+          a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
+          a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var;
+        }
+      }
+  }
+  __syncthreads();
+}
+
+// dst(oy - oa, ox, c) = dc[b, oy, ox, c] for conv-output rows [oa, ob) of image b.  The
+// caller has zero-filled the destination (positions a pool window did not select).
+template <class DST>
+__device__ __forceinline__ void route_stage(const RouteArgs& a, const RouteTables& t, int b, int oa, int ob,
+                                            DST dst) {
+  const int PSH = a.pool_on ? a.PSH : 1, PSW = a.pool_on ? a.PSW : 1;
+  const int py0 = oa / PSH, py1 = min(a.h, (ob - 1) / PSH + 1);
+  const int wc = a.w * a.C;
+  const int n = max(0, py1 - py0) * wc;
+  const FastDiv dwc(wc), dC(a.C);
+  const float inv_n = a.bn_on ? 1.0f / a.bn.count : 0.f;
+  const long base = ((long)b * a.h + py0) * wc;
+  if (n <= 0) return;
+  constexpr int U = 4;
+  for (int i0 = 0; i0 < n; i0 += CONV_THREADS * U) {
+    float gz[U], yv[U];
+    int am[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * CONV_THREADS + (int)threadIdx.x, n - 1);
+      gz[u] = a.dz[base + i];
+      yv[u] = a.y[base + i];
+      am[u] = a.pool_on ? (int)a.argmax[base + i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * CONV_THREADS + (int)threadIdx.x;
+      if (i >= n) break;
+      int pr, rem, px, c;
+      dwc.divmod(i, pr, rem);
+      dC.divmod(rem, px, c);
+      float g = gz[u];
+      if (a.bn_on) {
+        const float xhat = (yv[u] - t.bn[c]) * t.bn[128 + c];
+        g = t.bn[256 + c] * (g - t.ss[c] * inv_n - xhat * t.ss[a.C + c] * inv_n);
+      }
+      g = act_bwd(g, yv[u], yv[u], a.out_act, a.out_alpha);
+      const int oy = (py0 + pr) * PSH + (a.pool_on ? am[u] / a.PKW : 0);
+      const int ox = px * PSW + (a.pool_on ? am[u] % a.PKW : 0);
+      if (oy >= oa && oy < ob && ox < a.OW) dst(oy - oa, ox, c, g);
+    }
+  }
+}
+
 // -----------------------------------------------------------------------------------
 // Conv input gradient:  dx[b,y,x,ci] = sum_{i,j,co} dc[b,oy,ox,co] * W[i,j,ci,co]
 // (one workgroup per image x row band x input-channel block, dc rows staged in LDS),
@@ -282,7 +353,8 @@ struct ConvDgradArgs {
 
 template <int CB>
 __device__ __forceinline__ void conv_dgrad_body(const ConvDgradArgs& a, int bid, float* smem,
-                                                float* s_bn, float* s_stat) {
+                                                float* s_bn, float* s_stat,
+                                                const RouteArgs* rt = nullptr, RouteTables rtt = {}) {
   // smem (dynamic): dc rows of the band [rows][OW][Cout] then weights [(i,j,ci)][Cout]
   const ConvGeom& g = a.g;
   const int b = bid / a.nbands, band = bid % a.nbands;
@@ -299,8 +371,14 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvDgradArgs& a, int bid,
   for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) s_stat[i] = 0.f;
   stage_to_lds<4>(s_w, a.w, nw, [](float v, int) { return v; });
   const int nd = max(0, o1 - o0) * rowlen;
-  const float* src = a.dc + ((long)b * g.OH + o0) * rowlen;
-  stage_to_lds<8>(s_dc, src, nd, [](float v, int) { return v; });
+  if (rt) {             // dc rows computed here from the unit output (route fused)
+    for (int e = threadIdx.x; e < nd; e += CONV_THREADS) s_dc[e] = 0.f;
+    __syncthreads();
+    route_stage(*rt, rtt, b, o0, o1, [&](int r, int ox, int c, float v) { s_dc[r * rowlen + ox * g.Cout + c] = v; });
+  } else {
+    const float* src = a.dc + ((long)b * g.OH + o0) * rowlen;
+    stage_to_lds<8>(s_dc, src, nd, [](float v, int) { return v; });
+  }
   __syncthreads();
 
   const int npix = (y1 - y0) * g.W;
@@ -655,7 +733,8 @@ struct ConvWgradArgs {
 
 template <bool U8>
 __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid, float* smem,
-                                                float* s_bn) {
+                                                float* s_bn, const RouteArgs* rt = nullptr,
+                                                RouteTables rtt = {}) {
   const ConvGeom& g = a.g;
   const int b = bid / a.nbands, band = bid % a.nbands;
   const int r0 = band * a.band_rows, r1 = min(g.OH, r0 + a.band_rows);
@@ -687,12 +766,14 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid,
   __syncthreads();
   {
     const long ioff = U8 ? idx[b] * (long)(g.H * irow) + (long)iy0 * irow : xoff;
-    const bool v4 = ((ioff | nx | doff | nd) & 3) == 0;
+    const bool v4 = ((ioff | nx | (rt ? 0 : doff | nd)) & 3) == 0;
     const int sx = v4 ? 4 : 1;
-    const int nxv = (nx + sx - 1) / sx, ndv = (nd + sx - 1) / sx, nmax = max(nxv, ndv);
+    const int nxv = (nx + sx - 1) / sx, ndv = rt ? 0 : (nd + sx - 1) / sx, nmax = max(nxv, ndv);
     const uint8_t* isrc = U8 ? a.img + ioff : nullptr;
     const float* xsrc = U8 ? nullptr : a.x + xoff;
-    const float* dsrc = a.dc + doff;
+    // with the route fused the dc rows come from route_stage below: the dc loads then read
+    // one valid element (unconditional, branch-free) and are discarded
+    const float* dsrc = rt ? rt->dz : a.dc + doff;
     const FastDiv dirow(irow), dcout(g.Cout), dcin(g.Cin);
     const int xcol0 = g.PL * g.Cin, trow0 = iy0 - ty0;
     constexpr int U = 4;
@@ -704,7 +785,7 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = base + u * CONV_THREADS + threadIdx.x;
-        const int jx = min(i, max(nxv - 1, 0)), jd = min(i, max(ndv - 1, 0));
+        const int jx = min(i, max(nxv - 1, 0)), jd = rt ? 0 : min(i, max(ndv - 1, 0));
         if (v4) {
           if (U8) {
             const uchar4 q = reinterpret_cast<const uchar4*>(isrc)[jx];
@@ -757,6 +838,8 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradArgs& a, int bid,
       }
     }
   }
+  if (rt)               // dc rows computed here from the unit output (route fused)
+    route_stage(*rt, rtt, b, r0, r1, [&](int r, int ox, int c, float v) { s_dc[(r * g.OW + ox) * a.c16 + c] = v; });
   __syncthreads();
 
   // ---- MFMA: rows = taps (i, j, ci | bias), cols = Cout, K = band pixels (wave-split).
@@ -880,6 +963,21 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_bwd_pair_kernel(ConvDgradAr
   __shared__ float s_stat[2 * 128];
   if ((int)blockIdx.x < nd) conv_dgrad_body<CB_T>(d, blockIdx.x, smem, s_bn, s_stat);
   else conv_wgrad_body<false>(w, blockIdx.x - nd, smem, s_bn);
+}
+
+// The same pair with the unit's route backward (BN backward + act backward + pool
+// routing) fused into both bodies' dc staging — one launch fewer per conv unit.
+__global__ __launch_bounds__(CONV_THREADS) void conv_bwd_route_pair_kernel(ConvDgradArgs d, ConvWgradArgs w,
+                                                                           int nd, RouteArgs r) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * 128 + 2 * 128];
+  __shared__ float s_stat[2 * 128];
+  __shared__ float s_rbn[4 * 128];
+  __shared__ float s_rss[2 * 128];
+  const RouteTables t{s_rbn, s_rss};
+  route_prologue(r, t, blockIdx.x);
+  if ((int)blockIdx.x < nd) conv_dgrad_body<CB_T>(d, blockIdx.x, smem, s_bn, s_stat, &r, t);
+  else conv_wgrad_body<false>(w, blockIdx.x - nd, smem, s_bn, &r, t);
 }
 
 static void fwd_bands(const ConvGeom& g, const PoolGeom& p, int& nbands, int& rows, int& rows_in) {
@@ -1139,6 +1237,64 @@ CSA_API int csa_conv_wgrad(const float* x, const uint8_t* img, const int64_t* id
   if (img) hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(CONV_THREADS), shm, st, a);
   else hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(CONV_THREADS), shm, st, a);
   return (int)hipGetLastError();
+}
+
+static RouteArgs route_args(const float* dz, const float* y, const uint8_t* argmax, float* dc, const int* g,
+                            int out_act, float out_alpha, const float* bn_slab, int bn_nslab, float bn_count,
+                            float bn_eps, const float* bn_scale, const float* bn_offset, const float* bwd_slab,
+                            int bwd_nslab, float* dscale, float* doffset, float* run_mean, float* run_var,
+                            float momentum) {
+  RouteArgs a{};
+  a.run_mean = run_mean; a.run_var = run_var; a.momentum = momentum;
+  a.dz = dz; a.y = y; a.argmax = argmax; a.dc = dc;
+  a.B = g[0]; a.h = g[1]; a.w = g[2]; a.C = g[3]; a.OH = g[4]; a.OW = g[5];
+  a.pool_on = g[6]; a.PKW = g[8]; a.PSH = g[9]; a.PSW = g[10]; a.PPT = g[11]; a.PPL = g[12];
+  a.overlap = a.pool_on && (g[7] != g[9] || g[8] != g[10]);
+  a.out_act = out_act; a.out_alpha = out_alpha;
+  a.bn = BNRef{bn_slab, bn_nslab, a.C, bn_count, bn_eps, bn_scale, bn_offset};
+  a.bn_on = bn_slab != nullptr;
+  a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab; a.dscale = dscale; a.doffset = doffset;
+  return a;
+}
+
+// Conv unit backward in ONE launch with the unit's route fused (see
+// conv_bwd_route_pair_kernel).  Returns 1 when launched, 0 when the route shape is outside
+// the fused family (overlapping or padded pool: the caller runs csa_route_bwd +
+// csa_conv_bwd), < 0 on error.
+CSA_API int csa_conv_bwd_route(const float* w, float* dx, const int* geom, const float* x_fwd, int in_act,
+                               float in_alpha, const float* bn_slab, int bn_nslab, float bn_count, float bn_eps,
+                               const float* bn_scale, const float* bn_offset, float* bwd_slab, float* dW,
+                               float* db, int stripes, const float* dz, const float* y, const uint8_t* argmax,
+                               const int* rg, int out_act, float out_alpha, const float* r_bn_slab,
+                               int r_bn_nslab, float r_bn_count, float r_bn_eps, const float* r_bn_scale,
+                               const float* r_bn_offset, const float* r_bwd_slab, int r_bwd_nslab,
+                               float* dscale, float* doffset, float* run_mean, float* run_var, float momentum,
+                               hipStream_t st) {
+  RouteArgs r = route_args(dz, y, argmax, nullptr, rg, out_act, out_alpha, r_bn_slab, r_bn_nslab, r_bn_count,
+                           r_bn_eps, r_bn_scale, r_bn_offset, r_bwd_slab, r_bwd_nslab, dscale, doffset,
+                           run_mean, run_var, momentum);
+  if (r.C > 128) return -1;
+  if (r.pool_on && (r.overlap || r.PPT != 0 || r.PPL != 0)) return 0;
+  ConvDgradArgs d;
+  ConvWgradArgs wg;
+  size_t shm_d, shm_w;
+  int rc = dgrad_args(nullptr, w, dx, geom, x_fwd, in_act, in_alpha, bn_slab, bn_nslab, bn_count, bn_eps,
+                      bn_scale, bn_offset, bwd_slab, d, shm_d);
+  if (rc) return rc;
+  const ConvGeom& g = d.g;
+  if (g.Cout != r.C || g.OH != r.OH || g.OW != r.OW) return -4;
+  rc = wgrad_args(x_fwd, nullptr, nullptr, nullptr, dW, db, stripes, g.B, g.H, g.W, g.Cin, g.KH, g.KW, g.SH, g.SW,
+                  g.PT, g.PL, g.OH, g.OW, g.Cout, bn_slab, bn_nslab, bn_count, bn_eps, bn_scale, bn_offset,
+                  in_act, in_alpha, nullptr, wg, shm_w);
+  if (rc) return rc;
+  static bool attr = set_lds_attr((const void*)conv_bwd_route_pair_kernel);
+  (void)attr;
+  const int nd = g.B * d.nbands;
+  dim3 grid((unsigned)(nd + g.B * wg.nbands));
+  hipLaunchKernelGGL(conv_bwd_route_pair_kernel, grid, dim3(CONV_THREADS), std::max(shm_d, shm_w), st, d, wg,
+                     nd, r);
+  const int e = (int)hipGetLastError();
+  return e ? -e : 1;
 }
 
 // Conv unit backward in ONE launch: input gradient (as csa_conv_dgrad) + weight gradient
