@@ -121,7 +121,7 @@ def restore_engine(eng, obj: Dict[str, Any]) -> None:
             eng.slots.copy_(slots.to(eng.slots.device))
         elif slots.dim() == 2 and slots.shape[1] >= hi:      # full slots -> this rank's shard
             eng.slots.copy_(slots[:, lo:hi].to(eng.slots.device))
-    eng.dstep.fill_(int(obj.get("dstep", obj["step"])))
-    eng.host_step = int(obj.get("host_step", obj["step"]))
+    eng.dstep.fill_(int(obj["dstep"] if "dstep" in obj else obj["step"]))
+    eng.host_step = int(obj["host_step"] if "host_step" in obj else obj["step"])
     # continue the batch sequence exactly where the unbroken run would be
     eng.stream.seek(eng.host_step)

@@ -206,3 +206,21 @@ def test_training_reduces_loss_cpu():
     late = eng.ring_loss[110:120].mean().item()
     assert late < 0.5 * early
     assert eng.evaluate(synthetic_mnist(500, seed=2)) > 0.8
+
+
+def test_dense_last_layout_same_params_by_name():
+    """The "lowrank" DP strategy lays the flat buffer out dense-last (conv/BN/head first)
+    so its all-reduced remainder is one range; values are identical by name."""
+    cfg = parse_train_config(SAMPLE_CONFIG)
+    a = build_model(cfg)
+    b = build_model(cfg, dense_last=True)
+    assert a.state.shapes.keys() == b.state.shapes.keys()
+    names = list(b.state.offsets)
+    dense = [lp.name for lp in cfg.plan().layers if isinstance(lp.spec, DenseSpec)]
+    assert dense
+    head_end = b.state.offsets["head.bias"]
+    assert all(b.state.offsets[f"{n}.weight"] > head_end for n in dense)
+    for n in names:
+        assert torch.equal(a.state.view(n), b.state.view(n)), n
+    x = torch.rand(4, 784)
+    torch.testing.assert_close(a(x), b(x))

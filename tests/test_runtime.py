@@ -297,3 +297,22 @@ def test_watchdog_kills_hung_worker(tmp_path, monkeypatch):
         assert "heartbeat" in db.get_job(jid)["error"]
     finally:
         jm.shutdown()
+
+
+def test_checkpoint_resume_across_flat_layouts():
+    """Optimizer slots saved under the dense-last ("lowrank") layout re-map by name when
+    the job resumes under the DSL-order layout of "allreduce"."""
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    cfg = parse_train_config(dict(SMALL, optimizer_name="AdagradOptimizer"))
+    train, _ = _data()
+    a = TrainEngine(cfg, train, strategy="lowrank")
+    for _ in range(3):
+        a.step()
+    obj = ckpt.engine_state(a)
+    b = TrainEngine(cfg, train, strategy="allreduce")
+    assert a.model.state.offsets != b.model.state.offsets
+    ckpt.restore_engine(b, obj)
+    for n in a.model.state.shapes:
+        torch.testing.assert_close(a.model.state.view(n, a.slots[0]), b.model.state.view(n, b.slots[0]))
+        torch.testing.assert_close(a.model.state.view(n, a.flat), b.model.state.view(n, b.flat))
