@@ -164,7 +164,9 @@ class TrainEngine:
         self.dstep.copy_(saved[2]); self.stream.cursor.copy_(saved[3])
         self.program.reset_after_warmup() if hasattr(self.program, "reset_after_warmup") else None
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: the RCCL watchdog thread queries events of earlier collectives while
+        # this thread captures; in "global" mode that query aborts the process
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.program.run()
         self.graph = g
         # capture does not execute: the cursor/step still point at this step
