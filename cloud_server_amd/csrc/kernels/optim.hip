@@ -28,9 +28,16 @@ struct ZeroList { float* p[MAXZ]; long n[MAXZ]; int count; };
 struct Fold { long off, n, ld; float* src; int S; };
 struct FoldList { Fold f[MAXF]; int count; long lo, hi; };
 
+constexpr int MAXK = 8;
+// Gradient ranges whose producer STORES every element each step (e.g. a dense weight
+// gradient computed without split-K): the update need not re-zero them — for the sample
+// model that is fc1's 8 MB, ~15 % of the optimizer's memory traffic.
+struct KeepList { long lo[MAXK], hi[MAXK]; int count; };
+
 struct OptArgs {
   int opt; float* w; const float* g; float* s0; float* s1; long n;
   float* gz;                       // if set (== g): each thread zeroes the gradient it read
+  KeepList keep;                   // ... except inside these ranges (float4-aligned)
   float lr; const int64_t* step;   // 1-based step AFTER the head kernel's increment
   ZeroList z; FoldList fold;
   int64_t* cursor;                 // batch-stream cursor: += 1 at the end of the step
@@ -97,7 +104,11 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     // Zeroing the accumulators the next step adds into must not race with this read:
     // a zero-list pass over flat-gradient ranges run by OTHER threads could clear an
     // element before its owner read it, so the owner clears what it read.
-    if (a.gz) reinterpret_cast<float4*>(a.gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.gz) {
+      bool keep = false;
+      for (int k = 0; k < a.keep.count; ++k) keep |= (i * 4 >= a.keep.lo[k]) & (i * 4 < a.keep.hi[k]);
+      if (!keep) reinterpret_cast<float4*>(a.gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (i * 4 + 3 >= a.fold.lo && i * 4 < a.fold.hi) g = fold_grad(a.fold, i * 4, g);
     float* wp = (float*)&w;
     const float* gp = (const float*)&g;
@@ -160,10 +171,16 @@ using namespace csa;
 CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, long n, int zero_grad,
                           float lr, const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
                           int nzero, const long* fold_off, const long* fold_n, float* const* fold_src,
-                          const int* fold_S, const long* fold_ld, int nfold, int64_t* cursor,
-                          hipStream_t st) {
-  if (n % 4 || nzero > MAXZ || nfold > MAXF) return -1;
+                          const int* fold_S, const long* fold_ld, int nfold, const long* keep_lo,
+                          const long* keep_hi, int nkeep, int64_t* cursor, hipStream_t st) {
+  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK) return -1;
   OptArgs a{};
+  a.keep.count = nkeep;
+  for (int i = 0; i < nkeep; ++i) {
+    if (keep_lo[i] % 4 || keep_hi[i] % 4) return -1;
+    a.keep.lo[i] = keep_lo[i];
+    a.keep.hi[i] = keep_hi[i];
+  }
   a.cursor = cursor;
   a.opt = opt; a.w = w; a.g = g; a.s0 = s0; a.s1 = s1; a.n = n; a.lr = lr; a.step = step;
   a.gz = zero_grad ? g : nullptr;

@@ -405,6 +405,21 @@ class HipProgram:
                 regs.append(u.in_tf.slab.view(-1))          # forward stats (atomic rows)
                 if u.kind == "conv":
                     regs.append(u.in_tf.bwd_slab.view(-1))  # conv dgrad folds rows atomically
+        # dense weight gradients produced without split-K are STORED whole every step (by the
+        # fused dense backward, the separate wgrad or the lowrank wgrad), so the optimizer
+        # skips re-zeroing them (keep ranges, float4-aligned: the flat layout aligns to 64)
+        self.keep_ranges = []
+        offs = self.model.state.offsets
+        for u in self.units:
+            if u.kind != "dense":
+                continue
+            fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
+            m = B * (self.e.ctx.world if u in getattr(self, "lr_units", []) else 1)
+            if self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
+                for p in ("weight", "bias"):
+                    n = f"{u.layer.name}.{p}"
+                    lo = offs[n]
+                    self.keep_ranges.append((lo, lo + (self.gviews[n].numel() // 4) * 4))
         self.ps_mode = self.e.sync.strategy == "ps" and self.e.ctx.enabled
         self.zero_regions = regs + (flat if self.ps_mode else [])
         if len(self.zero_regions) > 16:
@@ -703,10 +718,13 @@ class HipProgram:
         fs = (C.c_void_p * 8)(*[f[2].data_ptr() for f in folds])
         fS = (C.c_int * 8)(*[f[3] for f in folds])
         fl = (C.c_long * 8)(*[f[1] for f in folds])
+        keep = self.keep_ranges[:8]
+        klo = (C.c_long * 8)(*[k[0] for k in keep])
+        khi = (C.c_long * 8)(*[k[1] for k in keep])
         self._rc(lib.csa_optimizer(
             e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), 0 if self.ps_mode else 1,
             float(e.lr), K.ptr(e.dstep),
-            zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, len(folds),
+            zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, len(folds), klo, khi, len(keep),
             K.ptr(e.stream.cursor), st), "optimizer")
         if e.sync.strategy == "ps" and e.ctx.enabled:
             e.sync.all_gather_params(e.flat)
