@@ -331,12 +331,16 @@ __device__ __forceinline__ void gemm_body(LA la, LB lb, EPI epi, int M, int N, i
       stA.fetch(la, m0, k + KC, ke);
       stB.fetch(lb, n0, k + KC, ke);
     }
+    // all of the chunk's operand reads are issued before the MFMA chain (read -> MFMA
+    // pairs left each MFMA waiting on its own ds_read: ~120 cycles per 64-cycle MFMA)
+    float av[KC / 2], bv[KC / 2];
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 2) {
-      float av = sa[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
-      float bv = sb[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      av[kk / 2] = sa[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
+      bv[kk / 2] = sb[(kk + (lane >> 5)) * LDS_PAD + (lane & 31)];
     }
+#pragma unroll
+    for (int kk = 0; kk < KC / 2; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc, 0, 0, 0);
     if (it == 1) GEMM_STAMP(12);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
