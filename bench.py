@@ -71,6 +71,8 @@ def main() -> int:
     eng.sync_device()
     dt = time.perf_counter() - t0
     dt = all_reduce_max(ctx, dt)
+    if eng.sync is not None:
+        eng.sync.check()   # a timed-out xGMI peer wait invalidates the run: fail loudly
     m = eng.metrics_since(eng.host_step - min(args.steps, 100))
 
     total = args.batch * ctx.world * args.steps / dt
@@ -97,6 +99,12 @@ def main() -> int:
                 "parallelism": f"dp{ctx.world}" + ("" if args.strategy == "allreduce" else f"-{args.strategy}"),
                 "backend": eng.backend,
                 "hip_graph": eng.use_graph,
+                # per call site: xGMI peer-buffer kernel or RCCL, and (CSA_XGMI=auto) the
+                # start-up timings that decided it
+                "collectives": {t: ("xgmi" if c is not None else "rccl") for t, c in eng.sync._choice.items()}
+                               or ("rccl" if ctx.world > 1 else "none"),
+                "xgmi": eng.sync.xgmi_reason,
+                "collective_tuning_us": eng.sync.xgmi_tuning,
             },
             "final_loss": round(m["loss"], 4),
             "final_batch_accuracy": round(m["accuracy"], 4),

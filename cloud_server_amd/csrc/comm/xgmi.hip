@@ -1,0 +1,208 @@
+// Intra-node collectives over xGMI through IPC-mapped peer buffers (gfx950).
+//
+// Replaces the reference's per-step PS pull/push over TF gRPC (construct_distribute.py:
+// 355-357, 413) for the small, latency-bound messages of this
+// workload.  RCCL rings move a message hop by hop over ONE xGMI link per step; an
+// MI355X has 7 point-to-point links per GPU, so here every rank PUSHES its whole message
+// into a slot of every peer's receive buffer at once (7 links busy, posted writes), then
+// raises a per-(block, source) flag in each peer.  A receiving block waits only for the
+// flags of the chunk it owns and then works from LOCAL memory:
+//
+//   * all-gather  — copy the world slots of its chunk into the rank-major output;
+//   * all-reduce  — sum the world slots of its chunk (fp32) into the in/out tensor.
+//
+// Protocol details
+//   * receive buffers and flags are allocated uncached (hipDeviceMallocUncached), so a
+//     reader never hits a stale L2 line written by a peer (XCD/L2 non-coherence);
+//   * data stores -> __threadfence_system() -> __syncthreads() -> flag store with
+//     release/system scope; the waiter does an acquire/system load of the flag;
+//   * the epoch e = (device sequence counter + 1) is the flag value; the buffer parity
+//     e & 1 double-buffers the slots: a rank can write epoch e+2 into a peer only after
+//     it saw that peer's epoch e+1 push, which the peer issues after finishing epoch e;
+//   * the counter advances in the launch's last-finishing block, so the same kernel
+//     node replays correctly inside a HIP graph (no host-side epoch);
+//   * every wait is bounded (wall clock): on timeout the kernel raises `err` and every
+//     later call returns at once, so a missing peer can never hang the GPU.
+// One channel (buffers + flags + counter) serves ONE device-ordered sequence of calls;
+// call sites that may run concurrently on different streams use different channels.
+#include "../kernels/common.h"
+#include <cstring>
+
+namespace csa {
+
+constexpr int XG_MAXR = 8;     // ranks per node
+constexpr int XG_MAXB = 256;   // blocks per launch (all co-resident: 256 CUs)
+constexpr int XG_MAXSEG = 8;
+
+struct XgSeg { const char* src; char* dst; long bytes; long off; };
+
+struct XgArgs {
+  int op, rank, world, nseg;
+  long msg_bytes, slot_bytes;
+  char* buf[XG_MAXR];           // rank r's receive buffer [2][world][slot_bytes] (mapped)
+  unsigned* flags[XG_MAXR];     // rank r's flags [2][XG_MAXB][XG_MAXR] (mapped)
+  XgSeg seg[XG_MAXSEG];
+  unsigned* seq; unsigned* done; int* err;
+  unsigned long long timeout_ticks;
+};
+
+__device__ __forceinline__ int xg_find(const XgArgs& a, long off) {
+  int s = 0;
+#pragma unroll 1
+  for (int k = 1; k < a.nseg; ++k) s = off >= a.seg[k].off ? k : s;
+  return s;
+}
+
+__global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
+  __shared__ int s_abort;
+  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  if (t == 0) s_abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  __syncthreads();
+  if (s_abort) return;
+  const unsigned e = *a.seq + 1u;
+  const int par = e & 1u;
+  // this block's chunk of the packed per-rank message, in 16-byte units
+  const long units = a.msg_bytes >> 4;
+  const long per = (units + nb - 1) / nb;
+  const long u0 = b * per < units ? b * per : units;
+  const long u1 = u0 + per < units ? u0 + per : units;
+  const long my_slot = ((long)par * a.world + a.rank) * a.slot_bytes;
+
+  // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included)
+  for (long u = u0 + t; u < u1; u += blockDim.x) {
+    const long off = u << 4;
+    const XgSeg& s = a.seg[xg_find(a, off)];
+    const uint4 v = *reinterpret_cast<const uint4*>(s.src + (off - s.off));
+#pragma unroll
+    for (int p = 0; p < XG_MAXR; ++p)
+      if (p < a.world) *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
+  }
+  // publish: every wave drains its stores, the barrier, then ONE system-scope release
+  // (one L2 write-back per block, not per wave) before this block's flags go out
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const long fidx = ((long)par * XG_MAXB + b) * XG_MAXR;
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    for (int p = 0; p < a.world; ++p)
+      __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+
+  // 2) wait for every source's flag of this chunk (one lane polls all sources, bounded),
+  // then ONE system-scope acquire for the block (the vector L1 is per CU)
+  if (t == 0) {
+    const unsigned* f = a.flags[a.rank] + fidx;
+    const unsigned long long t0 = wall_clock64();
+    for (int r = 0; r < a.world; ++r) {
+      while (__hip_atomic_load(f + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+        if (wall_clock64() - t0 > a.timeout_ticks) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (s_abort) break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+
+  // 3) consume from local memory
+  if (!s_abort) {
+    const char* mine = a.buf[a.rank] + (long)par * a.world * a.slot_bytes;
+    for (long u = u0 + t; u < u1; u += blockDim.x) {
+      const long off = u << 4;
+      const XgSeg& s = a.seg[xg_find(a, off)];
+      const long so = off - s.off;
+      if (a.op == 0) {           // all-gather: out is rank-major [world][seg.bytes]
+        uint4 v[XG_MAXR];
+#pragma unroll
+        for (int r = 0; r < XG_MAXR; ++r)
+          if (r < a.world) v[r] = *reinterpret_cast<const uint4*>(mine + (long)r * a.slot_bytes + off);
+#pragma unroll
+        for (int r = 0; r < XG_MAXR; ++r)
+          if (r < a.world) *reinterpret_cast<uint4*>(s.dst + (long)r * s.bytes + so) = v[r];
+      } else {                   // all-reduce (fp32 sum), rank order fixed -> bitwise identical on all ranks
+        float4 v[XG_MAXR];
+#pragma unroll
+        for (int r = 0; r < XG_MAXR; ++r)
+          if (r < a.world) v[r] = *reinterpret_cast<const float4*>(mine + (long)r * a.slot_bytes + off);
+        float4 acc = v[0];
+#pragma unroll
+        for (int r = 1; r < XG_MAXR; ++r)
+          if (r < a.world) { acc.x += v[r].x; acc.y += v[r].y; acc.z += v[r].z; acc.w += v[r].w; }
+        *reinterpret_cast<float4*>(s.dst + so) = acc;
+      }
+    }
+  }
+
+  // 4) the last block to finish advances the epoch for the next call on this channel
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(a.done, 1u);
+    if (prev == (unsigned)nb - 1) {
+      *a.done = 0;
+      *a.seq = e;
+      __threadfence();
+    }
+  }
+}
+
+}  // namespace csa
+
+using namespace csa;
+
+// Uncached device allocation + its IPC handle (64 bytes written to `handle`).
+CSA_API int csa_xgmi_alloc(long bytes, void** ptr, void* handle) {
+  hipError_t e = hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  if ((e = hipMemset(*ptr, 0, (size_t)bytes)) != hipSuccess) return (int)e;
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), *ptr);
+}
+
+CSA_API int csa_xgmi_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+CSA_API int csa_xgmi_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+CSA_API int csa_xgmi_free(void* ptr) { return (int)hipFree(ptr); }
+CSA_API int csa_xgmi_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+CSA_API int csa_xgmi_max_blocks() { return XG_MAXB; }
+
+// op 0 = all-gather (dst[r] = src of rank r, rank-major per segment), 1 = fp32 sum all-reduce
+// (src == dst allowed).  Segments are packed back to back into one per-rank message of
+// sum(bytes) <= slot_bytes; every segment size and pointer must be 16-byte aligned.
+// state = 3 x uint32 on the device: {seq, done, err}.
+CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* const* bufs, void* const* flags,
+                         int nseg, void* const* srcs, void* const* dsts, const long* seg_bytes,
+                         unsigned* state, double timeout_s, int nblocks, hipStream_t st) {
+  if (world < 1 || world > XG_MAXR || rank < 0 || rank >= world || nseg < 1 || nseg > XG_MAXSEG) return -1;
+  XgArgs a{};
+  a.op = op; a.rank = rank; a.world = world; a.nseg = nseg; a.slot_bytes = slot_bytes;
+  long off = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (seg_bytes[i] <= 0 || (seg_bytes[i] & 15) || ((uintptr_t)srcs[i] & 15) || ((uintptr_t)dsts[i] & 15)) return -2;
+    a.seg[i] = XgSeg{static_cast<const char*>(srcs[i]), static_cast<char*>(dsts[i]), seg_bytes[i], off};
+    off += seg_bytes[i];
+  }
+  if (off > slot_bytes) return -3;
+  a.msg_bytes = off;
+  for (int r = 0; r < world; ++r) {
+    a.buf[r] = static_cast<char*>(bufs[r]);
+    a.flags[r] = static_cast<unsigned*>(flags[r]);
+  }
+  a.seq = state; a.done = state + 1; a.err = reinterpret_cast<int*>(state + 2);
+  a.timeout_ticks = (unsigned long long)(timeout_s * 1.0e8);   // wall_clock64: 100 MHz
+  const long units = off >> 4;
+  // ~8 KB per block: measured 9.6 us vs 16.9 (32 KB) / 52.5 (128 KB) for the 0.9 MB
+  // lowrank gather (profiles/r1s4_xgmi_collectives.md)
+  int nb = nblocks > 0 ? nblocks : (int)((units + 511) / 512);
+  nb = nb < 1 ? 1 : (nb > XG_MAXB ? XG_MAXB : nb);
+  hipLaunchKernelGGL(xgmi_kernel, dim3(nb), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}

@@ -1,6 +1,7 @@
 """Build the native libraries in-tree with hipcc for gfx950 (no hipify, no JIT cache).
 
-* ``libcsa_kernels.so`` — the HIP/CDNA4 kernels (``csrc/kernels/*.hip``), C ABI, called
+* ``libcsa_kernels.so`` — the HIP/CDNA4 kernels (``csrc/kernels/*.hip``) and the xGMI
+  peer-buffer collectives (``csrc/comm/*.hip``), C ABI, called
   through ctypes from ``ops.fused``.  Launchers take a ``hipStream_t`` and never
   allocate or synchronise, so they are captured into HIP graphs by the engine.
 * ``libcsa_runtime.so`` — host-side C++ runtime pieces (``csrc/runtime/*.cpp``): the
@@ -58,8 +59,8 @@ def _run(cmd: List[str], verbose: bool) -> None:
 
 
 def build_kernels(verbose: bool = False, force: bool = False) -> str:
-    srcs = _sources("kernels", (".hip",))
-    hdrs = _sources("kernels", (".h",))
+    srcs = _sources("kernels", (".hip",)) + _sources("comm", (".hip",))
+    hdrs = _sources("kernels", (".h",)) + _sources("comm", (".h",))
     flags = ["-O3", "-fPIC", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=fast-honor-pragmas",
              "-Wno-unused-result"]
     stamp = _hash(srcs + hdrs, " ".join(flags))

@@ -52,6 +52,13 @@ _SIGS = {
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),
     "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),
+    "csa_xgmi_alloc": (I, [L, C.POINTER(P), P]),
+    "csa_xgmi_open": (I, [P, C.POINTER(P)]),
+    "csa_xgmi_close": (I, [P]),
+    "csa_xgmi_free": (I, [P]),
+    "csa_xgmi_handle_bytes": (I, []),
+    "csa_xgmi_max_blocks": (I, []),
+    "csa_xgmi_run": (I, [I, I, I, L, P, P, I, P, P, P, P, C.c_double, I, P]),
 }
 
 

@@ -21,7 +21,10 @@ SURVEY.md §2.3).  On one MI355X node that becomes:
   config fc1 that is 0.9 MB gathered per rank instead of an 8 MB all-reduce.
 
 All strategies are written against ``torch.distributed`` so the identical code runs on
-gloo (CPU tests) and RCCL (MI355X).
+gloo (CPU tests) and RCCL (MI355X).  On a single node with RCCL the latency-bound
+collectives (lowrank gathers, the remainder all-reduce, allreduce buckets) go through
+the xGMI peer-buffer path (``parallel.xgmi``, one launch, all 7 links) instead, once a
+start-up self-test passed on every rank (``CSA_XGMI=auto|1|0``).
 """
 from __future__ import annotations
 
@@ -32,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 from .dist import DistContext
+from . import xgmi as _xg
 
 DEFAULT_BUCKET_BYTES = 32 << 20   # one bucket covers the sample model's 9.1 MB gradient
 
@@ -49,6 +53,105 @@ class GradSync:
         # grouped RCCL launches for the multi-tensor lowrank collectives (opt-in: a grouped
         # collective inside HIP-graph capture crashed capture_end on ROCm 7 / torch 2.10)
         self.coalesce = ctx.backend == "nccl" and os.environ.get("CSA_COALESCE", "0") == "1"
+        self.xgmi: Optional[_xg.XgmiComm] = None
+        self.xgmi_reason = "off"
+        self.xgmi_mode = _xg.enabled_by_env()
+        self.xgmi_tuning: dict = {}      # tag -> {"bytes", "xgmi_us", "rccl_us"} (auto mode)
+        self._choice: dict = {}
+        self._setup_xgmi()
+
+    def _setup_xgmi(self) -> None:
+        mode = self.xgmi_mode
+        if mode in ("0", "off", "false") or self.ctx.backend != "nccl" or not self.ctx.enabled:
+            self.xgmi_reason = "disabled" if self.ctx.enabled else "single rank"
+            return
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.ctx.world)))
+        if local_world != self.ctx.world or self.ctx.world > 8:
+            self.xgmi_reason = "multi-node job: RCCL"
+            return
+        comm = _xg.XgmiComm(self.ctx.rank, self.ctx.world, self.ctx.device)
+        if _xg.self_test(comm):
+            self.xgmi, self.xgmi_reason = comm, "on"
+            return
+        comm.close()
+        if mode in ("1", "on", "true"):
+            raise RuntimeError("CSA_XGMI=1 but the xGMI peer-buffer self-test failed")
+        self.xgmi_reason = "self-test failed: RCCL"
+
+    def check(self) -> None:
+        """Raise if a peer-buffer collective timed out (its results are not valid)."""
+        if self.xgmi is not None:
+            self.xgmi.check()
+
+    def _xg_channel(self, tag: str, srcs, dsts=None) -> Optional["_xg.XgmiChannel"]:
+        """The xGMI channel for call site ``tag``, or None for RCCL.  Decided once per tag,
+        collectively (same answer on every rank): the messages must fit the kernel's
+        alignment rules, and under ``CSA_XGMI=auto`` both paths are timed on scratch
+        copies of the real tensors (each as a HIP graph of 10 calls) and the faster wins."""
+        if self.xgmi is None:
+            return None
+        if tag in self._choice:
+            return self._choice[tag]
+        if torch.cuda.is_current_stream_capturing():
+            return None                  # undecided inside capture: RCCL (same on all ranks)
+        nbytes = sum(t.numel() * t.element_size() for t in srcs)
+        ch = self.xgmi.channel(tag, nbytes)
+        ok = ch.fits(srcs) and (dsts is None or all(d.is_contiguous() and d.data_ptr() % 16 == 0 for d in dsts))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        choice = ch if flag.item() else None
+        if choice is not None and self.xgmi_mode == "auto":
+            xg_us, rc_us = self._time_paths(ch, srcs, dsts)
+            self.xgmi_tuning[tag] = {"bytes": nbytes, "xgmi_us": round(xg_us, 2), "rccl_us": round(rc_us, 2)}
+            if not xg_us < rc_us:
+                choice = None
+        self._choice[tag] = choice
+        return choice
+
+    def _time_paths(self, ch, srcs, dsts) -> Tuple[float, float]:
+        dev = self.ctx.device
+        ss = [torch.zeros_like(t) for t in srcs]
+        sd = None if dsts is None else [torch.empty_like(d) for d in dsts]
+
+        def xg():
+            if sd is None:
+                ch.all_reduce(ss)
+            else:
+                ch.all_gather(list(zip(ss, sd)))
+
+        def rc():
+            for i, t in enumerate(ss):
+                if sd is None:
+                    dist.all_reduce(t)
+                else:
+                    dist.all_gather_into_tensor(sd[i], t)
+
+        out = []
+        for fn in (xg, rc):
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                fn()                          # eager warm-up (RCCL communicator paths)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for _ in range(10):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize(dev)
+            dist.all_reduce(torch.zeros(1, device=dev))   # line the ranks up
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(3):
+                g.replay()
+            b.record()
+            torch.cuda.synchronize(dev)
+            out.append(a.elapsed_time(b) * 1e3 / 30)
+            del g
+        t = torch.tensor(out, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0]), float(t[1])
 
     @property
     def grad_scale(self) -> float:
@@ -74,7 +177,11 @@ class GradSync:
         if not self.ctx.enabled:
             return
         for a, b in self.buckets(lo, hi):
-            dist.all_reduce(flat_grad[a:b])
+            ch = self._xg_channel(f"ar:{a}:{b}", [flat_grad[a:b]])
+            if ch is not None:
+                ch.all_reduce([flat_grad[a:b]])
+            else:
+                dist.all_reduce(flat_grad[a:b])
 
     # ---- ps (sharded) ----
     def reduce_scatter(self, flat_grad: torch.Tensor, shard_out: torch.Tensor) -> None:
@@ -98,12 +205,18 @@ class GradSync:
             return
         dist.all_gather_into_tensor(out, local.contiguous())
 
-    def all_gather_rows_many(self, pairs) -> None:
-        """Several ``all_gather_rows`` issued as ONE grouped RCCL launch where the backend
-        supports coalescing (each separate collective pays its own fixed latency)."""
+    def all_gather_rows_many(self, pairs, tag: str = "gather") -> None:
+        """Several ``all_gather_rows`` issued as ONE launch: the xGMI peer-buffer kernel, or
+        a grouped RCCL launch where the backend supports coalescing (each separate
+        collective pays its own fixed latency).  ``tag`` names the call site (one
+        device-ordered sequence of calls per tag)."""
         if not self.ctx.enabled:
             for local, out in pairs:
                 out.copy_(local)
+            return
+        ch = self._xg_channel(tag, [p[0] for p in pairs], [p[1] for p in pairs]) if len(pairs) <= 8 else None
+        if ch is not None:
+            ch.all_gather(pairs)
             return
         if self.coalesce and len(pairs) > 1:
             with dist._coalescing_manager(async_ops=False):
@@ -113,9 +226,14 @@ class GradSync:
         for local, out in pairs:
             dist.all_gather_into_tensor(out, local.contiguous())
 
-    def allreduce_ranges(self, flat: torch.Tensor, ranges) -> None:
-        """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one grouped launch on RCCL)."""
+    def allreduce_ranges(self, flat: torch.Tensor, ranges, tag: str = "ranges") -> None:
+        """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one launch: xGMI kernel or a
+        grouped RCCL launch)."""
         if not self.ctx.enabled or not ranges:
+            return
+        ch = self._xg_channel(tag, [flat[lo:hi] for lo, hi in ranges]) if len(ranges) <= 8 else None
+        if ch is not None:
+            ch.all_reduce([flat[lo:hi] for lo, hi in ranges])
             return
         if self.coalesce and len(ranges) > 1:
             with dist._coalescing_manager(async_ops=False):

@@ -1,0 +1,182 @@
+"""Peer-buffer collectives over xGMI (the custom one-shot path of SURVEY.md §5.8).
+
+Each ``XgmiChannel`` owns, per rank, an uncached receive buffer ``[2][world][slot]``
+and a flag array, both exported with ``hipIpcGetMemHandle`` and mapped into every
+other rank with ``hipIpcOpenMemHandle`` (handles travel through the process group's
+object all-gather; the data plane never touches RCCL).  A call is ONE kernel launch
+(``csrc/comm/xgmi.hip``): every rank pushes its message to all peers over its 7 xGMI
+links at once and each block then waits only on the flags of its own chunk.  The epoch
+counter lives on the device, so a call captured into a HIP graph replays correctly.
+
+Reference: the per-step variable pull / gradient push between worker and PS over TF
+gRPC (construct_distribute.py:355-357, 413).
+
+Rules
+* one channel = one device-ordered sequence of calls; call sites that can run on
+  different streams concurrently get different channels (``XgmiComm.channel(tag)``);
+* every rank must issue the same calls on a channel in the same order (SPMD);
+* waits are bounded (``timeout_s``): a missing peer sets the channel's error word and
+  later calls return at once; ``check()`` turns it into an exception on the host.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..ops import fused as K
+
+OP_GATHER, OP_ALLREDUCE = 0, 1
+
+
+def _aligned(t: torch.Tensor) -> bool:
+    return t.is_contiguous() and t.data_ptr() % 16 == 0 and (t.numel() * t.element_size()) % 16 == 0
+
+
+class XgmiChannel:
+    def __init__(self, rank: int, world: int, slot_bytes: int, device: torch.device,
+                 group=None, timeout_s: float = 20.0):
+        if not 1 <= world <= 8:
+            raise ValueError("xGMI channel: 1..8 ranks of one node")
+        self.lib = K.load(required=True)
+        self.rank, self.world, self.device = rank, world, device
+        self.slot_bytes = (int(slot_bytes) + 15) // 16 * 16
+        self.timeout_s = timeout_s
+        hb = self.lib.csa_xgmi_handle_bytes()
+        nblk = self.lib.csa_xgmi_max_blocks()
+        sizes = (2 * world * self.slot_bytes, 2 * nblk * 8 * 4)
+        self._local: List[int] = []
+        handles: List[bytes] = []
+        with torch.cuda.device(device):
+            for n in sizes:
+                p = C.c_void_p()
+                h = C.create_string_buffer(hb)
+                rc = self.lib.csa_xgmi_alloc(n, C.byref(p), h)
+                if rc:
+                    raise RuntimeError(f"xgmi alloc failed ({rc})")
+                self._local.append(p.value)
+                handles.append(h.raw)
+            allh: List[Optional[List[bytes]]] = [None] * world
+            dist.all_gather_object(allh, handles, group=group)
+            self._opened: List[int] = []
+            ptrs: List[List[int]] = [[], []]
+            for r in range(world):
+                for k in range(2):
+                    if r == rank:
+                        ptrs[k].append(self._local[k])
+                        continue
+                    p = C.c_void_p()
+                    rc = self.lib.csa_xgmi_open(C.create_string_buffer(allh[r][k], hb), C.byref(p))
+                    if rc:
+                        raise RuntimeError(f"xgmi open of rank {r}'s buffer failed ({rc})")
+                    self._opened.append(p.value)
+                    ptrs[k].append(p.value)
+        self._bufs = (C.c_void_p * world)(*ptrs[0])
+        self._flags = (C.c_void_p * world)(*ptrs[1])
+        self.state = torch.zeros(4, dtype=torch.int32, device=device)   # seq, done, err, pad
+        # workgroups per call (0: one per ~8 KB of the per-rank message, at most 256)
+        kb = int(os.environ.get("CSA_XGMI_BLOCK_KB", "0"))
+        self.nblocks = 0 if kb <= 0 else max(1, min(nblk, -(-self.slot_bytes // (kb * 1024))))
+
+    # ---------------------------------------------------------------- calls
+    def _run(self, op: int, srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
+        n = len(srcs)
+        sb = [s.numel() * s.element_size() for s in srcs]
+        rc = self.lib.csa_xgmi_run(
+            op, self.rank, self.world, self.slot_bytes, self._bufs, self._flags, n,
+            (C.c_void_p * n)(*[s.data_ptr() for s in srcs]), (C.c_void_p * n)(*[d.data_ptr() for d in dsts]),
+            (C.c_long * n)(*sb), self.state.data_ptr(), self.timeout_s, self.nblocks,
+            torch.cuda.current_stream(self.device).cuda_stream)
+        if rc:
+            raise RuntimeError(f"xgmi collective launch failed ({rc})")
+
+    def all_gather(self, pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> None:
+        """``out`` = rank-major concatenation of every rank's ``local`` (per pair)."""
+        self._run(OP_GATHER, [p[0] for p in pairs], [p[1] for p in pairs])
+
+    def all_reduce(self, tensors: Sequence[torch.Tensor]) -> None:
+        """In-place fp32 SUM over ranks (identical bits on every rank: fixed rank order)."""
+        self._run(OP_ALLREDUCE, tensors, tensors)
+
+    def fits(self, tensors: Sequence[torch.Tensor]) -> bool:
+        return (len(tensors) <= 8 and all(_aligned(t) for t in tensors)
+                and sum(t.numel() * t.element_size() for t in tensors) <= self.slot_bytes)
+
+    def error(self) -> int:
+        return int(self.state[2].item())
+
+    def check(self) -> None:
+        if self.error():
+            raise RuntimeError("xGMI collective timed out waiting for a peer (channel poisoned)")
+
+    def close(self) -> None:
+        if not self._local:
+            return
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            self.lib.csa_xgmi_close(p)
+        for p in self._local:
+            self.lib.csa_xgmi_free(p)
+        self._local, self._opened = [], []
+
+
+class XgmiComm:
+    """Channels by call-site tag, created lazily (collectively) on first use — which must
+    happen outside HIP-graph capture (the engine's eager warm-up steps do it)."""
+
+    def __init__(self, rank: int, world: int, device: torch.device, group=None, timeout_s: float = 20.0):
+        self.rank, self.world, self.device, self.group = rank, world, device, group
+        self.timeout_s = timeout_s
+        self.channels: Dict[str, XgmiChannel] = {}
+
+    def channel(self, tag: str, nbytes: int) -> XgmiChannel:
+        ch = self.channels.get(tag)
+        if ch is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"xgmi channel {tag!r} first used inside graph capture")
+            ch = XgmiChannel(self.rank, self.world, nbytes, self.device, self.group, self.timeout_s)
+            self.channels[tag] = ch
+        return ch
+
+    def check(self) -> None:
+        for ch in self.channels.values():
+            ch.check()
+
+    def close(self) -> None:
+        for ch in self.channels.values():
+            ch.close()
+        self.channels.clear()
+
+
+def self_test(comm: XgmiComm) -> bool:
+    """Collective sanity check run once at start-up: an all-gather and an all-reduce of
+    rank-dependent data, verified on the host; every rank learns whether ALL passed."""
+    dev = comm.device
+    ok = True
+    try:
+        W, r = comm.world, comm.rank
+        x = torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * r
+        out = torch.empty(W * 1024, dtype=torch.float32, device=dev)
+        ch = XgmiChannel(comm.rank, W, 4096, dev, comm.group, timeout_s=5.0)
+        ch.all_gather([(x, out)])
+        want = torch.cat([torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * k for k in range(W)])
+        y = x.clone()
+        ch.all_reduce([y])
+        torch.cuda.synchronize(dev)
+        ok = (ch.error() == 0 and torch.equal(out, want)
+              and torch.equal(y, W * torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * sum(range(W))))
+        ch.close()
+    except Exception:
+        ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
+    return bool(flag.item())
+
+
+def enabled_by_env() -> str:
+    """``CSA_XGMI``: ``auto`` (default: on for RCCL jobs after a passing self-test),
+    ``1`` (on, fail loudly), ``0`` (RCCL only)."""
+    return os.environ.get("CSA_XGMI", "auto").lower()

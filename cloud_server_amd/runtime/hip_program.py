@@ -210,7 +210,7 @@ class HipProgram:
             return
         self.lr_side.wait_stream(torch.cuda.current_stream(self.e.device))
         with torch.cuda.stream(self.lr_side):
-            self.e.sync.all_gather_rows_many([(u.lr_src, u.lr_x) for u in self.lr_units])
+            self.e.sync.all_gather_rows_many([(u.lr_src, u.lr_x) for u in self.lr_units], tag="lr_x")
 
     def _lowrank_wgrads(self) -> None:
         """Once every lowrank unit's output gradient is final: gather them and form the
@@ -219,7 +219,7 @@ class HipProgram:
         self.lr_side.wait_stream(torch.cuda.current_stream(self.e.device))
         with torch.cuda.stream(self.lr_side):
             ss = self.lr_side.cuda_stream
-            self.e.sync.all_gather_rows_many([(u.dy.view(B, -1), u.lr_dy) for u in self.lr_units])
+            self.e.sync.all_gather_rows_many([(u.dy.view(B, -1), u.lr_dy) for u in self.lr_units], tag="lr_dy")
             for u in self.lr_units:
                 lp = u.layer
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
@@ -624,7 +624,7 @@ class HipProgram:
         if self.overlap:
             main.wait_stream(self.side)
         elif e.ctx.enabled and e.sync.strategy == "lowrank":
-            e.sync.allreduce_ranges(e.flat_grad, self.lr_ranges)
+            e.sync.allreduce_ranges(e.flat_grad, self.lr_ranges, tag="lr_rem")
             if self.lr_units:
                 main.wait_stream(self.lr_side)
         else:

@@ -34,11 +34,13 @@ def pg():
     dist.destroy_process_group()
 
 
-def test_overlap_buckets_match_single_gpu(pg):
+def test_overlap_buckets_match_single_gpu(pg, monkeypatch):
+    monkeypatch.setenv("CSA_XGMI", "1")      # force the peer-buffer path (world 1: RCCL is a no-op)
     cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdamOptimizer", learning_rate=1e-3))
     ds = synthetic_mnist(2000, seed=0)
     ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
     a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip")
+    assert a.sync.xgmi is not None, a.sync.xgmi_reason      # buckets on the xGMI peer path
     assert a.program.overlap and len(a.program.bucket_at) >= 2, a.program.bucket_at
     spans = sorted(a.program.bucket_at.values())
     assert spans[0][0] == 0 and spans[-1][1] == a.flat.numel()
@@ -50,14 +52,16 @@ def test_overlap_buckets_match_single_gpu(pg):
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
 
 
-def test_lowrank_strategy_matches_single_gpu(pg):
+def test_lowrank_strategy_matches_single_gpu(pg, monkeypatch):
     """``lowrank`` DP: dense weight gradients from all-gathered GEMM inputs / output
     gradients (K = world·B) on a side stream, the rest all-reduced — captured in the HIP
     graph; world 1 must reproduce the single-GPU step."""
     cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdamOptimizer", learning_rate=1e-3))
     ds = synthetic_mnist(2000, seed=0)
     ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    monkeypatch.setenv("CSA_XGMI", "1")
     a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy="lowrank")
+    assert a.sync.xgmi is not None, a.sync.xgmi_reason
     assert a.backend == "hip", a.fallback_reason
     names = [u.layer.name for u in a.program.lr_units]
     assert len(names) == 2, names                      # fc1 (materialised BN input) and fc2
@@ -69,6 +73,33 @@ def test_lowrank_strategy_matches_single_gpu(pg):
     for _ in range(20):
         a.step(); b.step()
     torch.cuda.synchronize()
+    assert a.sync._choice["lr_x"] is not None and a.sync._choice["lr_dy"] is not None, a.sync._choice
+    a.sync.check()
     for n in a.model.state.shapes:          # the two flat layouts differ: compare by name
+        torch.testing.assert_close(a.model.state.view(n, a.flat), b.model.state.view(n, b.flat),
+                                   rtol=2e-3, atol=2e-5)
+
+
+def test_collective_autotune_records_both_paths(pg, monkeypatch):
+    """CSA_XGMI=auto: each call site is timed on both paths (HIP graphs of 10 calls) at
+    first use and the choice is recorded; training still matches the single-GPU step."""
+    monkeypatch.setenv("CSA_XGMI", "auto")
+    # Adam: the step is scale-free, so 20 steps of two summation orders stay within
+    # tolerance (SGD/Adagrad at lr 1e-2 drift ~1e-3 between ANY two layouts, allreduce too:
+    # scripts/diag_lowrank_opt.py)
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdamOptimizer", learning_rate=1e-3))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy="lowrank")
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for _ in range(20):
+        a.step(); b.step()
+    torch.cuda.synchronize()
+    a.sync.check()
+    assert set(a.sync.xgmi_tuning) >= {"lr_x", "lr_dy"}, a.sync.xgmi_tuning
+    for v in a.sync.xgmi_tuning.values():
+        assert v["xgmi_us"] > 0 and v["rccl_us"] > 0
+    print("collective tuning (world 1):", a.sync.xgmi_tuning)
+    for n in a.model.state.shapes:          # lowrank uses the dense-last layout: compare by name
         torch.testing.assert_close(a.model.state.view(n, a.flat), b.model.state.view(n, b.flat),
                                    rtol=2e-3, atol=2e-5)
