@@ -109,6 +109,22 @@ def act_fwd(x: torch.Tensor, sp: ActSpec) -> torch.Tensor:
     return torch.sigmoid(x)
 
 
+def _global_moments(h: torch.Tensor, dims) -> "tuple[torch.Tensor, torch.Tensor]":
+    """Biased mean / variance of ``h`` over ``dims`` AND over every rank of the default
+    process group: one all-reduce of [sum, sum of squares, count] (2C + 1 floats)."""
+    import torch.distributed as dist
+    from torch.distributed.nn.functional import all_reduce
+    C = h.shape[-1]
+    n = torch.full((1,), float(h.numel() // C), dtype=h.dtype, device=h.device)
+    st = torch.cat([h.sum(dim=dims), (h * h).sum(dim=dims), n])
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        st = all_reduce(st)
+    cnt = st[2 * C]
+    mean = st[:C] / cnt
+    var = (st[C:2 * C] / cnt - mean * mean).clamp_min(0.0)
+    return mean, var
+
+
 class DigitNet(nn.Module):
     """Eager model over a ``FlatState``.  ``forward(x)`` takes NHWC [B,28,28,1] or [B,784]."""
 
@@ -118,6 +134,11 @@ class DigitNet(nn.Module):
         self.plan = plan
         self.bn_mode = bn_mode
         self.bn_momentum = bn_momentum
+        # SyncBN: under data parallelism the reference's single worker
+        # normalised over its whole batch; with sync_bn the per-channel {sum, sum of
+        # squares, count} are all-reduced (autograd-aware, so the backward statistics are
+        # global too) and every replica normalises with the GLOBAL batch statistics
+        self.sync_bn = False
         self.state = FlatState(plan.param_shapes(dense_last), device=device, pad_multiple=pad_multiple)
         init_params(plan, self.state, seed)
         self.flat = nn.Parameter(self.state.buffer)
@@ -170,7 +191,13 @@ class DigitNet(nn.Module):
             dims = tuple(range(h.dim() - 1))
             scale, offset = self.p(f"{lp.name}.scale"), self.p(f"{lp.name}.offset")
             rm, rv = getattr(self, f"bn{lp.index}_mean"), getattr(self, f"bn{lp.index}_var")
-            if use_batch_stats:
+            if use_batch_stats and self.sync_bn and self.training:
+                mean, var = _global_moments(h, dims)
+                with torch.no_grad():
+                    m = self.bn_momentum
+                    rm.mul_(1 - m).add_(mean.detach(), alpha=m)
+                    rv.mul_(1 - m).add_(var.detach(), alpha=m)
+            elif use_batch_stats:
                 mean = h.mean(dim=dims)
                 var = h.var(dim=dims, unbiased=False)   # tf.nn.moments: biased
                 if self.training:

@@ -306,6 +306,7 @@ class TrainConfig:
     ckpt_every: int = 500                  # replaces Supervisor save_model_secs=60 (:391)
     bn_mode: str = "running"               # "batch" = reference quirk 3
     compat_adagrad: bool = False           # True = reference quirk 1 (Adagrad 1e-4)
+    sync_bn: bool = False                  # DP: BatchNorm statistics over the GLOBAL batch
     seed: int = 0
 
     @property
@@ -360,6 +361,7 @@ def parse_train_config(cfg: Union[str, bytes, Dict[str, Any]]) -> TrainConfig:
         ckpt_every=_as_int(ext.get("ckpt_every", 500), "ckpt_every"),
         bn_mode=str(ext.get("bn_mode", "running")),
         compat_adagrad=bool(ext.get("compat_adagrad", False)),
+        sync_bn=str(ext.get("sync_bn", False)).lower() in ("1", "true", "yes"),
         seed=_as_int(ext.get("seed", 0), "seed"),
     )
     if tc.iter < 0:

@@ -243,6 +243,17 @@ class GradSync:
         for lo, hi in ranges:
             dist.all_reduce(flat[lo:hi])
 
+    def allreduce_tensors(self, tensors, tag: str) -> None:
+        """In-place SUM of small fp32 tensors across ranks (SyncBN statistics slabs)."""
+        if not self.ctx.enabled:
+            return
+        ch = self._xg_channel(tag, list(tensors)) if len(tensors) <= 8 else None
+        if ch is not None:
+            ch.all_reduce(list(tensors))
+            return
+        for t in tensors:
+            dist.all_reduce(t)
+
     def broadcast_params(self, flat_param: torch.Tensor) -> None:
         """Initial sync from rank 0 (reference: chief runs init_op, construct_distribute.py:379)."""
         if self.ctx.enabled:

@@ -71,6 +71,7 @@ class TrainEngine:
         self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world,
                                            dense_last=strategy == "lowrank")
         self.model.train()
+        self.model.sync_bn = bool(cfg.sync_bn and self.ctx.enabled)
         self.flat = self.model.flat.data
         self.flat_grad = torch.zeros_like(self.flat)
         self.model.flat.grad = self.flat_grad

@@ -97,6 +97,12 @@ class HipProgram:
             raise Unsupported("HIP program needs a GPU device")
         self.B = eng.cfg.batch_size
         self.model = eng.model
+        # SyncBN under DP: forward {sum, sumsq} slabs and backward {sum dz, sum dz*xhat}
+        # slabs are all-reduced between their producer and consumer launches, counts
+        # become global, and the BN parameter gradients (formed from the GLOBAL backward
+        # sums) are scaled by 1/world before the gradient all-reduce adds them up again
+        self.sync_bn = bool(eng.model.sync_bn)
+        self.W = eng.ctx.world if self.sync_bn else 1
         self.views = eng.model.state.views(eng.flat)
         self.gviews = eng.model.state.views(eng.flat_grad)
         self._lower()
@@ -335,7 +341,7 @@ class HipProgram:
                 nslab = self.lib.csa_conv_fwd_nslab(self._conv_geom(src.layer, B), self._pool_geom(src))
                 tf.slab = torch.zeros(nslab, 2, src.y.shape[3], **f32)
                 tf.nslab = nslab
-                tf.count = float(B * ph * pw)
+                tf.count = float(B * ph * pw * self.W)
                 # backward slab is produced by THIS unit's dgrad
                 C = src.y.shape[3]
                 if u.kind == "dense":
@@ -498,6 +504,8 @@ class HipProgram:
                     K.ptr(u.y), K.ptr(u.argmax), K.ptr(oslab),
                     self._conv_geom(lp, B), self._pool_geom(u), *bn, in_act, in_alpha,
                     _act_id(u.act), _alpha(u.act), K.ptr(cur) if raw else None, st), "conv_fwd")
+                if oslab is not None and self.sync_bn:
+                    e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
             else:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
                 if u.xt is not None:
@@ -533,6 +541,10 @@ class HipProgram:
             bn = self._bn_args(tf)
             in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
             prev = self.units[k - 1] if k > 0 else None
+            if self.sync_bn and k + 1 < len(self.units) and self.units[k + 1].in_tf.has_bn:
+                # unit k+1's dgrad produced its input transform's backward slab; this
+                # unit's route consumes it: make it the global sum first
+                e.sync.allreduce_tensors([self.units[k + 1].in_tf.bwd_slab], tag=f"bnb{k + 1}")
             if u.kind == "dense":
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
                 if (prev is not None and u not in self.lr_units and not self.wsplit
@@ -564,6 +576,7 @@ class HipProgram:
                 next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
                 need_route = next_tf.has_bn or u.act is not None or u.pool is not None
                 if need_route and prev is not None and self._conv_bwd_route_fused(u, prev, next_tf, st):
+                    self._sync_bn_param_grads(next_tf)
                     self._grad_ready(k)          # route + input gradient + weight gradient: one launch
                     continue
                 if need_route:
@@ -588,6 +601,7 @@ class HipProgram:
                         _act_id(u.act), _alpha(u.act), *nbn, K.ptr(next_tf.bwd_slab), next_tf.bwd_nslab,
                         K.ptr(dsc), K.ptr(dof), K.ptr(rm), K.ptr(rv), float(self.model.bn_momentum), st),
                         "route_bwd")
+                    self._sync_bn_param_grads(next_tf)
                     dc = u.dc
                 else:
                     dc = u.dy
@@ -641,6 +655,11 @@ class HipProgram:
         else:
             g += [1, 1, 1, 1, 0, 0]
         return g
+
+    def _sync_bn_param_grads(self, tf: Transform) -> None:
+        if self.sync_bn and tf.has_bn and self.W > 1:
+            for p in ("scale", "offset"):
+                self.gviews[f"{tf.norm.name}.{p}"].mul_(1.0 / self.W)
 
     def _conv_bwd_route_fused(self, u: Unit, prev: Unit, next_tf: Transform, st) -> bool:
         """Route backward (BN + act backward + pool routing) fused into the conv unit's

@@ -164,3 +164,51 @@ def test_distributed_job_rank0_writes_and_ps_resume(tmp_path):
     assert (full[:, :half] > 0).all() and (full[:, half:] > 0).all()   # both ranks' shards saved
     out = _spawn(_job, 2, mdir, dict(cfg, iter=16))
     assert out == {0: 16, 1: 16}
+
+
+BN_CFG = {"iter": 4, "learning_rate": 0.01, "ratio": 0.8, "loss_name": "entropy",
+          "optimizer_name": "AdamOptimizer", "options": {"batch_size": 6, "sync_bn": True},
+          "net_config": {"middle_layer": [{"layer": "conv", "filter": [3, 3, 4], "isBias": "True"},
+                                          {"layer": "norm"},
+                                          {"layer": "active", "active_func": "relu"},
+                                          {"layer": "pool"},
+                                          {"layer": "connect", "hidden": 16}]}}
+
+
+def _sync_bn(rank, world, port, out):
+    """SyncBN: each rank normalises its half of the batch with the GLOBAL statistics; the
+    forward equals the single-process full batch and the all-reduced mean gradient
+    equals the full-batch gradient."""
+    import torch.distributed as dist
+    from cloud_server_amd.models.cnn import build_model, loss_fn
+    _init(rank, world, port)
+    cfg = parse_train_config(BN_CFG)
+    assert cfg.sync_bn
+    g = torch.Generator().manual_seed(7)
+    X = torch.rand(12, 28, 28, 1, generator=g)
+    Y = torch.randint(0, 10, (12,), generator=g)
+    ref = build_model(cfg)
+    ref.train()
+    lr = ref(X)
+    loss_fn("entropy", lr, Y).backward()
+    net = build_model(cfg)
+    net.train()
+    net.sync_bn = True
+    sl = slice(rank * 6, (rank + 1) * 6)
+    logits = net(X[sl])
+    (loss_fn("entropy", logits, Y[sl]) / world).backward()
+    dist.all_reduce(net.flat.grad)
+    rm = [n for n, _ in net.named_buffers() if n.endswith("_mean")][0]
+    out[rank] = (torch.allclose(logits, lr[sl].detach(), atol=1e-5),
+                 float((net.flat.grad - ref.flat.grad).abs().max()),
+                 float(ref.flat.grad.abs().max()),
+                 torch.allclose(getattr(net, rm), getattr(ref, rm), atol=1e-6))
+
+
+def test_sync_bn_equals_full_batch():
+    out = _spawn(_sync_bn, 2)
+    for r in range(2):
+        fwd_ok, gdiff, gmax, run_ok = out[r]
+        assert fwd_ok, r
+        assert gdiff <= 1e-5 * max(1.0, gmax), (r, gdiff, gmax)
+        assert run_ok, r
