@@ -103,7 +103,16 @@ class GradSync:
         if choice is not None and self.xgmi_mode == "auto":
             xg_us, rc_us = self._time_paths(ch, srcs, dsts)
             self.xgmi_tuning[tag] = {"bytes": nbytes, "xgmi_us": round(xg_us, 2), "rccl_us": round(rc_us, 2)}
-            if not xg_us < rc_us:
+            # a peer wait that timed out during the timing poisons the channel (and would
+            # make it look fast): every rank then drops it and stays on RCCL
+            healthy = torch.tensor([0 if ch.error() else 1], dtype=torch.int32, device=self.ctx.device)
+            dist.all_reduce(healthy, op=dist.ReduceOp.MIN)
+            if not healthy.item():
+                self.xgmi_tuning[tag]["error"] = "peer wait timed out"
+                ch.close()
+                del self.xgmi.channels[tag]
+                choice = None
+            elif not xg_us < rc_us:
                 choice = None
         self._choice[tag] = choice
         return choice

@@ -123,6 +123,7 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
             # reference: the accuracy logged for step s is the batch of step s evaluated
             # with the pre-update weights — exactly this step's forward pass
             eng.sync_device()
+            eng.sync.check()   # a timed-out peer-buffer collective fails the job
             now = time.perf_counter()
             n = eng.host_step - int_start
             step_time = (now - t_int) / max(n, 1)

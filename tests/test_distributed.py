@@ -68,7 +68,7 @@ def _collectives(rank, world, port, out):
     rows = torch.full((3, 5), float(rank))
     allrows = torch.zeros(3 * world, 5)
     ga.all_gather_rows(rows, allrows)
-    ok &= torch.equal(allrows[3:], torch.ones(3, 5)) and torch.equal(allrows[:3], torch.zeros(3, 5))
+    ok &= all(torch.equal(allrows[3 * r:3 * r + 3], torch.full((3, 5), float(r))) for r in range(world))
     # lowrank identity: sum_r X_r^T dY_r == X_all^T dY_all with rank-major gathered rows
     gen = torch.Generator().manual_seed(rank)
     x, dy = torch.randn(4, 6, generator=gen), torch.randn(4, 3, generator=gen)
@@ -133,6 +133,23 @@ def test_ps_strategy_matches_allreduce():
     a = _spawn(_train, 2, "allreduce", 5)
     b = _spawn(_train, 2, "ps", 5)
     torch.testing.assert_close(b[0], b[1], rtol=0, atol=0)
+    n = min(a[0].numel(), b[0].numel())
+    torch.testing.assert_close(a[0][:n], b[0][:n], rtol=1e-5, atol=1e-6)
+
+
+def test_collectives_world4():
+    """More ranks than the 2-rank default: bucket, reduce-scatter, gather and range
+    collectives at world 4 (the 8-GPU path, rehearsed on CPU)."""
+    out = _spawn(_collectives, 4)
+    assert out == {r: True for r in range(4)}
+
+
+def test_ps_matches_allreduce_world4():
+    a = _spawn(_train, 4, "allreduce", 3)
+    b = _spawn(_train, 4, "ps", 3)
+    for r in range(1, 4):
+        torch.testing.assert_close(a[0], a[r], rtol=0, atol=0)
+        torch.testing.assert_close(b[0], b[r], rtol=0, atol=0)
     n = min(a[0].numel(), b[0].numel())
     torch.testing.assert_close(a[0][:n], b[0][:n], rtol=1e-5, atol=1e-6)
 
