@@ -95,7 +95,12 @@ class GradSync:
         if torch.cuda.is_current_stream_capturing():
             return None                  # undecided inside capture: RCCL (same on all ranks)
         nbytes = sum(t.numel() * t.element_size() for t in srcs)
-        ch = self.xgmi.channel(tag, nbytes)
+        try:
+            ch = self.xgmi.channel(tag, nbytes)
+        except RuntimeError as exc:      # raised on every rank together (collective agreement)
+            self.xgmi_tuning[tag] = {"bytes": nbytes, "error": str(exc)}
+            self._choice[tag] = None
+            return None
         ok = ch.fits(srcs) and (dsts is None or all(d.is_contiguous() and d.data_ptr() % 16 == 0 for d in dsts))
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)

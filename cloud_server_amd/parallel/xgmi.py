@@ -49,20 +49,29 @@ class XgmiChannel:
         nblk = self.lib.csa_xgmi_max_blocks()
         sizes = (2 * world * self.slot_bytes, 2 * nblk * 8 * 4)
         self._local: List[int] = []
-        handles: List[bytes] = []
+        self._opened: List[int] = []
+        # every failure is agreed on collectively (all ranks raise together), so a rank
+        # that cannot allocate or map never leaves its peers inside a collective
+        handles: Optional[List[bytes]] = []
         with torch.cuda.device(device):
-            for n in sizes:
-                p = C.c_void_p()
-                h = C.create_string_buffer(hb)
-                rc = self.lib.csa_xgmi_alloc(n, C.byref(p), h)
-                if rc:
-                    raise RuntimeError(f"xgmi alloc failed ({rc})")
-                self._local.append(p.value)
-                handles.append(h.raw)
+            try:
+                for n in sizes:
+                    p = C.c_void_p()
+                    h = C.create_string_buffer(hb)
+                    rc = self.lib.csa_xgmi_alloc(n, C.byref(p), h)
+                    if rc:
+                        raise RuntimeError(f"xgmi alloc failed ({rc})")
+                    self._local.append(p.value)
+                    handles.append(h.raw)
+            except Exception:
+                handles = None
             allh: List[Optional[List[bytes]]] = [None] * world
             dist.all_gather_object(allh, handles, group=group)
-            self._opened: List[int] = []
+            if any(h is None for h in allh):
+                self.close()
+                raise RuntimeError("xgmi: a rank could not allocate its peer buffers")
             ptrs: List[List[int]] = [[], []]
+            ok = True
             for r in range(world):
                 for k in range(2):
                     if r == rank:
@@ -71,9 +80,17 @@ class XgmiChannel:
                     p = C.c_void_p()
                     rc = self.lib.csa_xgmi_open(C.create_string_buffer(allh[r][k], hb), C.byref(p))
                     if rc:
-                        raise RuntimeError(f"xgmi open of rank {r}'s buffer failed ({rc})")
+                        ok = False
+                        ptrs[k].append(0)
+                        continue
                     self._opened.append(p.value)
                     ptrs[k].append(p.value)
+            oks: List[Optional[bool]] = [None] * world
+            dist.all_gather_object(oks, ok, group=group)
+            if not all(oks):
+                self.close()
+                raise RuntimeError(f"xgmi: mapping a peer buffer failed on rank(s) "
+                                   f"{[r for r, o in enumerate(oks) if not o]}")
         self._bufs = (C.c_void_p * world)(*ptrs[0])
         self._flags = (C.c_void_p * world)(*ptrs[1])
         self.state = torch.zeros(4, dtype=torch.int32, device=device)   # seq, done, err, pad
@@ -113,7 +130,7 @@ class XgmiChannel:
             raise RuntimeError("xGMI collective timed out waiting for a peer (channel poisoned)")
 
     def close(self) -> None:
-        if not self._local:
+        if not self._local and not self._opened:
             return
         torch.cuda.synchronize(self.device)
         for p in self._opened:
