@@ -18,6 +18,9 @@ import time
 from typing import Any, Dict, List, Optional
 
 
+_TOPOLOGY: List[Any] = []   # [src][dst] link type of the last _gpus() scan (None on the diagonal)
+
+
 def _gpus() -> List[Dict[str, Any]]:
     out: List[Dict[str, Any]] = []
     try:
@@ -42,7 +45,32 @@ def _gpus() -> List[Dict[str, Any]]:
                     h, amdsmi.AmdSmiTemperatureType.EDGE, amdsmi.AmdSmiTemperatureMetric.CURRENT)
             except Exception:
                 pass
+            # xGMI: per-link up/down status and the data-plane link metrics (the fabric the
+            # peer-buffer collectives of parallel/xgmi.py and RCCL run over)
+            for key, fn in (("xgmi_link_status", "amdsmi_get_gpu_xgmi_link_status"),
+                            ("xgmi_info", "amdsmi_get_xgmi_info"),
+                            ("link_metrics", "amdsmi_get_link_metrics")):
+                try:
+                    g[key] = getattr(amdsmi, fn)(h)
+                except Exception:
+                    pass
             out.append(_jsonable(g))
+        handles = amdsmi.amdsmi_get_processor_handles()
+        if len(handles) > 1 and out:
+            topo = []
+            for i, hs in enumerate(handles):
+                row = []
+                for j, hd in enumerate(handles):
+                    if i == j:
+                        row.append(None)
+                        continue
+                    try:
+                        lt = amdsmi.amdsmi_topo_get_link_type(hs, hd)
+                        row.append(_jsonable(lt))
+                    except Exception:
+                        row.append(None)
+                topo.append(row)
+            _TOPOLOGY[:] = topo
     finally:
         try:
             amdsmi.amdsmi_shut_down()
@@ -82,6 +110,7 @@ def node_status(jobs: Optional[List[Dict[str, Any]]] = None) -> Dict[str, Any]:
         "System Info": {"Operating System": platform.system(), "Kernel Version": platform.release(),
                         "Architecture": platform.machine(), "Python": platform.python_version()},
         "GPUs": gpus,
+        "Topology": list(_TOPOLOGY),
         "Non-terminated Pods": [
             {"Name": f"job-{j['id']}", "Model": j.get("model"), "State": j.get("state"), "GPU": j.get("gpu")}
             for j in (jobs or [])],

@@ -90,3 +90,15 @@ def test_job_manager_process_executor_on_gpu(tmp_path):
         assert st["gpu"] == "0" and st["progress"]["backend"] == "hip"
     finally:
         jm.shutdown()
+
+
+def test_node_status_reports_gpus_on_device():
+    """GET /runtime/kubernetes/ analogue on a real node: amdsmi sees the MI355X and the
+    report carries its VRAM and (where the driver exposes them) xGMI link fields."""
+    from cloud_server_amd.runtime.devices import node_status
+    st = node_status([])
+    assert st["Capacity"]["amd.com/gpu"] != "0", st["Conditions"]
+    g = st["GPUs"][0]
+    assert "vram" in g or "asic" in g, sorted(g)
+    assert isinstance(st["Topology"], list)
+    print("gpu0 fields:", sorted(g))
