@@ -13,11 +13,14 @@ Route table (reference views in parentheses):
            POST /construct/construction/<m>/<datatype>/ (ConstructView)
            POST /construct/inference/<m>/ (InferenceView)
   runtime  GET /runtime/train/<m>/<iter>/ (TensorResultView)  GET /runtime/kubernetes/
+  browser  /login/ /logout/ /password_change/(done/) /password_reset/(done/)
+           /reset/<uid>/<token>/ /reset/done/ (django.contrib.auth.urls), /admin/ (api/html_auth.py)
   documented-only in API.md, implemented here: /generation/options/list|next,
            /generation/generate, /generation/run/basic|details|runtime|stop|pause,
            /generation/restore/<job>/, /models/, /models/<m>/, /models/compare/
 
-Auth: ``Authorization: Token <key>`` (rest_framework.authtoken) or HTTP Basic.  Unlike
+Auth: ``Authorization: Token <key>`` (rest_framework.authtoken), HTTP Basic, or the
+``sessionid`` cookie set by the HTML ``/login/`` form (SessionAuthentication).  Unlike
 the reference, every data/model route requires authentication and checks ownership
 (quirk 8: DELETE /data/<pk>/ had no owner check; "auth only" routes let anonymous users
 write into NJUCloud/None/), names are validated and ``relative_path`` cannot escape the
@@ -40,6 +43,7 @@ from typing import Any, Dict, List, Optional
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, Response
 
+from . import html_auth
 from ..config import Settings, get_settings
 from ..models.dsl import ConfigError, parse_train_config, spec_to_dict
 from ..models.options import CATALOG, get_options
@@ -118,6 +122,9 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
             user = db.find_user(username=u)
             if user and check_password(p, user["password"]):
                 return user
+        sid = request.cookies.get(html_auth.COOKIE)     # browser session from /login/
+        if sid:
+            return db.user_for_token(sid, settings.token_ttl_s)
         return None
 
     def need_user(request: Request):
@@ -142,6 +149,8 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, f"{time.time():.6f}.eml"), "w", encoding="utf-8") as f:
             f.write(f"To: {to}\nSubject: {subject}\n\n{body}\n")
+
+    html_auth.install(app, db, settings, outbox, validate_password, form, current_user)
 
     # ================================================================== /rest-auth/
     @app.post("/rest-auth/login/")

@@ -23,7 +23,7 @@ import secrets
 import sqlite3
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 SCHEMA = """
 CREATE TABLE IF NOT EXISTS users (
@@ -134,6 +134,13 @@ class Database:
 
     def tx(self):
         return self._Tx(self.conn())
+
+    def table_counts(self) -> List[Tuple[str, int]]:
+        """(table, row count) of every platform table (the read-only admin index)."""
+        c = self.conn()
+        names = [r[0] for r in c.execute(
+            "SELECT name FROM sqlite_master WHERE type='table' AND name NOT LIKE 'sqlite_%' ORDER BY name")]
+        return [(n, int(c.execute(f'SELECT COUNT(*) FROM "{n}"').fetchone()[0])) for n in names]
 
     # ------------------------------------------------------------------ users
     def create_user(self, username: str, password: str, email: str = "", is_staff: bool = False) -> int:

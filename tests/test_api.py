@@ -290,3 +290,43 @@ def test_url_dataset_and_url_training(client, tmp_path):
     assert client.app.state.jobs.wait(jid, 300) == "done"
     res = client.get("/runtime/train/mu/20/", headers=h).json()
     assert len(res["every_result"]) == 2 and "final_accuracy" in res
+
+
+def test_browser_auth_pages_and_admin(client):
+    """django.contrib.auth.urls + admin analogues: form login sets a session cookie that
+    the JSON API accepts; password change / reset by form; /admin/ is staff-only."""
+    db = client.app.state.db
+    uid = db.create_user("webu", PW, "webu@x.org")
+    db.create_user("boss", PW, "boss@x.org", is_staff=True)
+    assert "<form" in client.get("/login/").text
+    r = client.post("/login/", data={"username": "webu", "password": "nope"}, follow_redirects=False)
+    assert r.status_code == 200 and "correct username" in r.text
+    r = client.post("/login/?next=//evil.example/", data={"username": "webu", "password": PW},
+                    follow_redirects=False)
+    assert r.status_code == 302 and r.headers["location"] == "/" and "sessionid" in r.cookies
+    assert client.get("/rest-auth/user/").json()["username"] == "webu"     # session auth on the API
+    assert client.get("/admin/", follow_redirects=False).status_code == 302  # not staff
+    new = PW + "-2"
+    r = client.post("/password_change/", data={"old_password": PW, "new_password1": new,
+                                               "new_password2": new}, follow_redirects=False)
+    assert r.status_code == 302 and r.headers["location"] == "/password_change/done/"
+    assert "Logged out" in client.get("/logout/").text
+    client.cookies.clear()
+    assert client.get("/rest-auth/user/").status_code == 401
+    assert client.get("/password_change/", follow_redirects=False).status_code == 302
+    # reset by e-mail link
+    r = client.post("/password_reset/", data={"email": "webu@x.org"}, follow_redirects=False)
+    assert r.headers["location"] == "/password_reset/done/"
+    box = os.path.join(client.settings.storage_root, "outbox")
+    mail = open(os.path.join(box, sorted(os.listdir(box))[-1])).read()
+    link = [w for w in mail.split() if w.startswith("/reset/")][0]
+    newer = PW + "-3"
+    r = client.post(link, data={"new_password1": newer, "new_password2": newer}, follow_redirects=False)
+    assert r.status_code == 302 and r.headers["location"] == "/reset/done/"
+    assert client.post(link, data={"new_password1": newer, "new_password2": newer}).status_code == 400  # one-shot
+    assert client.post("/rest-auth/login/", data={"username": "webu", "password": newer}).status_code == 200
+    # staff admin index
+    client.post("/login/", data={"username": "boss", "password": PW})
+    r = client.get("/admin/")
+    assert r.status_code == 200 and "Site administration" in r.text and "users" in r.text
+    assert uid
