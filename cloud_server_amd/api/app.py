@@ -30,18 +30,19 @@ from __future__ import annotations
 
 import base64
 import contextlib
+import hmac
 import io
 import json
 import mimetypes
 import os
 import shutil
 import time
-import urllib.request
 import zipfile
 from typing import Any, Dict, List, Optional
 
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, Response
+from starlette.concurrency import run_in_threadpool
 
 from . import html_auth
 from ..config import Settings, get_settings
@@ -53,6 +54,7 @@ from ..runtime.jobs import JobManager
 from ..runtime.trainer import METRICS, RESULT, STATUS, read_train_results
 from ..serve.inference import FAIL_NO_MODEL, InferenceService
 from ..store.db import FILE_TYPES, Database, check_password
+from ..utils import net
 from ..utils.files import csv_to_json, dir_tree, safe_join, timestamped_name, valid_name
 from .forms import FormError, read_form
 
@@ -110,7 +112,9 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
     _install_metrics(app, db)
 
     # ------------------------------------------------------------------ auth helpers
-    def current_user(request: Request) -> Optional[Dict[str, Any]]:
+    def current_user(request: Request, csrf_verified: bool = False) -> Optional[Dict[str, Any]]:
+        """Token / Basic / session-cookie auth.  ``csrf_verified``: the caller (an HTML
+        form handler) already checked the form's CSRF field."""
         h = request.headers.get("authorization", "")
         if h.lower().startswith("token "):
             return db.user_for_token(h.split(None, 1)[1].strip(), settings.token_ttl_s)
@@ -124,6 +128,13 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
                 return user
         sid = request.cookies.get(html_auth.COOKIE)     # browser session from /login/
         if sid:
+            # SessionAuthentication semantics: a cookie-authenticated unsafe request must
+            # carry the CSRF token (double submit: X-CSRFToken header == csrftoken cookie)
+            if not csrf_verified and request.method not in ("GET", "HEAD", "OPTIONS", "TRACE"):
+                cookie = request.cookies.get(html_auth.CSRF_COOKIE, "")
+                header = request.headers.get("x-csrftoken", "")
+                if not cookie or not hmac.compare_digest(cookie, header):
+                    return None
             return db.user_for_token(sid, settings.token_ttl_s)
         return None
 
@@ -263,8 +274,9 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         pe = validate_password(p1, u["username"], u["email"])
         if pe:
             return J({"new_password2": pe}, 400)
-        db.set_password(u["id"], p1)
-        return J({"detail": "New password has been saved."})
+        db.set_password(u["id"], p1)        # revokes every session/token of the user ...
+        # ... and this client gets a fresh one (Django's update_session_auth_hash)
+        return J({"detail": "New password has been saved.", "key": db.token_for(u["id"])})
 
     @app.get("/rest-auth/user/")
     async def user_get(request: Request):
@@ -368,7 +380,7 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
                 else:
                     stem = os.path.splitext(fname)[0]
                     dest = os.path.join(abs_dir, stem)
-                    _extract_zip(up.data, dest)
+                    await run_in_threadpool(_extract_zip, up.data, dest)
                     rel = os.path.join(rel_dir, stem)
             else:
                 if not settings.allow_url_fetch:
@@ -376,18 +388,19 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
                 urls = [x.strip() for x in str(f.get("url", "")).split(";") if x.strip()]
                 if not urls:
                     return J({"message": "error"}, 400)
+                try:
+                    for url in urls:
+                        net.check_url(url)       # http(s) only: refuse the whole request
+                except net.FetchRefused as exc:
+                    return J({"message": "error", "detail": str(exc)}, 400)
                 stem = timestamped_name("url")
                 dest = os.path.join(abs_dir, stem)
                 os.makedirs(dest, exist_ok=True)
-                for url in urls:
-                    if not url.split(":", 1)[0].lower() in ("http", "https", "ftp", "file"):
-                        continue
-                    name = os.path.basename(url.rstrip("/")) or "download"
-                    try:
-                        with urllib.request.urlopen(url, timeout=60) as r, open(os.path.join(dest, name), "wb") as out:
-                            shutil.copyfileobj(r, out)
-                    except Exception:
-                        pass          # reference: log and continue with the other URLs
+                errors = await run_in_threadpool(_fetch_urls, urls, dest, settings.url_allow_private,
+                                                 max_bytes)
+                if errors and len(errors) == len(urls):
+                    shutil.rmtree(dest, ignore_errors=True)
+                    return J({"message": "error", "detail": "; ".join(errors)}, 400)
                 rel = os.path.join(rel_dir, stem)
         except (zipfile.BadZipFile, OSError, ValueError):
             return J({"message": "error"}, 500)
@@ -475,7 +488,8 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
             if ops:
                 if not os.path.exists(tag):
                     return J({"message": "error", "detail": "upload tag.json first"}, 500)
-                pipeline.run(os.path.join(mdir, "data"), tag, ops, backend=settings.preprocess_backend)
+                await run_in_threadpool(pipeline.run, os.path.join(mdir, "data"), tag, ops,
+                                        backend=settings.preprocess_backend)
         except Exception as exc:
             return J({"message": "error", "detail": str(exc)}, 500)
         return J({"message": "success"})
@@ -558,7 +572,7 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         with open(os.path.join(idir, os.path.basename(up.filename) or "image"), "wb") as out:
             out.write(up.data)
         prep = str(request.query_params.get("prep", f.get("prep", "reference")))
-        return J(infer.predict(mdir, up.data, prep=prep))
+        return J(await infer.predict_async(mdir, up.data, prep=prep))
 
     # ================================================================== /runtime/
     @app.get("/runtime/train/{model}/{iters}/")
@@ -848,6 +862,21 @@ def _install_demo(app: FastAPI, db: Database, need_user, current_user, form) -> 
         except ValueError as exc:
             return J({"detail": f"invalid field {exc}"}, 400)
         return J(bill_json(db.get_bill(pk)))
+
+
+def _fetch_urls(urls: List[str], dest: str, allow_private: bool, max_bytes: int) -> List[str]:
+    """Sequential downloads (apps/data/views.py:193-208), each through the SSRF guard;
+    a failing URL is reported and the others continue (the reference logged and went on)."""
+    errors = []
+    for url in urls:
+        name = os.path.basename(url.split("?", 1)[0].rstrip("/")) or "download"
+        if not valid_name(name):
+            name = "download"
+        try:
+            net.fetch(url, os.path.join(dest, name), allow_private=allow_private, max_bytes=max_bytes)
+        except (net.FetchRefused, OSError, ValueError) as exc:
+            errors.append(f"{url}: {exc}")
+    return errors
 
 
 def _extract_zip(data: bytes, dest: str) -> None:

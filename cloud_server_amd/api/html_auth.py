@@ -3,7 +3,10 @@ from ``django.contrib.auth.urls`` and ``admin.site.urls`` (CloudServer/urls.py:2
 SURVEY.md §2.7 rows `/login/ …` and `/admin/`).
 
 * ``/login/`` ``/logout/`` — form login; the session cookie ``sessionid`` carries an API
-  token, so a logged-in browser can also call the JSON API (``current_user`` accepts it);
+  token, so a logged-in browser can also call the JSON API (``current_user`` accepts it,
+  with Django's CSRF rule for unsafe methods: ``X-CSRFToken`` must match the
+  ``csrftoken`` cookie).  Every form carries a ``csrfmiddlewaretoken`` field checked
+  against that cookie (login CSRF included); ``/logout/`` only acts on a POST;
 * ``/password_change/`` (+ ``done/``) — needs the session;
 * ``/password_reset/`` (+ ``done/``), ``/reset/<uid>/<token>/`` (+ ``/reset/done/``) —
   the e-mail lands in ``<storage>/outbox`` (no SMTP here);
@@ -14,13 +17,17 @@ Pages are plain server-rendered HTML with every user value escaped.
 """
 from __future__ import annotations
 
+import hmac
 import html
+import secrets
 from typing import Any, Callable, Dict, List, Optional
 
 from fastapi import FastAPI, Request
 from fastapi.responses import HTMLResponse, RedirectResponse
 
 COOKIE = "sessionid"
+CSRF_COOKIE = "csrftoken"
+SESSION_AGE_S = 14 * 86400          # Django's SESSION_COOKIE_AGE
 
 
 def _page(title: str, body: str, status: int = 200) -> HTMLResponse:
@@ -28,11 +35,32 @@ def _page(title: str, body: str, status: int = 200) -> HTMLResponse:
                         f"</title></head><body><h1>{html.escape(title)}</h1>{body}</body></html>", status)
 
 
-def _form(action: str, fields: List[tuple], submit: str, errors: Optional[List[str]] = None) -> str:
+def csrf_token(request: Request) -> str:
+    """The request's CSRF cookie value, or a fresh one (set by ``_with_csrf``)."""
+    tok = request.cookies.get(CSRF_COOKIE, "")
+    return tok if len(tok) >= 32 else secrets.token_hex(16)
+
+
+def _with_csrf(resp, request: Request, tok: str):
+    if request.cookies.get(CSRF_COOKIE) != tok:
+        resp.set_cookie(CSRF_COOKIE, tok, samesite="lax", max_age=365 * 86400)
+    return resp
+
+
+def csrf_ok(request: Request, fields: Dict[str, Any]) -> bool:
+    cookie = request.cookies.get(CSRF_COOKIE, "")
+    sent = str(fields.get("csrfmiddlewaretoken", "") or request.headers.get("x-csrftoken", ""))
+    return bool(cookie) and hmac.compare_digest(cookie, sent)
+
+
+def _form(action: str, fields: List[tuple], submit: str, errors: Optional[List[str]] = None,
+          csrf: str = "") -> str:
     err = "".join(f"<p class='error'>{html.escape(e)}</p>" for e in (errors or []))
     rows = "".join(f"<p><label>{html.escape(label)} <input type='{typ}' name='{name}'></label></p>"
                    for name, label, typ in fields)
-    return f"{err}<form method='post' action='{html.escape(action)}'>{rows}<button>{html.escape(submit)}</button></form>"
+    hidden = f"<input type='hidden' name='csrfmiddlewaretoken' value='{html.escape(csrf)}'>"
+    return (f"{err}<form method='post' action='{html.escape(action)}'>{hidden}{rows}"
+            f"<button>{html.escape(submit)}</button></form>")
 
 
 def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
@@ -44,31 +72,51 @@ def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
         f, _, e = await read_form(request)
         return {} if e else f
 
+    def page(request: Request, title: str, action: str, flds: List[tuple], submit: str,
+             errors: Optional[List[str]] = None, status: int = 200):
+        tok = csrf_token(request)
+        return _with_csrf(_page(title, _form(action, flds, submit, errors, tok), status), request, tok)
+
+    def csrf_failed(request: Request):
+        return _page("Forbidden", "<p>CSRF verification failed. Request aborted.</p>", 403)
+
     # ------------------------------------------------------------------ login / logout
     login_fields = [("username", "Username", "text"), ("password", "Password", "password")]
 
     @app.get("/login/")
     async def login_page(request: Request):
-        return _page("Log in", _form("/login/", login_fields, "Log in"))
+        return page(request, "Log in", "/login/", login_fields, "Log in")
 
     @app.post("/login/")
     async def login_submit(request: Request):
         f = await fields(request)
+        if not csrf_ok(request, f):
+            return csrf_failed(request)
         user = db.find_user(username=str(f.get("username", "")))
         from ..store.db import check_password
         if not user or not check_password(str(f.get("password", "")), user["password"]):
-            return _page("Log in", _form("/login/", login_fields, "Log in", [
-                "Please enter a correct username and password."]), 200)
+            return page(request, "Log in", "/login/", login_fields, "Log in",
+                        ["Please enter a correct username and password."])
         nxt = request.query_params.get("next", "/")
         if not nxt.startswith("/") or nxt.startswith("//"):
             nxt = "/"                                   # no open redirect
         r = RedirectResponse(nxt, status_code=302)
-        r.set_cookie(COOKIE, db.token_for(user["id"]), httponly=True, samesite="lax")
+        r.set_cookie(COOKIE, db.token_for(user["id"]), httponly=True, samesite="lax", max_age=SESSION_AGE_S)
+        # rotate the CSRF token at login (Django's rotate_token)
+        r.set_cookie(CSRF_COOKIE, secrets.token_hex(16), samesite="lax", max_age=365 * 86400)
         return r
 
-    @app.api_route("/logout/", methods=["GET", "POST"])
+    @app.get("/logout/")
+    async def logout_confirm(request: Request):
+        # a GET never logs out (a cross-site link must not delete the shared API token)
+        return page(request, "Log out", "/logout/", [], "Log out")
+
+    @app.post("/logout/")
     async def logout_page(request: Request):
-        u = session_user(request)
+        f = await fields(request)
+        if not csrf_ok(request, f):
+            return csrf_failed(request)
+        u = session_user(request, csrf_verified=True)
         if u:
             db.delete_token(u["id"])
         r = _page("Logged out", "<p>Thanks for spending some quality time with the web site today.</p>")
@@ -84,14 +132,16 @@ def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
     async def change_page(request: Request):
         if session_user(request) is None:
             return RedirectResponse("/login/?next=/password_change/", status_code=302)
-        return _page("Password change", _form("/password_change/", change_fields, "Change my password"))
+        return page(request, "Password change", "/password_change/", change_fields, "Change my password")
 
     @app.post("/password_change/")
     async def change_submit(request: Request):
-        u = session_user(request)
+        f = await fields(request)
+        if not csrf_ok(request, f):
+            return csrf_failed(request)
+        u = session_user(request, csrf_verified=True)
         if u is None:
             return RedirectResponse("/login/?next=/password_change/", status_code=302)
-        f = await fields(request)
         from ..store.db import check_password
         errs: List[str] = []
         if not check_password(str(f.get("old_password", "")), u["password"]):
@@ -101,9 +151,11 @@ def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
             errs.append("The two password fields didn't match.")
         errs += validate_password(p1, u["username"], u["email"]) if not errs else []
         if errs:
-            return _page("Password change", _form("/password_change/", change_fields, "Change my password", errs))
-        db.set_password(u["id"], p1)
-        return RedirectResponse("/password_change/done/", status_code=302)
+            return page(request, "Password change", "/password_change/", change_fields, "Change my password", errs)
+        db.set_password(u["id"], p1)          # revokes every session; this browser gets a new one
+        r = RedirectResponse("/password_change/done/", status_code=302)
+        r.set_cookie(COOKIE, db.token_for(u["id"]), httponly=True, samesite="lax", max_age=SESSION_AGE_S)
+        return r
 
     @app.get("/password_change/done/")
     async def change_done(request: Request):
@@ -112,11 +164,13 @@ def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
     # ------------------------------------------------------------------ password reset
     @app.get("/password_reset/")
     async def reset_page(request: Request):
-        return _page("Password reset", _form("/password_reset/", [("email", "Email", "email")], "Reset my password"))
+        return page(request, "Password reset", "/password_reset/", [("email", "Email", "email")], "Reset my password")
 
     @app.post("/password_reset/")
     async def reset_submit(request: Request):
         f = await fields(request)
+        if not csrf_ok(request, f):
+            return csrf_failed(request)
         email = str(f.get("email", ""))
         user = db.find_user(email=email) if email else None
         if user:
@@ -133,11 +187,13 @@ def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
 
     @app.get("/reset/{uid}/{token}/")
     async def reset_confirm_page(uid: int, token: str, request: Request):
-        return _page("Enter new password", _form(f"/reset/{uid}/{token}/", set_fields, "Change my password"))
+        return page(request, "Enter new password", f"/reset/{uid}/{token}/", set_fields, "Change my password")
 
     @app.post("/reset/{uid}/{token}/")
     async def reset_confirm_submit(uid: int, token: str, request: Request):
         f = await fields(request)
+        if not csrf_ok(request, f):
+            return csrf_failed(request)
         user = db.get_user(uid)
         p1, p2 = str(f.get("new_password1", "")), str(f.get("new_password2", ""))
         errs: List[str] = []
@@ -146,7 +202,8 @@ def install(app: FastAPI, db, settings, outbox: Callable[[str, str, str], None],
         elif user is not None:
             errs += validate_password(p1, user["username"], user["email"])
         if errs:
-            return _page("Enter new password", _form(f"/reset/{uid}/{token}/", set_fields, "Change my password", errs))
+            return page(request, "Enter new password", f"/reset/{uid}/{token}/", set_fields, "Change my password",
+                        errs)
         if user is None or not db.use_reset_token(uid, token):
             return _page("Password reset unsuccessful", "<p>The password reset link was invalid.</p>", 400)
         db.set_password(uid, p1)

@@ -13,7 +13,8 @@ local defaults.
 | CSA_GPUS              | all visible                     | comma list of GPU ids the scheduler uses |
 | CSA_EXECUTOR          | process                         | process / thread / inline job runner  |
 | CSA_TOKEN_TTL_S       | 0 (never expires)               | auth token lifetime                   |
-| CSA_ALLOW_URL_FETCH   | 1                               | allow the ``url`` dataset type        |
+| CSA_ALLOW_URL_FETCH   | 1                               | allow the ``url`` dataset type (http/https only) |
+| CSA_URL_ALLOW_PRIVATE | 0                               | let URL datasets reach loopback/private hosts |
 | CSA_MAX_UPLOAD_MB     | 512                             | request body limit                    |
 | CSA_CORS_ORIGINS      | (none)                          | comma list of allowed CORS origins ("*" = any) |
 | CSA_HEARTBEAT_S       | 900                             | a running job silent this long is killed + failed |
@@ -39,6 +40,7 @@ class Settings:
     executor: str = field(default_factory=lambda: _env("CSA_EXECUTOR", "process"))
     token_ttl_s: int = field(default_factory=lambda: int(_env("CSA_TOKEN_TTL_S", "0")))
     allow_url_fetch: bool = field(default_factory=lambda: _env("CSA_ALLOW_URL_FETCH", "1") == "1")
+    url_allow_private: bool = field(default_factory=lambda: _env("CSA_URL_ALLOW_PRIVATE", "0") == "1")
     max_upload_mb: int = field(default_factory=lambda: int(_env("CSA_MAX_UPLOAD_MB", "512")))
     preprocess_backend: str = field(default_factory=lambda: _env("CSA_PREPROCESS_BACKEND", "auto"))
     train_backend: str = field(default_factory=lambda: _env("CSA_TRAIN_BACKEND", "auto"))

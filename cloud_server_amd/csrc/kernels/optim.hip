@@ -40,7 +40,8 @@ struct OptArgs {
   KeepList keep;                   // ... except inside these ranges (float4-aligned)
   float lr; const int64_t* step;   // 1-based step AFTER the head kernel's increment
   ZeroList z; FoldList fold;
-  int64_t* cursor;                 // batch-stream cursor: += 1 at the end of the step
+  int64_t* cursor;                 // batch-stream cursor: += 1 (mod cursor_wrap) per step
+  long cursor_wrap;
 };
 
 constexpr int MAXS = 16;   // stripes per folded gradient
@@ -158,7 +159,10 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const long n = a.z.n[z];
     for (long i = tid; i < n; i += nth) p[i] = 0.f;
   }
-  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) *a.cursor += 1;
+  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t c = *a.cursor + 1;
+    *a.cursor = (a.cursor_wrap > 0 && c >= a.cursor_wrap) ? 0 : c;
+  }
 }
 
 }  // namespace csa
@@ -172,7 +176,8 @@ CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, lon
                           float lr, const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
                           int nzero, const long* fold_off, const long* fold_n, float* const* fold_src,
                           const int* fold_S, const long* fold_ld, int nfold, const long* keep_lo,
-                          const long* keep_hi, int nkeep, int64_t* cursor, hipStream_t st) {
+                          const long* keep_hi, int nkeep, int64_t* cursor, long cursor_wrap,
+                          hipStream_t st) {
   if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK) return -1;
   OptArgs a{};
   a.keep.count = nkeep;
@@ -182,6 +187,7 @@ CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, lon
     a.keep.hi[i] = keep_hi[i];
   }
   a.cursor = cursor;
+  a.cursor_wrap = cursor_wrap;
   a.opt = opt; a.w = w; a.g = g; a.s0 = s0; a.s1 = s1; a.n = n; a.lr = lr; a.step = step;
   a.gz = zero_grad ? g : nullptr;
   a.z.count = nzero;

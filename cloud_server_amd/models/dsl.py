@@ -303,7 +303,8 @@ class TrainConfig:
     # --- new-framework knobs (not in the reference JSON; all optional) ---
     batch_size: int = 50                   # construct_distribute.py:403 hard-codes 50
     log_every: int = 100                   # :405 — accuracy line every 100 global steps
-    ckpt_every: int = 500                  # replaces Supervisor save_model_secs=60 (:391)
+    ckpt_every: int = 0                    # optional step-based checkpoints (0 = off)
+    ckpt_secs: float = 60.0                # Supervisor(save_model_secs=60) (:391)
     bn_mode: str = "running"               # "batch" = reference quirk 3
     compat_adagrad: bool = False           # True = reference quirk 1 (Adagrad 1e-4)
     sync_bn: bool = False                  # DP: BatchNorm statistics over the GLOBAL batch
@@ -358,7 +359,8 @@ def parse_train_config(cfg: Union[str, bytes, Dict[str, Any]]) -> TrainConfig:
         layers=layers, raw=dict(cfg),
         batch_size=_as_int(ext.get("batch_size", 50), "batch_size"),
         log_every=_as_int(ext.get("log_every", 100), "log_every"),
-        ckpt_every=_as_int(ext.get("ckpt_every", 500), "ckpt_every"),
+        ckpt_every=_as_int(ext.get("ckpt_every", 0), "ckpt_every"),
+        ckpt_secs=_as_float(ext.get("ckpt_secs", 60.0), "ckpt_secs"),
         bn_mode=str(ext.get("bn_mode", "running")),
         compat_adagrad=bool(ext.get("compat_adagrad", False)),
         sync_bn=str(ext.get("sync_bn", False)).lower() in ("1", "true", "yes"),

@@ -47,7 +47,7 @@ _SIGS = {
     "csa_conv_bwd_route": (I, [P, P, P, P, I, F, P, I, F, F, P, P, P, P, P, I,
                                P, P, P, P, I, F, P, I, F, F, P, P, P, I, P, P, P, P, F, P]),
     "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P, P]),
-    "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P, I, P, P]),
+    "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P, I, P, L, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),

@@ -3,7 +3,7 @@
 Replaces the reference's TF ``ClusterSpec``/``tf.train.Server`` gRPC cluster
 (construct_distribute.py:344-349) and the ``--ps_hosts/--worker_hosts/--job_name/
 --task_index`` flags (:37-43).  Ranks come from the standard env:// variables that
-``torch.distributed.run`` (or our own launcher, ``parallel.launch``) sets:
+``torch.distributed.run`` (or the job manager's launcher, ``runtime.jobs``) sets:
 RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT.
 
 On ROCm the ``nccl`` backend IS RCCL; CPU tests use ``gloo`` with the same code.

@@ -28,12 +28,14 @@ start-up self-test passed on every rank (``CSA_XGMI=auto|1|0``).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
+from ..utils.tracing import trace_range
 from .dist import DistContext
 from . import xgmi as _xg
 
@@ -58,7 +60,23 @@ class GradSync:
         self.xgmi_mode = _xg.enabled_by_env()
         self.xgmi_tuning: dict = {}      # tag -> {"bytes", "xgmi_us", "rccl_us"} (auto mode)
         self._choice: dict = {}
+        self.timing: Optional[list] = None   # set by TrainEngine.probe: (start, end) events per call
         self._setup_xgmi()
+
+    @contextlib.contextmanager
+    def _timed(self):
+        """Bracket one collective with timing events on the current stream when a probe
+        step asked for it (never inside graph capture)."""
+        if self.timing is None or not self.ctx.device.type == "cuda" or torch.cuda.is_current_stream_capturing():
+            with trace_range("csa.comm"):
+                yield
+            return
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        with trace_range("csa.comm"):
+            yield
+        b.record()
+        self.timing.append((a, b))
 
     def _setup_xgmi(self) -> None:
         mode = self.xgmi_mode
@@ -82,6 +100,20 @@ class GradSync:
         """Raise if a peer-buffer collective timed out (its results are not valid)."""
         if self.xgmi is not None:
             self.xgmi.check()
+
+    def check_agreed(self) -> None:
+        """``check`` agreed on by every rank: the channels' error words are MAX-reduced, so
+        a timeout seen by one rank raises on ALL ranks together (no rank is left waiting in
+        the next collective while another tears down)."""
+        if not self.ctx.enabled:
+            return
+        bad = 0
+        if self.xgmi is not None:
+            bad = int(any(ch.error() for ch in self.xgmi.channels.values()))
+        flag = torch.tensor([bad], dtype=torch.int32, device=self.ctx.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item():
+            raise RuntimeError("xGMI collective timed out waiting for a peer on some rank (channel poisoned)")
 
     def _xg_channel(self, tag: str, srcs, dsts=None) -> Optional["_xg.XgmiChannel"]:
         """The xGMI channel for call site ``tag``, or None for RCCL.  Decided once per tag,
@@ -192,24 +224,27 @@ class GradSync:
             return
         for a, b in self.buckets(lo, hi):
             ch = self._xg_channel(f"ar:{a}:{b}", [flat_grad[a:b]])
-            if ch is not None:
-                ch.all_reduce([flat_grad[a:b]])
-            else:
-                dist.all_reduce(flat_grad[a:b])
+            with self._timed():
+                if ch is not None:
+                    ch.all_reduce([flat_grad[a:b]])
+                else:
+                    dist.all_reduce(flat_grad[a:b])
 
     # ---- ps (sharded) ----
     def reduce_scatter(self, flat_grad: torch.Tensor, shard_out: torch.Tensor) -> None:
         if not self.ctx.enabled:
             shard_out.copy_(flat_grad)
             return
-        dist.reduce_scatter_tensor(shard_out, flat_grad)
+        with self._timed():
+            dist.reduce_scatter_tensor(shard_out, flat_grad)
 
     def all_gather_params(self, flat_param: torch.Tensor) -> None:
         if not self.ctx.enabled:
             return
         lo, hi = self.shard_range()
-        dist.all_gather_into_tensor(flat_param, flat_param[lo:hi].clone()
-                                    if self.ctx.backend == "gloo" else flat_param[lo:hi])
+        with self._timed():
+            dist.all_gather_into_tensor(flat_param, flat_param[lo:hi].clone()
+                                        if self.ctx.backend == "gloo" else flat_param[lo:hi])
 
     # ---- lowrank ----
     def all_gather_rows(self, local: torch.Tensor, out: torch.Tensor) -> None:
@@ -229,16 +264,17 @@ class GradSync:
                 out.copy_(local)
             return
         ch = self._xg_channel(tag, [p[0] for p in pairs], [p[1] for p in pairs]) if len(pairs) <= 8 else None
-        if ch is not None:
-            ch.all_gather(pairs)
-            return
-        if self.coalesce and len(pairs) > 1:
-            with dist._coalescing_manager(async_ops=False):
-                for local, out in pairs:
-                    dist.all_gather_into_tensor(out, local.contiguous())
-            return
-        for local, out in pairs:
-            dist.all_gather_into_tensor(out, local.contiguous())
+        with self._timed():
+            if ch is not None:
+                ch.all_gather(pairs)
+                return
+            if self.coalesce and len(pairs) > 1:
+                with dist._coalescing_manager(async_ops=False):
+                    for local, out in pairs:
+                        dist.all_gather_into_tensor(out, local.contiguous())
+                return
+            for local, out in pairs:
+                dist.all_gather_into_tensor(out, local.contiguous())
 
     def allreduce_ranges(self, flat: torch.Tensor, ranges, tag: str = "ranges") -> None:
         """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one launch: xGMI kernel or a
@@ -246,27 +282,29 @@ class GradSync:
         if not self.ctx.enabled or not ranges:
             return
         ch = self._xg_channel(tag, [flat[lo:hi] for lo, hi in ranges]) if len(ranges) <= 8 else None
-        if ch is not None:
-            ch.all_reduce([flat[lo:hi] for lo, hi in ranges])
-            return
-        if self.coalesce and len(ranges) > 1:
-            with dist._coalescing_manager(async_ops=False):
-                for lo, hi in ranges:
-                    dist.all_reduce(flat[lo:hi])
-            return
-        for lo, hi in ranges:
-            dist.all_reduce(flat[lo:hi])
+        with self._timed():
+            if ch is not None:
+                ch.all_reduce([flat[lo:hi] for lo, hi in ranges])
+                return
+            if self.coalesce and len(ranges) > 1:
+                with dist._coalescing_manager(async_ops=False):
+                    for lo, hi in ranges:
+                        dist.all_reduce(flat[lo:hi])
+                return
+            for lo, hi in ranges:
+                dist.all_reduce(flat[lo:hi])
 
     def allreduce_tensors(self, tensors, tag: str) -> None:
         """In-place SUM of small fp32 tensors across ranks (SyncBN statistics slabs)."""
         if not self.ctx.enabled:
             return
         ch = self._xg_channel(tag, list(tensors)) if len(tensors) <= 8 else None
-        if ch is not None:
-            ch.all_reduce(list(tensors))
-            return
-        for t in tensors:
-            dist.all_reduce(t)
+        with self._timed():
+            if ch is not None:
+                ch.all_reduce(list(tensors))
+                return
+            for t in tensors:
+                dist.all_reduce(t)
 
     def broadcast_params(self, flat_param: torch.Tensor) -> None:
         """Initial sync from rank 0 (reference: chief runs init_op, construct_distribute.py:379)."""

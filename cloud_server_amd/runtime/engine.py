@@ -31,6 +31,7 @@ from ..models.dsl import TrainConfig
 from ..ops import optim_ref
 from ..parallel.dist import DistContext
 from ..parallel.dp import GradSync
+from ..utils.tracing import trace_range
 
 RING = 4096
 
@@ -174,13 +175,39 @@ class TrainEngine:
 
     def step(self) -> None:
         self.stream.before_step()
-        if self.use_graph:
-            if self.graph is None:
-                self._capture()
-            self.graph.replay()
-        else:
-            self.program.run()
+        with trace_range("csa.step"):          # ROCTx range when CSA_TRACE=1
+            if self.use_graph:
+                if self.graph is None:
+                    with trace_range("csa.capture"):
+                        self._capture()
+                self.graph.replay()
+            else:
+                self.program.run()
         self.host_step += 1
+
+    def probe_comm(self) -> float:
+        """Run THIS step eagerly with every collective bracketed by timing events and
+        return its communication time (ms; sum over call sites, side streams included).
+        A real training step, so the run's semantics do not change; data parallel only.
+        The per-rank value is what ``metrics.jsonl`` reports as ``comm_ms``."""
+        if not self.ctx.enabled:
+            self.step()
+            return 0.0
+        if self.use_graph and self.graph is None:
+            self._capture()
+        self.stream.before_step()
+        self.sync.timing = []
+        try:
+            self.program.run()
+        finally:
+            ev, self.sync.timing = self.sync.timing, None
+        self.host_step += 1
+        self.sync_device()
+        self._comm_ms = float(sum(a.elapsed_time(b) for a, b in ev))
+        return self._comm_ms
+
+    def comm_ms_per_step(self) -> float:
+        return getattr(self, "_comm_ms", 0.0)
 
     def sync_device(self) -> None:
         if self.device.type == "cuda":

@@ -744,6 +744,6 @@ class HipProgram:
             e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), 0 if self.ps_mode else 1,
             float(e.lr), K.ptr(e.dstep),
             zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, len(folds), klo, khi, len(keep),
-            K.ptr(e.stream.cursor), st), "optimizer")
+            K.ptr(e.stream.cursor), e.stream.wrap, st), "optimizer")
         if e.sync.strategy == "ps" and e.ctx.enabled:
             e.sync.all_gather_params(e.flat)

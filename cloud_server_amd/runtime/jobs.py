@@ -14,7 +14,11 @@ C29; apps/construction/views.py:97-146) — with a local manager:
 * control: stop / pause write ``control.json`` (the trainer checks it every log
   interval and checkpoints on pause); resume re-queues the job and the trainer restores
   the newest checkpoint; a worker that dies is marked failed (its slots are released)
-  and can be resumed the same way.
+  and can be resumed the same way;
+* recovery policy: a worker that fails AFTER making progress (a newer checkpoint than
+  the one it started from) is re-queued automatically, up to ``max_restarts`` times
+  (``CSA_MAX_RESTARTS``, default 2), and resumes from that checkpoint; a failure without
+  progress (bad data, a deterministic crash) ends the job as ``failed`` at once.
 """
 from __future__ import annotations
 
@@ -23,6 +27,7 @@ import multiprocessing as mp
 import os
 import queue
 import signal
+import socket
 import subprocess
 import sys
 import threading
@@ -31,6 +36,7 @@ import traceback
 from typing import Any, Dict, List, Optional
 
 from ..store.db import Database
+from . import checkpoint as ckpt
 from .scheduler import make_scheduler
 from .trainer import CONTROL, STATUS, run_job, write_status
 
@@ -83,6 +89,14 @@ def _launcher_main(req: "mp.Queue", resp: "mp.Queue") -> None:   # pragma: no co
                 del procs[jid]
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 class JobManager:
     def __init__(self, settings, db: Database, executor: Optional[str] = None,
                  ngpu: Optional[int] = None, slots_per_gpu: int = 4):
@@ -94,6 +108,7 @@ class JobManager:
         self.ngpu = ngpu
         self.use_cpu = ngpu == 0
         self.sched = make_scheduler(max(ngpu, 1), slots_per_gpu if ngpu else 2)
+        self.max_restarts = int(os.environ.get("CSA_MAX_RESTARTS", "2"))
         self.running: Dict[int, Dict[str, Any]] = {}
         self._lock = threading.RLock()
         self._stop = threading.Event()
@@ -152,6 +167,9 @@ class JobManager:
                 self.sched.cancel(jid)
                 self._finish(jid, "stopped" if action == "stop" else "paused")
             else:
+                with self._lock:
+                    if jid in self.running:
+                        self.running[jid]["user_stop"] = True
                 with open(os.path.join(mdir, CONTROL), "w") as f:
                     json.dump({"action": action, "time": time.time()}, f)
             return {"job": jid, "action": action}
@@ -253,6 +271,8 @@ class JobManager:
                 continue
             info["gpus"] = gpus
             info["state"] = "running"
+            last = ckpt.latest(info["mdir"])
+            info["ckpt_at_launch"] = last[0] if last else -1
             self.db.update_job(jid, state="running", started=time.time(),
                                gpu=",".join(map(str, gpus)) if not self.use_cpu else "cpu")
             self._launch(jid, info)
@@ -284,7 +304,7 @@ class JobManager:
         mod = ["-m", "cloud_server_amd.runtime.worker", "--model-dir", mdir, "--datatype", datatype,
                "--backend", self.settings.train_backend]
         if n > 1:
-            port = 29500 + (jid % 2000)
+            port = _free_port()             # a fixed 29500 + jid formula collided
             argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                     "--master-addr", "127.0.0.1", "--master-port", str(port)] + mod[1:]
         else:
@@ -320,7 +340,29 @@ class JobManager:
         err = None
         if state == "failed":
             err = (info or {}).get("kill_reason") or f"worker exit code {rc}"
+            if info is not None and self._auto_restart(jid, info, err):
+                return
         self._finish(jid, state, err)
+
+    def _auto_restart(self, jid: int, info: Dict[str, Any], err: str) -> bool:
+        """Re-queue a failed job that made progress since its launch (bounded)."""
+        if info.get("user_stop") or info.get("restarts", 0) >= self.max_restarts:
+            return False
+        last = ckpt.latest(info["mdir"])
+        if last is None or last[0] <= info.get("ckpt_at_launch", -1):
+            return False
+        self.sched.release(jid)
+        info["restarts"] = info.get("restarts", 0) + 1
+        info["state"] = "queued"
+        info.pop("killed", None)
+        info.pop("kill_reason", None)
+        write_status(info["mdir"], state="queued", restarts=info["restarts"], last_error=err)
+        self.db.update_job(jid, state="queued", error=f"restart {info['restarts']} after: {err}")
+        if not self.sched.submit(jid, 1 if self.use_cpu else info["ngpus"]):
+            return False
+        if self.executor == "inline":
+            self._admit()
+        return True
 
     def _finish(self, jid: int, state: str, error: Optional[str] = None) -> None:
         self.sched.release(jid)
@@ -328,4 +370,6 @@ class JobManager:
             info = self.running.pop(jid, None)
         if info and state in ("failed", "stopped", "paused"):
             write_status(info["mdir"], state=state)
+        if info and info.get("restarts") and error is None:
+            error = f"recovered after restart {info['restarts']}"
         self.db.update_job(jid, state=state, finished=time.time(), error=error)

@@ -30,6 +30,7 @@ from ..data.datasets import ArrayDataset, load_dataset_for_model, load_mnist_dir
 from ..models.dsl import parse_train_config
 from ..parallel.dist import DistContext, all_reduce_max, barrier
 from . import checkpoint as ckpt
+from ..utils.tracing import trace_range
 from .engine import TrainEngine
 
 RESULT = "result.txt"
@@ -82,6 +83,105 @@ def load_job_data(model_dir: str, datatype: str, ratio: float):
     return train, test
 
 
+def _fault_step(rank: int, model_dir: str) -> int:
+    """``CSA_FAULT_AT_STEP``: ``s`` (every rank raises at step s) or ``k:s`` (only rank k):
+    the "kill rank k at step s" hook of SURVEY.md §5.3.  With ``CSA_FAULT_ONCE=1`` the
+    fault fires on the first attempt only (a marker file in the model dir), so a test can
+    watch the automatic restart succeed."""
+    v = os.environ.get("CSA_FAULT_AT_STEP", "").strip()
+    if not v:
+        return -1
+    if os.environ.get("CSA_FAULT_ONCE", "0") == "1":
+        marker = os.path.join(model_dir, ".fault_fired")
+        if os.path.exists(marker):
+            return -1
+        open(marker, "w").close()
+    if ":" in v:
+        r, st = v.split(":", 1)
+        return int(st) if int(r) == rank else -1
+    return int(v)
+
+
+class _MetricLog:
+    """Training-log lines without stalling the device queue.
+
+    At a log step the engine's device metric rings are copied into pinned host memory
+    (non-blocking, stream-ordered) and a timing event is recorded; the line is written
+    once that event has completed — normally at the next log point, so the host never
+    waits for the GPU to drain.  Durations come from the device events (mean step time
+    over the interval).  CPU runs are synchronous and write immediately."""
+
+    def __init__(self, eng: TrainEngine, chief: bool, result_path: str, metrics_path: str, world: int):
+        from collections import deque
+        self.eng, self.chief, self.world = eng, chief, world
+        self.cuda = eng.device.type == "cuda"
+        self.pending = deque()
+        self.prev_ev = None
+        self.prev_step = None
+        self.t_host = time.perf_counter()
+        self.h_step = eng.host_step
+        self.last_acc = float("nan")
+        self.fr = open(result_path, "a") if chief else None
+        self.fm = open(metrics_path, "a") if chief else None
+        self.lines = 0
+
+    def mark(self, step: int, int_start: int) -> None:
+        e = self.eng
+        if self.cuda:
+            pc = torch.empty(e.ring_correct.shape, dtype=e.ring_correct.dtype, pin_memory=True)
+            pl = torch.empty(e.ring_loss.shape, dtype=e.ring_loss.dtype, pin_memory=True)
+            pc.copy_(e.ring_correct, non_blocking=True)
+            pl.copy_(e.ring_loss, non_blocking=True)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream(e.device))
+            self.pending.append((step, int_start, e.host_step, ev, pc, pl, time.perf_counter()))
+            self.drain(block=False)
+        else:
+            self.pending.append((step, int_start, e.host_step, None, e.ring_correct, e.ring_loss,
+                                 time.perf_counter()))
+            self.drain(block=True)
+
+    def drain(self, block: bool) -> None:
+        from .engine import RING
+        B = self.eng.cfg.batch_size
+        while self.pending:
+            step, s0, s1, ev, pc, pl, th = self.pending[0]
+            if ev is not None and not block and not ev.query():
+                return
+            self.pending.popleft()
+            if ev is not None:
+                ev.synchronize()
+            n = max(s1 - self.h_step, 1)
+            if ev is not None and self.prev_ev is not None:
+                step_time = self.prev_ev.elapsed_time(ev) / 1e3 / n
+            else:
+                step_time = (th - self.t_host) / n
+            self.prev_ev, self.t_host, self.h_step = ev, th, s1
+            acc = float(pc[step % RING]) / B
+            self.last_acc = acc
+            k = min(max(s1 - s0, 1), RING)
+            pos = [(s1 - 1 - i) % RING for i in range(k)]
+            mloss = float(pl[pos].double().mean())
+            macc = float(pc[pos].double().sum()) / (k * B)
+            if self.chief:
+                self.fr.write("step:%d,accuracy:%f,duration:%f\n" % (step, acc, step_time))
+                self.fm.write(json.dumps({"step": step, "loss": mloss, "accuracy": macc, "batch_accuracy": acc,
+                                          "step_ms": step_time * 1e3,
+                                          "samples_per_s": B * self.world / max(step_time, 1e-9),
+                                          "comm_ms": self.eng.comm_ms_per_step(),
+                                          "time": time.time()}) + "\n")
+                self.lines += 1
+        if self.chief:
+            self.fr.flush()
+            self.fm.flush()
+
+    def close(self) -> None:
+        self.drain(block=True)
+        if self.chief:
+            self.fr.close()
+            self.fm.close()
+
+
 def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
             device: Optional[str] = None, ctx: Optional[DistContext] = None,
             backend: str = "auto", data: Optional[tuple] = None) -> Dict[str, Any]:
@@ -101,65 +201,82 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
     last = ckpt.latest(model_dir)
     if last is not None:
         ckpt.restore_engine(eng, ckpt.load(last[1]))
-    fault_at = int(os.environ.get("CSA_FAULT_AT_STEP", "-1"))     # raise (crash) at this step
+    fault_at = _fault_step(ctx.rank, model_dir)                                 # raise (crash) at this step
     hang_at = int(os.environ.get("CSA_HANG_AT_STEP", "-1"))       # stop making progress (watchdog tests)
-    result_path = os.path.join(model_dir, RESULT)
-    metrics_path = os.path.join(model_dir, METRICS)
     log_every = max(1, cfg.log_every)
-    t_int = time.perf_counter()
+    # control / time-checkpoint decisions: every log point on one rank (a file stat); under
+    # data parallel they are a broadcast (a sync point), so every ~2000 steps
+    ctl_every = 1 if not ctx.enabled else max(1, 2000 // log_every)
+    ctl_path = os.path.join(model_dir, CONTROL)
+    ckpter = ckpt.AsyncCheckpointer(eng, model_dir)
+    mlog = _MetricLog(eng, chief, os.path.join(model_dir, RESULT), os.path.join(model_dir, METRICS), ctx.world)
+    t_ckpt = t_status = time.time()
     int_start = eng.host_step
+    nlog = 0
     state = "done"
     try:
         while eng.host_step < cfg.iter:
             step = eng.host_step
             if step == fault_at:
-                raise RuntimeError(f"injected fault at step {step}")
+                raise RuntimeError(f"injected fault at step {step} (rank {ctx.rank})")
             if step == hang_at:
                 while True:
                     time.sleep(1.0)
-            eng.step()
+            if ctx.enabled and eng.device.type == "cuda" and step % (ctl_every * log_every) == 1:
+                eng.probe_comm()            # per-rank collective time for metrics.jsonl
+            else:
+                eng.step()
             if step % log_every != 0:
                 continue
             # reference: the accuracy logged for step s is the batch of step s evaluated
             # with the pre-update weights — exactly this step's forward pass
-            eng.sync_device()
-            eng.sync.check()   # a timed-out peer-buffer collective fails the job
-            now = time.perf_counter()
-            n = eng.host_step - int_start
-            step_time = (now - t_int) / max(n, 1)
-            if chief:
-                acc = eng.last_batch_accuracy()
-                with open(result_path, "a") as f:
-                    f.write("step:%d,accuracy:%f,duration:%f\n" % (step, acc, step_time))
-                mm = eng.metrics_since(int_start)
-                with open(metrics_path, "a") as f:
-                    f.write(json.dumps({"step": step, "loss": mm["loss"], "accuracy": mm["accuracy"],
-                                        "batch_accuracy": acc, "step_ms": step_time * 1e3,
-                                        "samples_per_s": cfg.batch_size * ctx.world / max(step_time, 1e-9),
-                                        "time": time.time()}) + "\n")
-                write_status(model_dir, step=eng.host_step, heartbeat=time.time())   # watchdog liveness
+            with trace_range("csa.log"):
+                mlog.mark(step, int_start)
+            int_start = eng.host_step
+            now = time.time()
+            if chief and (now - t_status > 1.0 or nlog == 0):
+                write_status(model_dir, step=eng.host_step, heartbeat=now)     # watchdog liveness
+                t_status = now
+            nlog += 1
             if cfg.ckpt_every > 0 and step > 0 and step % cfg.ckpt_every == 0:
-                _checkpoint(model_dir, eng, chief)
-            t_int, int_start = time.perf_counter(), eng.host_step
-            action = _agree(ctx, read_control(model_dir) if chief else "")
-            if action == "stop":
+                ckpter.save(chief)
+                t_ckpt = now
+            if nlog % ctl_every:
+                continue
+            action = ""
+            if chief:
+                action = read_control(model_dir) if os.path.exists(ctl_path) else ""
+                if not action and cfg.ckpt_secs > 0 and now - t_ckpt >= cfg.ckpt_secs:
+                    action = "ckpt"         # Supervisor(save_model_secs=60), construct_distribute.py:391
+            action = _agree(ctx, action)
+            if action == "ckpt":
+                with trace_range("csa.ckpt"):
+                    ckpter.save(chief)
+                t_ckpt = now
+            elif action == "stop":
                 state = "stopped"
                 break
-            if action == "pause":
-                _checkpoint(model_dir, eng, chief)
+            elif action == "pause":
+                ckpter.save(chief)
+                ckpter.wait()
                 if chief:
                     write_status(model_dir, state="paused", step=eng.host_step)
                 state = "paused"
                 break
         eng.sync_device()
+        # a peer wait that timed out after the last log step left this rank's gradient
+        # un-reduced: fail before evaluating / checkpointing diverged parameters
+        eng.sync.check_agreed()
+        mlog.close()
         final_acc = None
         if state == "done":
-            final_acc = eng.evaluate(test) if len(test) else eng.last_batch_accuracy()
+            final_acc = eng.evaluate(test) if len(test) else mlog.last_acc
             if chief:
-                with open(result_path, "a") as f:
+                with open(os.path.join(model_dir, RESULT), "a") as f:
                     f.write("final_accuracy:%f\n\n" % final_acc)
         if state != "paused":
-            _checkpoint(model_dir, eng, chief)
+            ckpter.save(chief)
+        ckpter.wait()
         if chief:
             write_status(model_dir, state=state, step=eng.host_step, final_accuracy=final_acc,
                          backend=eng.backend, fallback=eng.fallback_reason)
@@ -168,6 +285,10 @@ def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
         if chief:
             write_status(model_dir, state="failed", step=eng.host_step, error=repr(exc),
                          trace=traceback.format_exc()[-4000:])
+        try:
+            ckpter.wait()           # never leave a half-written checkpoint thread behind
+        except Exception:
+            pass
         raise
 
 
@@ -182,7 +303,7 @@ def _agree(ctx: DistContext, action: str) -> str:
     if not ctx.enabled:
         return action
     import torch.distributed as dist
-    codes = {"": 0, "stop": 1, "pause": 2}
+    codes = {"": 0, "stop": 1, "pause": 2, "ckpt": 3}
     t = torch.tensor([codes.get(action, 0)], device=ctx.device)
     dist.broadcast(t, src=0)
     return {v: k for k, v in codes.items()}[int(t.item())]

@@ -10,7 +10,7 @@ containers over SSH (apps/construction/util/cmd.py:54-70, views.py:125-141).
 Reads ``DIR/model.json`` (the reference DSL, plus an optional ``options`` block), trains
 with ``runtime.trainer.run_job`` and exits 0 (done / stopped / paused) or 1 (failed).
 Data-parallel jobs run this module under ``torch.distributed.run`` (or
-``parallel.launch``): ranks come from RANK / WORLD_SIZE / LOCAL_RANK, one GPU each.
+``runtime.jobs``): ranks come from RANK / WORLD_SIZE / LOCAL_RANK, one GPU each.
 """
 from __future__ import annotations
 

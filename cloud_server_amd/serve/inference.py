@@ -110,6 +110,11 @@ class InferenceService:
             return dict(FAIL_NO_MODEL)
         return {"result": "success", "message": str(int(out[0]))}
 
+    async def predict_async(self, model_dir: str, img_bytes: bytes, prep: str = "reference") -> Dict[str, str]:
+        """``predict`` off the event loop (decode + forward run in the threadpool)."""
+        from starlette.concurrency import run_in_threadpool
+        return await run_in_threadpool(self.predict, model_dir, img_bytes, prep)
+
     def predict_many(self, model_dir: str, images: Sequence[bytes], prep: str = "reference") -> List[Dict[str, str]]:
         fn = prepare_reference if prep == "reference" else prepare_mnist
         xs = np.stack([fn(b) for b in images]) if images else np.zeros((0, 784), np.float32)

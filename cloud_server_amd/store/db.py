@@ -173,8 +173,13 @@ class Database:
             c.execute(f"UPDATE users SET {cols} WHERE id=?", (*allowed.values(), uid))
 
     def set_password(self, uid: int, password: str) -> None:
+        """New password hash; every API token / browser session and every outstanding
+        reset link of the user is revoked with it (Django invalidates sessions and reset
+        tokens once the password hash changes)."""
         with self.tx() as c:
             c.execute("UPDATE users SET password=? WHERE id=?", (hash_password(password), uid))
+            c.execute("DELETE FROM tokens WHERE user_id=?", (uid,))
+            c.execute("DELETE FROM reset_tokens WHERE user_id=?", (uid,))
 
     # ------------------------------------------------------------------ tokens
     def token_for(self, uid: int) -> str:

@@ -260,9 +260,29 @@ def test_metrics_cors_and_demo(tmp_path):
         assert c.get(f"/demo/{b['id']}/").status_code == 404
 
 
+class _FixtureServer:
+    """Serves a directory over http on 127.0.0.1 (URL datasets need http(s))."""
+
+    def __init__(self, root):
+        import functools
+        import http.server
+        import threading
+        h = functools.partial(http.server.SimpleHTTPRequestHandler, directory=str(root))
+        h.log_message = lambda *a, **k: None
+        self.httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), h)
+        self.port = self.httpd.server_address[1]
+        self.t = threading.Thread(target=self.httpd.serve_forever, daemon=True)
+        self.t.start()
+
+    def close(self):
+        self.httpd.shutdown()
+        self.httpd.server_close()
+
+
 def test_url_dataset_and_url_training(client, tmp_path):
-    """datatype=url: ';'-separated URLs downloaded into the dataset (file:// here — no
-    network), then the MNIST-idx training variant (construct_distribute_url.py)."""
+    """datatype=url: ';'-separated URLs downloaded into the dataset (a local http server
+    here — no network; private destinations are opted in for the test), then the
+    MNIST-idx training variant (construct_distribute_url.py)."""
     from cloud_server_amd.data.datasets import write_idx
     src = tmp_path / "mnist"
     src.mkdir()
@@ -276,9 +296,14 @@ def test_url_dataset_and_url_training(client, tmp_path):
         with open(src / stem, "rb") as f, gzip.open(str(src / (stem + ".gz")), "wb") as g:
             g.write(f.read())
         os.remove(src / stem)
-    urls = ";".join(f"file://{src}/{n}" for n in sorted(os.listdir(src)))
-    h = _auth(client)
-    pk = _mp(client, "/data/list/", {"file_type": "url", "file_class": "picture", "url": urls}, {}, h).json()["data_id"]
+    srv = _FixtureServer(src)
+    try:
+        urls = ";".join(f"http://127.0.0.1:{srv.port}/{n}" for n in sorted(os.listdir(src)))
+        h = _auth(client)
+        client.settings.url_allow_private = True
+        pk = _mp(client, "/data/list/", {"file_type": "url", "file_class": "picture", "url": urls}, {}, h).json()["data_id"]
+    finally:
+        srv.close()
     tree = json.dumps(client.get(f"/data/{pk}/", headers=h).json())
     assert "t10k-images-idx3-ubyte.gz" in tree
     client.post("/data/create/", json={"modelName": "mu"}, headers=h)
@@ -292,41 +317,110 @@ def test_url_dataset_and_url_training(client, tmp_path):
     assert len(res["every_result"]) == 2 and "final_accuracy" in res
 
 
+def test_url_fetch_refuses_file_and_private(client, tmp_path):
+    """ADVICE r1 (high): file:// (server files: the DB, the outbox) and loopback/private
+    destinations are refused; only http(s) to public addresses is fetched."""
+    from cloud_server_amd.utils import net
+    secret = tmp_path / "secret.txt"
+    secret.write_text("token")
+    h = _auth(client)
+    for url in (f"file://{secret}", "ftp://example.org/x", "gopher://x/"):
+        r = _mp(client, "/data/list/", {"file_type": "url", "file_class": "doc", "url": url}, {}, h)
+        assert r.status_code == 400, url
+    srv = _FixtureServer(tmp_path)
+    try:
+        client.settings.url_allow_private = False
+        r = _mp(client, "/data/list/", {"file_type": "url", "file_class": "doc",
+                                        "url": f"http://127.0.0.1:{srv.port}/secret.txt"}, {}, h)
+        assert r.status_code == 400 and "not allowed" in r.json()["detail"]
+    finally:
+        srv.close()
+    assert client.get("/data/list/", headers=h).json() == []
+    for a in ("127.0.0.1", "10.1.2.3", "192.168.0.1", "169.254.169.254", "::1", "::ffff:127.0.0.1", "0.0.0.0"):
+        assert not net.address_allowed(a, False), a
+    assert net.address_allowed("8.8.8.8", False)
+
+
+def test_password_change_revokes_tokens(client):
+    """a password change/reset revokes existing tokens and reset links."""
+    h = _auth(client)
+    db = client.app.state.db
+    tok_old = db.new_reset_token(1)
+    new = "An0ther-pass-77"
+    r = client.post("/rest-auth/password/change/", json={"old_password": PW, "new_password1": new,
+                                                         "new_password2": new}, headers=h)
+    assert r.status_code == 200 and r.json()["key"]
+    assert client.get("/rest-auth/user/", headers=h).status_code == 401          # old token revoked
+    h2 = {"Authorization": "Token " + r.json()["key"]}
+    assert client.get("/rest-auth/user/", headers=h2).status_code == 200
+    assert not db.use_reset_token(1, tok_old)                                     # old reset link revoked
+
+
+def _csrf(c, path):
+    import re
+    html = c.get(path).text
+    return re.search(r"name='csrfmiddlewaretoken' value='([0-9a-f]+)'", html).group(1)
+
+
 def test_browser_auth_pages_and_admin(client):
     """django.contrib.auth.urls + admin analogues: form login sets a session cookie that
-    the JSON API accepts; password change / reset by form; /admin/ is staff-only."""
+    the JSON API accepts; password change / reset by form; /admin/ is staff-only; every
+    form POST and every cookie-authenticated unsafe API call needs the CSRF token."""
     db = client.app.state.db
     uid = db.create_user("webu", PW, "webu@x.org")
     db.create_user("boss", PW, "boss@x.org", is_staff=True)
     assert "<form" in client.get("/login/").text
-    r = client.post("/login/", data={"username": "webu", "password": "nope"}, follow_redirects=False)
-    assert r.status_code == 200 and "correct username" in r.text
-    r = client.post("/login/?next=//evil.example/", data={"username": "webu", "password": PW},
+    tok = _csrf(client, "/login/")
+    # login CSRF: a form post without the token is refused
+    r = client.post("/login/", data={"username": "webu", "password": PW}, follow_redirects=False)
+    assert r.status_code == 403
+    r = client.post("/login/", data={"username": "webu", "password": "nope", "csrfmiddlewaretoken": tok},
                     follow_redirects=False)
+    assert r.status_code == 200 and "correct username" in r.text
+    r = client.post("/login/?next=//evil.example/", data={"username": "webu", "password": PW,
+                                                         "csrfmiddlewaretoken": tok}, follow_redirects=False)
     assert r.status_code == 302 and r.headers["location"] == "/" and "sessionid" in r.cookies
     assert client.get("/rest-auth/user/").json()["username"] == "webu"     # session auth on the API
+    # cookie-authenticated unsafe API call: needs X-CSRFToken == csrftoken cookie
+    assert client.patch("/rest-auth/user/", json={"first_name": "W"}).status_code == 401
+    ctok = client.cookies.get("csrftoken")
+    r = client.patch("/rest-auth/user/", json={"first_name": "W"}, headers={"X-CSRFToken": ctok})
+    assert r.status_code == 200 and r.json()["first_name"] == "W"
     assert client.get("/admin/", follow_redirects=False).status_code == 302  # not staff
     new = PW + "-2"
+    tok = _csrf(client, "/password_change/")
     r = client.post("/password_change/", data={"old_password": PW, "new_password1": new,
-                                               "new_password2": new}, follow_redirects=False)
+                                               "new_password2": new, "csrfmiddlewaretoken": tok},
+                    follow_redirects=False)
     assert r.status_code == 302 and r.headers["location"] == "/password_change/done/"
-    assert "Logged out" in client.get("/logout/").text
+    assert client.get("/rest-auth/user/").json()["username"] == "webu"     # re-issued session
+    # GET /logout/ only shows the confirmation form; the POST logs out
+    assert "<form" in client.get("/logout/").text
+    assert client.get("/rest-auth/user/").status_code == 200
+    tok = _csrf(client, "/logout/")
+    assert "Logged out" in client.post("/logout/", data={"csrfmiddlewaretoken": tok}).text
     client.cookies.clear()
     assert client.get("/rest-auth/user/").status_code == 401
     assert client.get("/password_change/", follow_redirects=False).status_code == 302
     # reset by e-mail link
-    r = client.post("/password_reset/", data={"email": "webu@x.org"}, follow_redirects=False)
+    tok = _csrf(client, "/password_reset/")
+    r = client.post("/password_reset/", data={"email": "webu@x.org", "csrfmiddlewaretoken": tok},
+                    follow_redirects=False)
     assert r.headers["location"] == "/password_reset/done/"
     box = os.path.join(client.settings.storage_root, "outbox")
     mail = open(os.path.join(box, sorted(os.listdir(box))[-1])).read()
     link = [w for w in mail.split() if w.startswith("/reset/")][0]
     newer = PW + "-3"
-    r = client.post(link, data={"new_password1": newer, "new_password2": newer}, follow_redirects=False)
+    tok = _csrf(client, link)
+    r = client.post(link, data={"new_password1": newer, "new_password2": newer, "csrfmiddlewaretoken": tok},
+                    follow_redirects=False)
     assert r.status_code == 302 and r.headers["location"] == "/reset/done/"
-    assert client.post(link, data={"new_password1": newer, "new_password2": newer}).status_code == 400  # one-shot
+    r = client.post(link, data={"new_password1": newer, "new_password2": newer, "csrfmiddlewaretoken": tok})
+    assert r.status_code == 400  # one-shot
     assert client.post("/rest-auth/login/", data={"username": "webu", "password": newer}).status_code == 200
     # staff admin index
-    client.post("/login/", data={"username": "boss", "password": PW})
+    tok = _csrf(client, "/login/")
+    client.post("/login/", data={"username": "boss", "password": PW, "csrfmiddlewaretoken": tok})
     r = client.get("/admin/")
     assert r.status_code == 200 and "Site administration" in r.text and "users" in r.text
     assert uid

@@ -229,3 +229,39 @@ def test_sync_bn_equals_full_batch():
         assert fwd_ok, r
         assert gdiff <= 1e-5 * max(1.0, gmax), (r, gdiff, gmax)
         assert run_ok, r
+
+
+def _agreed_error(rank, world, port, out):
+    """a peer-buffer timeout seen by ONE rank (here a fake poisoned channel on
+    rank 1) must raise on EVERY rank together, after the last log step too."""
+    from cloud_server_amd.parallel.dp import GradSync
+    from cloud_server_amd.parallel.dist import shutdown
+    ctx = _init(rank, world, port)
+    gs = GradSync(ctx, 16, "allreduce")
+
+    class _Ch:
+        def __init__(self, err):
+            self.err = err
+
+        def error(self):
+            return self.err
+
+    class _Comm:
+        channels = {"ar": _Ch(1 if rank == 1 else 0)}
+
+        def check(self):
+            pass
+
+    gs.check_agreed()                       # no channels: fine on every rank
+    gs.xgmi = _Comm()
+    try:
+        gs.check_agreed()
+        out[rank] = "no-raise"
+    except RuntimeError:
+        out[rank] = "raised"
+    shutdown(ctx)
+
+
+def test_xgmi_error_agreed_across_ranks():
+    out = _spawn(_agreed_error, 2)
+    assert out == {0: "raised", 1: "raised"}

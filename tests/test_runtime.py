@@ -316,3 +316,63 @@ def test_checkpoint_resume_across_flat_layouts():
     for n in a.model.state.shapes:
         torch.testing.assert_close(a.model.state.view(n, a.slots[0]), b.model.state.view(n, b.slots[0]))
         torch.testing.assert_close(a.model.state.view(n, a.flat), b.model.state.view(n, b.flat))
+
+
+def test_auto_restart_from_checkpoint(tmp_path, monkeypatch):
+    """SURVEY §5.3 recovery policy: a worker that fails after making progress is re-queued
+    and resumes from its newest checkpoint (bounded); the fault fires once here."""
+    s = _settings(tmp_path, "thread")
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    monkeypatch.setenv("CSA_FAULT_AT_STEP", "25")
+    monkeypatch.setenv("CSA_FAULT_ONCE", "1")
+    jm = JobManager(s, db, executor="thread", ngpu=0)
+    try:
+        mdir = _prep_model(s, uid, "m")
+        jid = jm.submit(uid, "m", "file", dict(SMALL, iter=30))
+        t0 = time.time()
+        while time.time() - t0 < 120:
+            st = db.get_job(jid)["state"]
+            if st in ("done", "failed"):
+                break
+            time.sleep(0.05)
+        assert db.get_job(jid)["state"] == "done"
+        assert "restart 1" in (db.get_job(jid)["error"] or "")  # recovered after restart 1
+        assert json.load(open(os.path.join(mdir, STATUS)))["step"] == 30
+    finally:
+        jm.shutdown()
+
+
+def test_fault_step_per_rank(monkeypatch, tmp_path):
+    from cloud_server_amd.runtime.trainer import _fault_step
+    monkeypatch.setenv("CSA_FAULT_AT_STEP", "1:7")
+    assert _fault_step(1, str(tmp_path)) == 7 and _fault_step(0, str(tmp_path)) == -1
+    monkeypatch.setenv("CSA_FAULT_AT_STEP", "9")
+    assert _fault_step(0, str(tmp_path)) == 9 and _fault_step(3, str(tmp_path)) == 9
+
+
+def test_tracing_ranges_wired(monkeypatch):
+    """CSA_TRACE=1 turns on ROCTx ranges around steps / collectives / logs
+    (the ROCTx library is part of the ROCm image; calls are no-ops without a profiler)."""
+    from cloud_server_amd.utils import tracing
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    monkeypatch.setenv("CSA_TRACE", "1")
+    monkeypatch.setattr(tracing, "_TRIED", False)
+    monkeypatch.setattr(tracing, "_ROCTX", None)
+    calls = []
+    real = tracing.trace_range
+
+    def spy(name):
+        calls.append(name)
+        return real(name)
+
+    import cloud_server_amd.runtime.engine as E
+    monkeypatch.setattr(E, "trace_range", spy)
+    train, _ = _data()
+    eng = TrainEngine(parse_train_config(SMALL), train, device="cpu")
+    eng.step()
+    eng.step()
+    assert calls.count("csa.step") == 2
+    assert tracing.enabled() == any(os.path.exists(os.path.join("/opt/rocm/lib", n))
+                                    for n in ("librocprofiler-sdk-roctx.so.1", "libroctx64.so.4"))
