@@ -468,6 +468,161 @@ __global__ __launch_bounds__(RT) void head_cols_kernel(HeadArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Row-group head with PARTIAL outputs (the fused-update step program): ceil(M / RG)
+// workgroups of 4 waves, RG <= 16 batch rows each; the waves split K (hidden features).
+// Every output has exactly one writer, so there are no atomics, no arrival counter and
+// nothing to zero:
+//   * dh rows [RG][K]            — plain stores (consumer: the last dense layer's backward);
+//   * dWh/dbh partial row g       — part[g][K*10 + 10] (the optimizer folds the G rows
+//                                   while it applies the head's update);
+//   * loss sum / #correct of g    — mpart[g], mcorr[g] (the optimizer writes the metric ring).
+// Block 0 advances the device step counter first thing, so every parameter update of the
+// step (fused dense updates, the optimizer) sees the same 1-based t (optim_common.h).
+// The row-group kernel above spent most of its 14.5 µs in ~20k same-line dWh atomics and
+// a last-arriver hand-off.
+// ---------------------------------------------------------------------------------
+constexpr int PRG_MAX = 16;        // rows per workgroup
+constexpr int PKL = 8;             // K elements per lane: K <= 4 waves * 64 lanes * PKL
+
+struct HeadPartArgs {
+  const float* h; int M, K, RG; int in_act; float in_alpha;
+  const float* w; const float* b;
+  const int64_t* labels; const int64_t* idx; const int64_t* cursor;
+  int loss; float grad_scale;
+  float* dh;                 // [M][K] or null
+  float* part;               // [G][K*10 + 10]
+  float* mpart; int* mcorr;  // [G]
+  float* logits_out;         // optional [M][10]
+  int64_t* step;
+};
+
+__global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
+  __shared__ float s_red[4][PRG_MAX * NCLS];     // per-wave logit partials
+  __shared__ float s_dl[PRG_MAX * NCLS];         // dlogits of the group
+  __shared__ float s_loss[PRG_MAX];
+  __shared__ int s_cor[PRG_MAX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = a.M, K = a.K, RG = a.RG;
+  const int g = blockIdx.x, m0 = g * RG, rows = min(RG, M - m0);
+  if (g == 0 && tid == 0) *a.step += 1;
+  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
+  // this lane's K elements: k = (e * 4 + wave) * 64 + lane  (coalesced per e, waves interleaved)
+  float wv[PKL][NCLS];
+  bool okk[PKL];
+#pragma unroll
+  for (int e = 0; e < PKL; ++e) {
+    const int k = (e * 4 + wave) * 64 + lane;
+    okk[e] = k < K;
+    const float* wr = a.w + (long)(okk[e] ? k : 0) * NCLS;
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) wv[e][j] = okk[e] ? wr[j] : 0.f;
+  }
+  int label = 0;
+  if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
+  // logits partials: per row, this lane's K slice, reduced over the wave then the waves
+  for (int r = 0; r < rows; ++r) {
+    float hv[PKL];
+#pragma unroll
+    for (int e = 0; e < PKL; ++e) {
+      const int k = (e * 4 + wave) * 64 + lane;
+      const float v = a.h[(long)(m0 + r) * K + (okk[e] ? k : 0)];
+      hv[e] = okk[e] ? act_fwd(v, a.in_act, a.in_alpha) : 0.f;
+    }
+    float acc[NCLS];
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) {
+      acc[j] = 0.f;
+#pragma unroll
+      for (int e = 0; e < PKL; ++e) acc[j] = fmaf(hv[e], wv[e][j], acc[j]);
+      acc[j] = wave_sum(acc[j]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) s_red[wave][r * NCLS + j] = acc[j];
+    }
+  }
+  __syncthreads();
+  // loss / dlogits / correct: one thread per row
+  if (tid < rows) {
+    float row[NCLS];
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j)
+      row[j] = s_red[0][tid * NCLS + j] + s_red[1][tid * NCLS + j] + s_red[2][tid * NCLS + j] +
+               s_red[3][tid * NCLS + j] + a.b[j];
+    float mx = row[0];
+    int am = 0;
+#pragma unroll
+    for (int j = 1; j < NCLS; ++j)
+      if (row[j] > mx) { mx = row[j]; am = j; }
+    if (a.logits_out) {
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) a.logits_out[(long)(m0 + tid) * NCLS + j] = row[j];
+    }
+    float ls = 0.f;
+    if (a.loss == 0) {
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) se += __expf(row[j] - mx);
+      const float lse = mx + __logf(se);
+      ls = lse - row[label];
+      const float inv = a.grad_scale / (float)M;
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) s_dl[tid * NCLS + j] = (__expf(row[j] - lse) - (j == label ? 1.f : 0.f)) * inv;
+    } else {
+      const float inv = 2.f * a.grad_scale / (float)(M * NCLS);
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) {
+        const float d = row[j] - (j == label ? 1.f : 0.f);
+        ls += d * d;
+        s_dl[tid * NCLS + j] = d * inv;
+      }
+    }
+    s_loss[tid] = ls;
+    s_cor[tid] = am == label;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float ls = 0.f;
+    int nc = 0;
+    for (int r = 0; r < rows; ++r) { ls += s_loss[r]; nc += s_cor[r]; }
+    a.mpart[g] = ls;
+    a.mcorr[g] = nc;
+  }
+  float* prow = a.part + (long)g * (K * NCLS + NCLS);
+  if (tid < NCLS) {            // dbh partial
+    float acc = 0.f;
+    for (int r = 0; r < rows; ++r) acc += s_dl[r * NCLS + tid];
+    prow[K * NCLS + tid] = acc;
+  }
+  // dWh partial[k][j] = sum_r T(h)[r][k] dl[r][j]; dh[r][k] = sum_j dl[r][j] Wh[k][j] * T'
+#pragma unroll
+  for (int e = 0; e < PKL; ++e) {
+    const int k = (e * 4 + wave) * 64 + lane;
+    if (!okk[e]) continue;
+    float dw[NCLS];
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) dw[j] = 0.f;
+    for (int r = 0; r < rows; ++r) {
+      const float hraw = a.h[(long)(m0 + r) * K + k];
+      const float hv = act_fwd(hraw, a.in_act, a.in_alpha);
+      float gv = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) {
+        const float d = s_dl[r * NCLS + j];
+        dw[j] = fmaf(hv, d, dw[j]);
+        gv = fmaf(d, wv[e][j], gv);
+      }
+      if (a.dh) {
+        if (a.in_act) gv = act_bwd(gv, hv, hv, a.in_act, a.in_alpha);
+        a.dh[(long)(m0 + r) * K + k] = gv;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) prow[k * NCLS + j] = dw[j];
+  }
+}
+
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.
 __global__ __launch_bounds__(HT) void head_generic_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -520,6 +675,26 @@ __global__ __launch_bounds__(HT) void head_generic_kernel(HeadArgs a) {
 }  // namespace csa
 
 using namespace csa;
+
+// Rows per workgroup of the partial-output head (0: shape outside its family).
+CSA_API int csa_head_part_rows(int M, int K) {
+  if (M < 1 || K < 1 || K > 4 * 64 * PKL) return 0;
+  int rg = 4;
+  while ((M + rg - 1) / rg > 16 && rg < PRG_MAX) rg *= 2;
+  return (M + rg - 1) / rg <= 16 ? rg : 0;
+}
+
+CSA_API int csa_head_part(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
+                          const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,
+                          int loss, float grad_scale, float* dh, float* part, float* mpart, int* mcorr,
+                          float* logits_out, int64_t* step, hipStream_t st) {
+  const int rg = csa_head_part_rows(M, K);
+  if (!rg) return -1;
+  HeadPartArgs a{h, M, K, rg, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, part,
+                 mpart, mcorr, logits_out, step};
+  hipLaunchKernelGGL(head_part_kernel, dim3((unsigned)((M + rg - 1) / rg)), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
 
 CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
                      const float* b, const int64_t* labels, const int64_t* idx, int loss,

@@ -2,49 +2,59 @@
 //
 // Reference: tf.train.AdagradOptimizer(1e-4).minimize (construct_distribute.py:372-373)
 // running ApplyAdagrad on the parameter server, plus the GD / Adam / Adadelta choices of
-// the option catalog (apps/construction/util/options.py:26-37).  All 2.28 M parameters of
-// the sample model live in one contiguous buffer, so the whole update is ONE launch of a
-// float4-vectorised streaming kernel (memory-bound: w, g, slots read, w, slots written).
+// the option catalog (apps/construction/util/options.py:26-37).  All parameters of a
+// model live in one contiguous buffer, so the update is ONE launch of a float4-vectorised
+// streaming kernel over a list of flat SEGMENTS — the whole buffer, or (with the fused
+// dense updates of dense_update.hip) only what those kernels did not already update.
+// The per-element rule is shared with the fused kernels (optim_common.h).
 //
 // Side jobs folded into the same launch (each would otherwise be its own tiny launch):
 //   * zero the split-K / atomic accumulators the NEXT step's kernels add into,
-//   * fold striped gradient accumulators: a conv weight gradient is accumulated by
-//     hundreds of workgroups into S stripes (S x fewer atomics per cache line, see
-//     conv.hip); the update of those parameters reads g = sum of the S stripes,
-//   * advance the batch-stream cursor.
+//   * fold striped / partial gradients: a conv weight gradient accumulated by hundreds of
+//     workgroups into S stripes, or the head's per-row-group partial dWh / dbh; the update
+//     of those parameters reads g = sum of the S rows,
+//   * write the step's metric-ring entry from the head's per-group loss / #correct,
+//   * advance the batch-stream cursor (mod its wrap).
 #include "common.h"
+#include "optim_common.h"
 
 namespace csa {
 
-enum Opt : int { OPT_SGD = 0, OPT_ADAGRAD = 1, OPT_ADAM = 2, OPT_ADADELTA = 3 };
-
 constexpr int MAXZ = 16;
 constexpr int MAXF = 8;
+constexpr int MAXSEG = 16;
 
 struct ZeroList { float* p[MAXZ]; long n[MAXZ]; int count; };
 
 // g[off + e] = sum_s src[s * ld + e] for e < n (flat-buffer offsets; off % 4 == 0);
-// the stripes are re-zeroed by the thread that folds them (their only reader)
-struct Fold { long off, n, ld; float* src; int S; };
+// zero != 0: the rows are accumulators that the fold re-zeroes (their only reader)
+struct Fold { long off, n, ld; float* src; int S; int zero; };
 struct FoldList { Fold f[MAXF]; int count; long lo, hi; };
 
 constexpr int MAXK = 8;
-// Gradient ranges whose producer STORES every element each step (e.g. a dense weight
-// gradient computed without split-K): the update need not re-zero them — for the sample
-// model that is fc1's 8 MB, ~15 % of the optimizer's memory traffic.
+// Gradient ranges whose producer STORES every element each step: the update need not
+// re-zero them.
 struct KeepList { long lo[MAXK], hi[MAXK]; int count; };
 
+struct SegList { long lo[MAXSEG]; long start4[MAXSEG + 1]; int count; };
+
+struct MetricFold {        // head partials -> ring[(step - 1) % ring]
+  const float* loss; const int* corr; int parts; float div;
+  float* ring_loss; int* ring_correct; int ring;
+};
+
 struct OptArgs {
-  int opt; float* w; const float* g; float* s0; float* s1; long n;
+  int opt; float* w; const float* g; float* s0; float* s1;
+  SegList seg;                     // flat segments to update
   float* gz;                       // if set (== g): each thread zeroes the gradient it read
   KeepList keep;                   // ... except inside these ranges (float4-aligned)
-  float lr; const int64_t* step;   // 1-based step AFTER the head kernel's increment
-  ZeroList z; FoldList fold;
+  float lr; const int64_t* step;   // 1-based step (the head kernel already advanced it)
+  ZeroList z; FoldList fold; MetricFold met;
   int64_t* cursor;                 // batch-stream cursor: += 1 (mod cursor_wrap) per step
   long cursor_wrap;
 };
 
-constexpr int MAXS = 16;   // stripes per folded gradient
+constexpr int MAXS = 16;   // stripes / partial rows per folded gradient
 
 __device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g) {
   float gs[4] = {g.x, g.y, g.z, g.w};
@@ -62,7 +72,7 @@ __device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g
 #pragma unroll
       for (int s2 = 0; s2 < MAXS; ++s2) {
         acc.x += v[s2].x; acc.y += v[s2].y; acc.z += v[s2].z; acc.w += v[s2].w;
-        if (s2 < f.S) *reinterpret_cast<float4*>(f.src + s2 * f.ld + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (f.zero && s2 < f.S) *reinterpret_cast<float4*>(f.src + s2 * f.ld + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       gs[0] = acc.x; gs[1] = acc.y; gs[2] = acc.z; gs[3] = acc.w;
       continue;
@@ -78,7 +88,7 @@ __device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g
 #pragma unroll
       for (int s2 = 0; s2 < MAXS; ++s2) {
         acc += v[s2];
-        if (s2 < f.S) f.src[s2 * f.ld + i] = 0.f;
+        if (f.zero && s2 < f.S) f.src[s2 * f.ld + i] = 0.f;
       }
       gs[j] = acc;
     }
@@ -89,69 +99,39 @@ __device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long nth = (long)gridDim.x * blockDim.x;
-  float lr = a.lr;
-  if (a.opt == OPT_ADAM) {
-    const float t = (float)(*a.step);
-    lr = a.lr * sqrtf(1.f - powf(0.999f, t)) / (1.f - powf(0.9f, t));
-  }
-  const long n4 = a.n >> 2;
+  const float lr = opt_step_lr(a.opt, a.lr, a.step);
+  const long n4 = a.seg.start4[a.seg.count];
   float4* w4 = (float4*)a.w;
   const float4* g4 = (const float4*)a.g;
   float4* s04 = (float4*)a.s0;
   float4* s14 = (float4*)a.s1;
-  for (long i = tid; i < n4; i += nth) {
+  const int nslot = opt_nslots(a.opt);
+  for (long t = tid; t < n4; t += nth) {
+    int k = 0;
+    for (int j = 1; j < a.seg.count; ++j) k = t >= a.seg.start4[j] ? j : k;
+    const long i = (a.seg.lo[k] >> 2) + (t - a.seg.start4[k]);   // float4 index in the flat buffer
     float4 w = w4[i];
     float4 g = g4[i];
+    float4 s0 = nslot >= 1 ? s04[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s1 = nslot >= 2 ? s14[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     // Zeroing the accumulators the next step adds into must not race with this read:
     // a zero-list pass over flat-gradient ranges run by OTHER threads could clear an
     // element before its owner read it, so the owner clears what it read.
     if (a.gz) {
       bool keep = false;
-      for (int k = 0; k < a.keep.count; ++k) keep |= (i * 4 >= a.keep.lo[k]) & (i * 4 < a.keep.hi[k]);
+      for (int q = 0; q < a.keep.count; ++q) keep |= (i * 4 >= a.keep.lo[q]) & (i * 4 < a.keep.hi[q]);
       if (!keep) reinterpret_cast<float4*>(a.gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (i * 4 + 3 >= a.fold.lo && i * 4 < a.fold.hi) g = fold_grad(a.fold, i * 4, g);
     float* wp = (float*)&w;
     const float* gp = (const float*)&g;
-    if (a.opt == OPT_SGD) {
+    float* sp0 = (float*)&s0;
+    float* sp1 = (float*)&s1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wp[j] -= lr * gp[j];
-    } else if (a.opt == OPT_ADAGRAD) {
-      float4 s = s04[i];
-      float* sp = (float*)&s;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sp[j] += gp[j] * gp[j];
-        wp[j] -= lr * gp[j] * rsqrtf(sp[j]);
-      }
-      s04[i] = s;
-    } else if (a.opt == OPT_ADAM) {
-      float4 m = s04[i], v = s14[i];
-      float* mp = (float*)&m;
-      float* vp = (float*)&v;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        mp[j] = 0.9f * mp[j] + 0.1f * gp[j];
-        vp[j] = 0.999f * vp[j] + 0.001f * gp[j] * gp[j];
-        wp[j] -= lr * mp[j] / (sqrtf(vp[j]) + 1e-8f);
-      }
-      s04[i] = m;
-      s14[i] = v;
-    } else {  // Adadelta (TF: rho 0.95, eps 1e-8)
-      float4 acc = s04[i], au = s14[i];
-      float* ap = (float*)&acc;
-      float* up = (float*)&au;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ap[j] = 0.95f * ap[j] + 0.05f * gp[j] * gp[j];
-        const float upd = sqrtf(up[j] + 1e-8f) / sqrtf(ap[j] + 1e-8f) * gp[j];
-        up[j] = 0.95f * up[j] + 0.05f * upd * upd;
-        wp[j] -= lr * upd;
-      }
-      s04[i] = acc;
-      s14[i] = au;
-    }
+    for (int j = 0; j < 4; ++j) opt_update(a.opt, lr, wp[j], gp[j], sp0[j], sp1[j]);
     w4[i] = w;
+    if (nslot >= 1) s04[i] = s0;
+    if (nslot >= 2) s14[i] = s1;
   }
   // zero accumulators for the next step
   for (int z = 0; z < a.z.count; ++z) {
@@ -159,9 +139,19 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const long n = a.z.n[z];
     for (long i = tid; i < n; i += nth) p[i] = 0.f;
   }
-  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) {
-    const int64_t c = *a.cursor + 1;
-    *a.cursor = (a.cursor_wrap > 0 && c >= a.cursor_wrap) ? 0 : c;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (a.met.parts > 0) {
+      float ls = 0.f;
+      int nc = 0;
+      for (int p = 0; p < a.met.parts; ++p) { ls += a.met.loss[p]; nc += a.met.corr[p]; }
+      const int pos = (int)((*a.step - 1) % a.met.ring);
+      a.met.ring_loss[pos] = ls / a.met.div;
+      a.met.ring_correct[pos] = nc;
+    }
+    if (a.cursor) {
+      const int64_t c = *a.cursor + 1;
+      *a.cursor = (a.cursor_wrap > 0 && c >= a.cursor_wrap) ? 0 : c;
+    }
   }
 }
 
@@ -169,16 +159,20 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
 
 using namespace csa;
 
-// zero_ptrs/zero_ns: count <= 16 regions; fold_*: count <= 8 striped-gradient descriptors.
+// Segments seg_lo/seg_hi (count <= 16, float4-aligned; nseg == 0: the whole [0, n)).
+// zero_ptrs/zero_ns: count <= 16 regions; fold_*: count <= 8 striped/partial descriptors.
 // zero_grad != 0: the update clears g[i] after reading it (g is then an accumulator that
 // must start the next step at zero); zero_ptrs must NOT overlap g or the fold stripes.
-CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, long n, int zero_grad,
-                          float lr, const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
-                          int nzero, const long* fold_off, const long* fold_n, float* const* fold_src,
-                          const int* fold_S, const long* fold_ld, int nfold, const long* keep_lo,
-                          const long* keep_hi, int nkeep, int64_t* cursor, long cursor_wrap,
-                          hipStream_t st) {
-  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK) return -1;
+// met_parts > 0: write the metric ring from the head's partial loss / #correct.
+CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, long n, const long* seg_lo,
+                           const long* seg_hi, int nseg, int zero_grad, float lr, const int64_t* step,
+                           float* const* zero_ptrs, const long* zero_ns, int nzero, const long* fold_off,
+                           const long* fold_n, float* const* fold_src, const int* fold_S, const long* fold_ld,
+                           const int* fold_zero, int nfold, const long* keep_lo, const long* keep_hi, int nkeep,
+                           const float* met_loss, const int* met_corr, int met_parts, float met_div,
+                           float* ring_loss, int* ring_correct, int ring, int64_t* cursor, long cursor_wrap,
+                           hipStream_t st) {
+  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG) return -1;
   OptArgs a{};
   a.keep.count = nkeep;
   for (int i = 0; i < nkeep; ++i) {
@@ -186,9 +180,17 @@ CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, lon
     a.keep.lo[i] = keep_lo[i];
     a.keep.hi[i] = keep_hi[i];
   }
+  a.seg.count = nseg > 0 ? nseg : 1;
+  a.seg.start4[0] = 0;
+  for (int i = 0; i < a.seg.count; ++i) {
+    const long lo = nseg > 0 ? seg_lo[i] : 0, hi = nseg > 0 ? seg_hi[i] : n;
+    if (lo % 4 || hi % 4 || hi < lo || hi > n) return -4;
+    a.seg.lo[i] = lo;
+    a.seg.start4[i + 1] = a.seg.start4[i] + (hi - lo) / 4;
+  }
   a.cursor = cursor;
   a.cursor_wrap = cursor_wrap;
-  a.opt = opt; a.w = w; a.g = g; a.s0 = s0; a.s1 = s1; a.n = n; a.lr = lr; a.step = step;
+  a.opt = opt; a.w = w; a.g = g; a.s0 = s0; a.s1 = s1; a.lr = lr; a.step = step;
   a.gz = zero_grad ? g : nullptr;
   a.z.count = nzero;
   for (int i = 0; i < nzero; ++i) { a.z.p[i] = zero_ptrs[i]; a.z.n[i] = zero_ns[i]; }
@@ -197,16 +199,31 @@ CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, lon
   a.fold.hi = 0;
   for (int i = 0; i < nfold; ++i) {
     if (fold_off[i] % 4 || fold_S[i] > MAXS || fold_S[i] < 1) return -1;
-    a.fold.f[i] = Fold{fold_off[i], fold_n[i], fold_ld[i], fold_src[i], fold_S[i]};
+    a.fold.f[i] = Fold{fold_off[i], fold_n[i], fold_ld[i], fold_src[i], fold_S[i], fold_zero ? fold_zero[i] : 1};
     a.fold.lo = fold_off[i] < a.fold.lo ? fold_off[i] : a.fold.lo;
     a.fold.hi = fold_off[i] + fold_n[i] > a.fold.hi ? fold_off[i] + fold_n[i] : a.fold.hi;
   }
-  long n4 = n / 4;
-  int blocks = (int)((n4 + 255) / 256);
+  a.met = MetricFold{met_loss, met_corr, met_parts, met_div, ring_loss, ring_correct, ring};
+  const long n4 = a.seg.start4[a.seg.count];
+  long zmax = 0;
+  for (int i = 0; i < nzero; ++i) zmax = zero_ns[i] > zmax ? zero_ns[i] : zmax;
+  const long work = n4 > zmax ? n4 : zmax;
+  int blocks = (int)((work + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(optim_kernel, dim3(blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
+}
+
+// Backward-compatible entry: the whole buffer, the head wrote the metric ring itself.
+CSA_API int csa_optimizer(int opt, float* w, float* g, float* s0, float* s1, long n, int zero_grad,
+                          float lr, const int64_t* step, float* const* zero_ptrs, const long* zero_ns,
+                          int nzero, const long* fold_off, const long* fold_n, float* const* fold_src,
+                          const int* fold_S, const long* fold_ld, int nfold, const long* keep_lo,
+                          const long* keep_hi, int nkeep, int64_t* cursor, long cursor_wrap, hipStream_t st) {
+  return csa_optimizer2(opt, w, g, s0, s1, n, nullptr, nullptr, 0, zero_grad, lr, step, zero_ptrs, zero_ns, nzero,
+                        fold_off, fold_n, fold_src, fold_S, fold_ld, nullptr, nfold, keep_lo, keep_hi, nkeep,
+                        nullptr, nullptr, 0, 1.f, nullptr, nullptr, 1, cursor, cursor_wrap, st);
 }
 
 // Zero a list of regions (used once at init and by tests).

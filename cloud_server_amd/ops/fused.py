@@ -48,6 +48,14 @@ _SIGS = {
                                P, P, P, P, I, F, P, I, F, F, P, P, P, I, P, P, P, P, F, P]),
     "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P, P]),
     "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P, I, P, L, P]),
+    "csa_optimizer2": (I, [I, P, P, P, P, L, P, P, I, I, F, P, P, P, I, P, P, P, P, P, P, I, P, P, I,
+                           P, P, I, F, P, P, I, P, L, P]),
+    "csa_dense_bwd_update_ok": (I, [I, I, I, I]),
+    "csa_dense_bwd_update_slabs": (I, [I]),
+    "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
+                                 P, P, P, P, F, P]),
+    "csa_head_part_rows": (I, [I, I]),
+    "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),

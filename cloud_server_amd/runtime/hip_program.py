@@ -106,12 +106,17 @@ class HipProgram:
         self.views = eng.model.state.views(eng.flat)
         self.gviews = eng.model.state.views(eng.flat_grad)
         self._lower()
+        self._plan_fused()
         self._alloc()
         self._plan_lowrank()
         self.zero_regions: List[torch.Tensor] = []
         self._collect_zero_regions()
         self._zero_now()
         self._plan_grad_buckets()
+        self.opt_segments = self._opt_segments()
+        nfold = sum(1 + (u.db_acc is not None) for u in self.units if u.kind == "conv" and u.wg_stripes > 1)
+        if nfold + (2 if self.head_rg else 0) > 8:
+            raise Unsupported("more than 8 striped gradients")
 
     # ------------------------------------------------------------------ DP overlap
     def _plan_grad_buckets(self) -> None:
@@ -255,6 +260,36 @@ class HipProgram:
         with torch.cuda.stream(self.side):
             self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
 
+    # ------------------------------------------------------------------ fused updates
+    def _plan_fused(self) -> None:
+        """On one GPU the dense weight gradients feed nothing but the optimizer: such a
+        layer's backward becomes ``csa_dense_bwd_update`` (dgrad + wgrad + the optimizer
+        update of its W rows in one launch, dense_update.hip) and the head writes
+        per-row-group partial gradients + metrics that the (now small) optimizer launch
+        folds (``csa_head_part``).  Data parallel keeps the materialised gradients: they
+        must be all-reduced before any update."""
+        e, B = self.e, self.B
+        self.fused = (not e.ctx.enabled) and os.environ.get("CSA_FUSED_UPDATE", "1") == "1"
+        for u in self.units:
+            u.fused = False
+            if not self.fused or u.kind != "dense":
+                continue
+            tf = u.in_tf
+            fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
+            if tf.has_bn and fin % 4:            # the BN'd input is not materialised (see _alloc)
+                continue
+            if tf.act is not None and not tf.has_bn:
+                continue                         # weight-gradient operand would need the act
+            C = tf.norm.in_shape.c if tf.has_bn else 0
+            u.fused = bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C))
+        self.head_rg = 0
+        if self.fused and self.head_tf.norm is None:
+            last = self.units[-1]
+            K = last.layer.spec.hidden if last.kind == "dense" else last.layer.out_shape.numel
+            if last.kind == "conv" and last.pool is not None:
+                K = last.pool.out_shape.numel
+            self.head_rg = int(self.lib.csa_head_part_rows(B, K))
+
     # ------------------------------------------------------------------ lowering
     def _lower(self) -> None:
         layers = self.e.model.plan.layers
@@ -344,7 +379,9 @@ class HipProgram:
                 tf.count = float(B * ph * pw * self.W)
                 # backward slab is produced by THIS unit's dgrad
                 C = src.y.shape[3]
-                if u.kind == "dense":
+                if u.kind == "dense" and u.fused:
+                    nb = self.lib.csa_dense_bwd_update_slabs(u.layer.in_shape.numel)
+                elif u.kind == "dense":
                     nb = self.lib.csa_dense_dgrad_slabs(B, u.layer.in_shape.numel, u.layer.spec.hidden)
                 else:
                     nb = self.lib.csa_conv_dgrad_nslab(self._conv_geom(u.layer, B))
@@ -357,6 +394,12 @@ class HipProgram:
                 u.xt = torch.zeros(B, u.layer.in_shape.numel, **f32)
         self.dlast = self.units[-1].dy     # head input grad
         self.idx = None
+        if self.head_rg:
+            K = self.dlast[0].numel()
+            G = -(-B // self.head_rg)
+            self.head_part = torch.zeros(G, K * 10 + 10, **f32)     # per-group dWh | dbh
+            self.head_mloss = torch.zeros(G, **f32)
+            self.head_mcorr = torch.zeros(G, dtype=torch.int32, device=dev)
 
     def _collect_zero_regions(self) -> None:
         """Accumulators that must start every step at zero.  ``zero_regions`` are cleared
@@ -376,6 +419,8 @@ class HipProgram:
                 u.splits_fwd = self.lib.csa_dense_fwd_splits(B, fout, fin)
                 if u.splits_fwd > 1:
                     regs.append(u.y)
+                if u.fused:
+                    continue                     # plain stores; W never has a gradient buffer
                 if k > 0:
                     tfm = u.in_tf.has_bn or u.in_tf.act is not None
                     if self.lib.csa_dense_dgrad_splits(B, fin, fout, int(tfm)) > 1:
@@ -403,8 +448,10 @@ class HipProgram:
                     pk, ps = u.pool.spec.kernel, u.pool.spec.stride
                     if tuple(pk) != tuple(ps):
                         regs.append(u.dc.view(-1))
-        # the head accumulates dWh/dbh across its row-group workgroups
-        flat.append(self.e.flat_grad[self.e.model.state.offsets["head.weight"]:])
+        # the atomic head accumulates dWh/dbh across its row-group workgroups (the
+        # partial-output head of the fused program writes per-group rows instead)
+        if not self.head_rg:
+            flat.append(self.e.flat_grad[self.e.model.state.offsets["head.weight"]:])
         self.head_ws = torch.zeros(4, dtype=torch.int32, device=self.e.device)   # arrival counter + sums
         for u in self.units:
             if u.in_tf.has_bn:
@@ -417,7 +464,7 @@ class HipProgram:
         self.keep_ranges = []
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind != "dense":
+            if u.kind != "dense" or u.fused:
                 continue
             fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
             m = B * (self.e.ctx.world if u in getattr(self, "lr_units", []) else 1)
@@ -525,13 +572,21 @@ class HipProgram:
         # ---------------- head (loss, head grads, input grad, metrics) ----------------
         last = self.units[-1]
         hin = last.y.view(B, -1)
-        self._rc(lib.csa_head(
-            K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
-            K.ptr(V["head.weight"]), K.ptr(V["head.bias"]), K.ptr(e.data.labels), K.ptr(rows),
-            0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
-            K.ptr(G["head.weight"]), K.ptr(G["head.bias"]), K.ptr(last.dy), None,
-            K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(),
-            K.ptr(cur), K.ptr(self.head_ws), st), "head")
+        if self.head_rg:
+            self._rc(lib.csa_head_part(
+                K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
+                K.ptr(V["head.weight"]), K.ptr(V["head.bias"]), K.ptr(e.data.labels), K.ptr(rows), K.ptr(cur),
+                0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale), K.ptr(last.dy),
+                K.ptr(self.head_part), K.ptr(self.head_mloss), K.ptr(self.head_mcorr), None, K.ptr(e.dstep), st),
+                "head_part")
+        else:
+            self._rc(lib.csa_head(
+                K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
+                K.ptr(V["head.weight"]), K.ptr(V["head.bias"]), K.ptr(e.data.labels), K.ptr(rows),
+                0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
+                K.ptr(G["head.weight"]), K.ptr(G["head.bias"]), K.ptr(last.dy), None,
+                K.ptr(e.dstep), K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel(),
+                K.ptr(cur), K.ptr(self.head_ws), st), "head")
         self._grad_ready("head")
 
         # ---------------- backward ----------------
@@ -547,6 +602,9 @@ class HipProgram:
                 e.sync.allreduce_tensors([self.units[k + 1].in_tf.bwd_slab], tag=f"bnb{k + 1}")
             if u.kind == "dense":
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if u.fused:
+                    self._dense_bwd_update(u, prev, st)
+                    continue
                 if (prev is not None and u not in self.lr_units and not self.wsplit
                         and self._dense_bwd_fused(u, prev, st)):
                     self._grad_ready(k)          # dgrad + wgrad in one launch
@@ -711,6 +769,53 @@ class HipProgram:
             raise RuntimeError(f"dense_bwd failed: {rc}")
         return rc > 0
 
+    def _dense_bwd_update(self, u: Unit, prev: Optional[Unit], st) -> None:
+        """Dense backward + optimizer update of W / b in one launch (dense_update.hip)."""
+        e, lib, B = self.e, self.lib, self.B
+        lp, tf = u.layer, u.in_tf
+        fin, fout = lp.in_shape.numel, lp.spec.hidden
+        offs = self.model.state.offsets
+        ow, ob = offs[f"{lp.name}.weight"], offs[f"{lp.name}.bias"]
+        sl = e.slots
+        s0 = sl[0] if sl.shape[0] > 0 else None
+        s1 = sl[1] if sl.shape[0] > 1 else None
+        xw = u.xt if u.xt is not None else u.x.view(B, -1)
+        self._rc(lib.csa_dense_bwd_update(
+            K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
+            K.ptr(prev.dy) if prev is not None else None, B, fin, fout,
+            K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
+            K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
+            K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
+            K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
+            1.0, st), "dense_bwd_update")
+
+    def _opt_segments(self):
+        """Flat [lo, hi) spans the optimizer launch updates: everything except the
+        parameters a fused dense backward already updated (spans padded to float4; the
+        flat layout's alignment padding is zero and stays zero)."""
+        n = self.e.flat.numel()
+        offs = self.model.state.offsets
+        spans = sorted(offs.values())
+        ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
+        skip = set()
+        for u in self.units:
+            if u.kind == "dense" and u.fused:
+                skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
+        if not skip:
+            return []
+        segs: List[list] = []
+        for o in spans:
+            if o in skip:
+                continue
+            lo, hi = o - o % 4, -(-ends[o] // 4) * 4
+            if segs and segs[-1][1] >= lo:
+                segs[-1][1] = max(segs[-1][1], hi)
+            else:
+                segs.append([lo, hi])
+        if len(segs) > 16:
+            raise Unsupported("more than 16 optimizer segments")
+        return segs
+
     def _optimizer(self, st) -> None:
         e, lib = self.e, self.lib
         lo, hi = e.sync.shard_range()
@@ -722,28 +827,43 @@ class HipProgram:
         s1 = e.slots[1] if e.slots.shape[0] > 1 else None
         zp = (C.c_void_p * 16)(*[r.data_ptr() for r in self.zero_regions])
         zn = (C.c_long * 16)(*[r.numel() for r in self.zero_regions])
-        folds = []          # striped conv weight gradients -> summed inside the update
+        folds = []          # striped conv weight gradients / head partials -> summed inside the update
         offs = self.model.state.offsets
         for u in self.units:
             if u.kind == "conv" and u.wg_stripes > 1:
                 lp = u.layer
-                folds.append((offs[f"{lp.name}.weight"], u.dw_acc.shape[1], u.dw_acc, u.wg_stripes))
+                folds.append((offs[f"{lp.name}.weight"], u.dw_acc.shape[1], u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], 1))
                 if u.db_acc is not None:
-                    folds.append((offs[f"{lp.name}.bias"], u.db_acc.shape[1], u.db_acc, u.wg_stripes))
+                    folds.append((offs[f"{lp.name}.bias"], u.db_acc.shape[1], u.db_acc, u.wg_stripes, u.db_acc.shape[1], 1))
+        if self.head_rg:
+            hp = self.head_part
+            kw = hp.shape[1] - 10
+            folds.append((offs["head.weight"], kw, hp, hp.shape[0], hp.shape[1], 0))
+            folds.append((offs["head.bias"], 10, hp[:, kw:], hp.shape[0], hp.shape[1], 0))
         if len(folds) > 8:
             raise Unsupported("more than 8 striped gradients")
         fo = (C.c_long * 8)(*[f[0] for f in folds])
         fn = (C.c_long * 8)(*[f[1] for f in folds])
         fs = (C.c_void_p * 8)(*[f[2].data_ptr() for f in folds])
         fS = (C.c_int * 8)(*[f[3] for f in folds])
-        fl = (C.c_long * 8)(*[f[1] for f in folds])
+        fl = (C.c_long * 8)(*[f[4] for f in folds])
+        fz = (C.c_int * 8)(*[f[5] for f in folds])
         keep = self.keep_ranges[:8]
         klo = (C.c_long * 8)(*[k[0] for k in keep])
         khi = (C.c_long * 8)(*[k[1] for k in keep])
-        self._rc(lib.csa_optimizer(
-            e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), 0 if self.ps_mode else 1,
-            float(e.lr), K.ptr(e.dstep),
-            zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, len(folds), klo, khi, len(keep),
-            K.ptr(e.stream.cursor), e.stream.wrap, st), "optimizer")
+        segs = self.opt_segments
+        slo = (C.c_long * 16)(*[x[0] for x in segs])
+        shi = (C.c_long * 16)(*[x[1] for x in segs])
+        if self.head_rg:
+            div = float(self.B if e.cfg.loss_name == "entropy" else self.B * 10)
+            met = (K.ptr(self.head_mloss), K.ptr(self.head_mcorr), self.head_mloss.numel(), div,
+                   K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel())
+        else:
+            met = (None, None, 0, 1.0, None, None, 1)
+        self._rc(lib.csa_optimizer2(
+            e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), slo, shi, len(segs),
+            0 if self.ps_mode else 1, float(e.lr), K.ptr(e.dstep),
+            zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, fz, len(folds), klo, khi, len(keep),
+            *met, K.ptr(e.stream.cursor), e.stream.wrap, st), "optimizer")
         if e.sync.strategy == "ps" and e.ctx.enabled:
             e.sync.all_gather_params(e.flat)

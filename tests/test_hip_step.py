@@ -140,3 +140,29 @@ def test_batch_sizes_match_torch(batch):
         a, b = eh.model.state.view(k, gh), et.model.state.view(k, gt)
         scale = b.abs().max().item() + 1e-6
         assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6, f"batch {batch} grad {k}"
+
+
+def test_fused_update_path_active_and_matches_unfused(monkeypatch):
+    """Single-GPU program: the dense layers' backward applies the optimizer in-kernel
+    (csa_dense_bwd_update) and the head writes partial gradients folded by the small
+    optimizer launch.  Several Adam / Adagrad steps match the unfused program (materialised
+    gradients + the flat optimizer) and the metric ring agrees."""
+    ds = synthetic_mnist(600, seed=17)
+    for opt in ("AdamOptimizer", "AdagradOptimizer"):
+        cfg = _cfg(CASES["sample"], optimizer=opt, lr=1e-3)
+        monkeypatch.setenv("CSA_FUSED_UPDATE", "1")
+        a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
+        monkeypatch.setenv("CSA_FUSED_UPDATE", "0")
+        b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
+        assert a.program.fused and a.program.head_rg > 0
+        assert [u.fused for u in a.program.units if u.kind == "dense"] == [True, True]
+        assert not b.program.fused
+        for _ in range(5):
+            a.step()
+            b.step()
+        torch.cuda.synchronize()
+        d = (a.flat - b.flat).abs().max().item()
+        assert d < 2e-4, f"{opt}: fused vs unfused params differ by {d}"
+        ma, mb = a.metrics_since(0), b.metrics_since(0)
+        assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
+        assert int(a.dstep.item()) == int(b.dstep.item()) == 5
