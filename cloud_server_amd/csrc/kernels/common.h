@@ -76,6 +76,12 @@ __device__ __forceinline__ void stage_to_lds(float* dst, const T* src, int n, F 
   }
 }
 
+// Materialise loaded values here (the empty asm "reads and writes" them): hipcc otherwise
+// sinks each load into the conditional block that consumes it and waits for it there, one
+// serial memory round trip per element.  Pin a batch of loads after issuing all of them.
+__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

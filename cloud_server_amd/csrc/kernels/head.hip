@@ -483,7 +483,7 @@ __global__ __launch_bounds__(RT) void head_cols_kernel(HeadArgs a) {
 // a last-arriver hand-off.
 // ---------------------------------------------------------------------------------
 constexpr int PRG_MAX = 16;        // rows per workgroup
-constexpr int PKL = 8;             // K elements per lane: K <= 4 waves * 64 lanes * PKL
+constexpr size_t PHEAD_LDS_MAX = 150 * 1024;
 
 struct HeadPartArgs {
   const float* h; int M, K, RG; int in_act; float in_alpha;
@@ -497,49 +497,72 @@ struct HeadPartArgs {
   int64_t* step;
 };
 
+__host__ __device__ inline size_t head_part_lds(int RG, int K) {
+  return ((size_t)RG * K + (size_t)K * NCLS + (size_t)PRG_MAX * NCLS * 2) * sizeof(float);
+}
+
+// Stages the group's T(h) rows and Wh in LDS (one batched round trip: every load of a
+// thread in flight, pinned, then the stores), then everything runs from LDS.
 __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
-  __shared__ float s_red[4][PRG_MAX * NCLS];     // per-wave logit partials
-  __shared__ float s_dl[PRG_MAX * NCLS];         // dlogits of the group
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float s_loss[PRG_MAX];
   __shared__ int s_cor[PRG_MAX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = a.M, K = a.K, RG = a.RG;
   const int g = blockIdx.x, m0 = g * RG, rows = min(RG, M - m0);
+  float* s_h = smem;                       // [RG][K]  T(h)
+  float* s_w = s_h + RG * K;               // [K][10]
+  float* s_lg = s_w + K * NCLS;            // [PRG_MAX][10] logits
+  float* s_dl = s_lg + PRG_MAX * NCLS;     // [PRG_MAX][10] dlogits
   if (g == 0 && tid == 0) *a.step += 1;
   const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
-  // this lane's K elements: k = (e * 4 + wave) * 64 + lane  (coalesced per e, waves interleaved)
-  float wv[PKL][NCLS];
-  bool okk[PKL];
-#pragma unroll
-  for (int e = 0; e < PKL; ++e) {
-    const int k = (e * 4 + wave) * 64 + lane;
-    okk[e] = k < K;
-    const float* wr = a.w + (long)(okk[e] ? k : 0) * NCLS;
-#pragma unroll
-    for (int j = 0; j < NCLS; ++j) wv[e][j] = okk[e] ? wr[j] : 0.f;
-  }
   int label = 0;
   if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
-  // logits partials: per row, this lane's K slice, reduced over the wave then the waves
-  for (int r = 0; r < rows; ++r) {
-    float hv[PKL];
+  {
+    const int K4 = K >> 2, nh4 = rows * K4, nw4 = (K * NCLS) >> 2, tot = nh4 + nw4;
+    const float4* h4 = reinterpret_cast<const float4*>(a.h + (long)m0 * K);
+    const float4* w4 = reinterpret_cast<const float4*>(a.w);
+    constexpr int U = 16;
+    for (int base = 0; base < tot; base += 256 * U) {
+      float4 v[U];
 #pragma unroll
-    for (int e = 0; e < PKL; ++e) {
-      const int k = (e * 4 + wave) * 64 + lane;
-      const float v = a.h[(long)(m0 + r) * K + (okk[e] ? k : 0)];
-      hv[e] = okk[e] ? act_fwd(v, a.in_act, a.in_alpha) : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int e = min(base + u * 256 + tid, tot - 1);
+        const float4* src = e < nh4 ? h4 + e : w4 + (e - nh4);
+        v[u] = *src;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) pin(v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * 256 + tid;
+        if (e < nh4) {
+          float4 t = v[u];
+          t.x = act_fwd(t.x, a.in_act, a.in_alpha); t.y = act_fwd(t.y, a.in_act, a.in_alpha);
+          t.z = act_fwd(t.z, a.in_act, a.in_alpha); t.w = act_fwd(t.w, a.in_act, a.in_alpha);
+          reinterpret_cast<float4*>(s_h)[e] = t;
+        } else if (e < tot) {
+          reinterpret_cast<float4*>(s_w)[e - nh4] = v[u];
+        }
+      }
     }
+  }
+  __syncthreads();
+  // logits: wave w takes rows w, w+4, ...; lanes split K, then a wave reduction per class
+  for (int r = wave; r < rows; r += 4) {
     float acc[NCLS];
 #pragma unroll
-    for (int j = 0; j < NCLS; ++j) {
-      acc[j] = 0.f;
+    for (int j = 0; j < NCLS; ++j) acc[j] = 0.f;
+    for (int k = lane; k < K; k += 64) {
+      const float hv = s_h[r * K + k];
+      const float* wr = s_w + k * NCLS;
 #pragma unroll
-      for (int e = 0; e < PKL; ++e) acc[j] = fmaf(hv[e], wv[e][j], acc[j]);
-      acc[j] = wave_sum(acc[j]);
+      for (int j = 0; j < NCLS; ++j) acc[j] = fmaf(hv, wr[j], acc[j]);
     }
-    if (lane == 0) {
 #pragma unroll
-      for (int j = 0; j < NCLS; ++j) s_red[wave][r * NCLS + j] = acc[j];
+    for (int j = 0; j < NCLS; ++j) {
+      const float t = wave_sum(acc[j]);
+      if (lane == 0) s_lg[r * NCLS + j] = t;
     }
   }
   __syncthreads();
@@ -547,9 +570,7 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
   if (tid < rows) {
     float row[NCLS];
 #pragma unroll
-    for (int j = 0; j < NCLS; ++j)
-      row[j] = s_red[0][tid * NCLS + j] + s_red[1][tid * NCLS + j] + s_red[2][tid * NCLS + j] +
-               s_red[3][tid * NCLS + j] + a.b[j];
+    for (int j = 0; j < NCLS; ++j) row[j] = s_lg[tid * NCLS + j] + a.b[j];
     float mx = row[0];
     int am = 0;
 #pragma unroll
@@ -595,26 +616,22 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
     for (int r = 0; r < rows; ++r) acc += s_dl[r * NCLS + tid];
     prow[K * NCLS + tid] = acc;
   }
-  // dWh partial[k][j] = sum_r T(h)[r][k] dl[r][j]; dh[r][k] = sum_j dl[r][j] Wh[k][j] * T'
+  // one thread per k: dWh partial[k][:] and dh[:][k]
+  for (int k = tid; k < K; k += 256) {
+    float dw[NCLS], wk[NCLS];
 #pragma unroll
-  for (int e = 0; e < PKL; ++e) {
-    const int k = (e * 4 + wave) * 64 + lane;
-    if (!okk[e]) continue;
-    float dw[NCLS];
-#pragma unroll
-    for (int j = 0; j < NCLS; ++j) dw[j] = 0.f;
+    for (int j = 0; j < NCLS; ++j) { dw[j] = 0.f; wk[j] = s_w[k * NCLS + j]; }
     for (int r = 0; r < rows; ++r) {
-      const float hraw = a.h[(long)(m0 + r) * K + k];
-      const float hv = act_fwd(hraw, a.in_act, a.in_alpha);
+      const float hv = s_h[r * K + k];
       float gv = 0.f;
 #pragma unroll
       for (int j = 0; j < NCLS; ++j) {
         const float d = s_dl[r * NCLS + j];
         dw[j] = fmaf(hv, d, dw[j]);
-        gv = fmaf(d, wv[e][j], gv);
+        gv = fmaf(d, wk[j], gv);
       }
       if (a.dh) {
-        if (a.in_act) gv = act_bwd(gv, hv, hv, a.in_act, a.in_alpha);
+        if (a.in_act) gv = act_bwd(gv, hv, hv, a.in_act, a.in_alpha);   // post-activation value
         a.dh[(long)(m0 + r) * K + k] = gv;
       }
     }
@@ -676,12 +693,14 @@ __global__ __launch_bounds__(HT) void head_generic_kernel(HeadArgs a) {
 
 using namespace csa;
 
-// Rows per workgroup of the partial-output head (0: shape outside its family).
+// Rows per workgroup of the partial-output head (0: shape outside its family: more than
+// 16 groups of <= 16 rows, K % 4, or the LDS budget).
 CSA_API int csa_head_part_rows(int M, int K) {
-  if (M < 1 || K < 1 || K > 4 * 64 * PKL) return 0;
+  if (M < 1 || K < 4 || K % 4) return 0;
   int rg = 4;
   while ((M + rg - 1) / rg > 16 && rg < PRG_MAX) rg *= 2;
-  return (M + rg - 1) / rg <= 16 ? rg : 0;
+  if ((M + rg - 1) / rg > 16 || head_part_lds(rg, K) > PHEAD_LDS_MAX) return 0;
+  return rg;
 }
 
 CSA_API int csa_head_part(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
@@ -692,7 +711,13 @@ CSA_API int csa_head_part(const float* h, int M, int K, int in_act, float in_alp
   if (!rg) return -1;
   HeadPartArgs a{h, M, K, rg, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, part,
                  mpart, mcorr, logits_out, step};
-  hipLaunchKernelGGL(head_part_kernel, dim3((unsigned)((M + rg - 1) / rg)), dim3(256), 0, st, a);
+  const size_t shm = head_part_lds(rg, K);
+  if (shm > 64 * 1024) {
+    static bool attr = hipFuncSetAttribute((const void*)head_part_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)PHEAD_LDS_MAX) == hipSuccess;
+    if (!attr) return -3;
+  }
+  hipLaunchKernelGGL(head_part_kernel, dim3((unsigned)((M + rg - 1) / rg)), dim3(256), shm, st, a);
   return (int)hipGetLastError();
 }
 

@@ -141,9 +141,21 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (a.met.parts > 0) {
+      // all partials' loads in flight together (a serial load -> add loop is one memory
+      // round trip per partial on the critical path of the whole step)
+      float lv[MAXS];
+      int cv[MAXS];
+#pragma unroll
+      for (int p = 0; p < MAXS; ++p) {
+        const int pp = p < a.met.parts ? p : 0;
+        lv[p] = a.met.loss[pp];
+        cv[p] = a.met.corr[pp];
+      }
       float ls = 0.f;
       int nc = 0;
-      for (int p = 0; p < a.met.parts; ++p) { ls += a.met.loss[p]; nc += a.met.corr[p]; }
+#pragma unroll
+      for (int p = 0; p < MAXS; ++p)
+        if (p < a.met.parts) { ls += lv[p]; nc += cv[p]; }
       const int pos = (int)((*a.step - 1) % a.met.ring);
       a.met.ring_loss[pos] = ls / a.met.div;
       a.met.ring_correct[pos] = nc;
@@ -172,7 +184,7 @@ CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, lo
                            const float* met_loss, const int* met_corr, int met_parts, float met_div,
                            float* ring_loss, int* ring_correct, int ring, int64_t* cursor, long cursor_wrap,
                            hipStream_t st) {
-  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG) return -1;
+  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG || met_parts > MAXS) return -1;
   OptArgs a{};
   a.keep.count = nkeep;
   for (int i = 0; i < nkeep; ++i) {

@@ -55,6 +55,7 @@ _SIGS = {
     "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
                                  P, P, P, P, F, P]),
     "csa_head_part_rows": (I, [I, I]),
+    "csa_du_debug": (I, [P]),
     "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),

@@ -270,9 +270,13 @@ class HipProgram:
         must be all-reduced before any update."""
         e, B = self.e, self.B
         self.fused = (not e.ctx.enabled) and os.environ.get("CSA_FUSED_UPDATE", "1") == "1"
+        # measured on MI355X (profiles/r2_dense_fused.md): at one workgroup per CU the fused
+        # dense kernel's serial chunk chain (18 / 23 us for fc2 / fc1) loses to the
+        # split-K backward pair + flat optimizer, so the dense half is opt-in for now
+        fuse_dense = self.fused and os.environ.get("CSA_FUSED_DENSE", "0") == "1"
         for u in self.units:
             u.fused = False
-            if not self.fused or u.kind != "dense":
+            if not fuse_dense or u.kind != "dense":
                 continue
             tf = u.in_tf
             fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
@@ -456,8 +460,8 @@ class HipProgram:
         for u in self.units:
             if u.in_tf.has_bn:
                 regs.append(u.in_tf.slab.view(-1))          # forward stats (atomic rows)
-                if u.kind == "conv":
-                    regs.append(u.in_tf.bwd_slab.view(-1))  # conv dgrad folds rows atomically
+                if u.kind == "conv" or u.fused:
+                    regs.append(u.in_tf.bwd_slab.view(-1))  # conv dgrad / fused dense fold rows atomically
         # dense weight gradients produced without split-K are STORED whole every step (by the
         # fused dense backward, the separate wgrad or the lowrank wgrad), so the optimizer
         # skips re-zeroing them (keep ranges, float4-aligned: the flat layout aligns to 64)

