@@ -54,6 +54,12 @@ struct FastDiv {
   }
 };
 
+// Materialise loaded values here (the empty asm "reads and writes" them): hipcc otherwise
+// sinks each load into the conditional block that consumes it and waits for it there, one
+// serial memory round trip per element.  Pin a batch of loads after issuing all of them.
+__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+
 // Block-cooperative copy global -> LDS with a per-element transform, issuing UNROLL
 // independent loads per thread before any store (branch-free clamped addresses), so a
 // thread waits for one memory round trip per UNROLL elements instead of one per element
@@ -75,12 +81,6 @@ __device__ __forceinline__ void stage_to_lds(float* dst, const T* src, int n, F 
     }
   }
 }
-
-// Materialise loaded values here (the empty asm "reads and writes" them): hipcc otherwise
-// sinks each load into the conditional block that consumes it and waits for it there, one
-// serial memory round trip per element.  Pin a batch of loads after issuing all of them.
-__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
-__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -121,9 +121,21 @@ __device__ __forceinline__ void slab_sum_to_lds(const float* slab, int nslab, in
   if (per > 0) {
     const int col = threadIdx.x % C2, lane_row = threadIdx.x / C2;
     if (lane_row < per) {
+      // batches of 8 loads in flight per thread (a load -> add chain is one memory round
+      // trip per row)
       float acc = 0.f;
-#pragma unroll 4
-      for (int r = lane_row; r < nslab; r += per) acc += slab[(size_t)r * C2 + col];
+      for (int r0 = lane_row; r0 < nslab; r0 += 8 * per) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = r0 + u * per;
+          v[u] = slab[(size_t)(r < nslab ? r : lane_row) * C2 + col];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pin(v[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += (r0 + u * per < nslab) ? v[u] : 0.f;
+      }
       atomicAdd(&s_out[col], acc);
     }
   } else {

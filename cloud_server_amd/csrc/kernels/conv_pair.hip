@@ -1,0 +1,718 @@
+// A first-layer conv PAIR fused forward and backward (gfx950 / CDNA4).
+//
+// Reference: the DSL's leading `conv, [active], conv, [active], [pool]` layers
+// (construct_distribute.py:91-130, 222-240) — in the sample config (API.md:306-332)
+// conv[2,2,10] -> conv[2,2,20] -> pool, on 28x28x1 digits.  The per-layer path runs
+// conv1, conv2(+pool) forward and route, conv2 dgrad/wgrad, conv1 wgrad backward as five
+// launches that pass 1.6-3.1 MB intermediates (c1, dc2, dc1) through HBM.  Here:
+//
+//   forward  ONE launch: per (image, band of pooled rows) the band's input rows are
+//            gathered (uint8, /255) into LDS, conv A is evaluated into an LDS tile
+//            (with conv B's zero padding materialised), conv B + act + 2x2 max-pool run
+//            on it, the pooled output, argmax and the following BatchNorm's partial
+//            statistics are written.  c1 never leaves the CU.
+//   backward ONE launch: per band, BatchNorm backward + act backward + pool routing of
+//            the band's (and one halo row's) output gradient into an LDS dc2 tile, c1
+//            recomputed from the input rows (40 MACs per value: cheaper than storing
+//            it), conv B's weight gradient, conv B's input gradient dc1 (through act A),
+//            conv A's weight gradient — all from LDS; the weight gradients leave the
+//            launch as one atomic add per (workgroup, weight) into S stripes that the
+//            optimizer folds.  No dc2 / dc1 / c1 tensor is ever written.
+//
+// Family: stride-1 convs, kernels <= 5x5 (SAME / VALID), C0 <= 4, C1 <= 32 (even),
+// C2 <= 64 (multiple of 4), optional 2x2 stride-2 unpadded pool, H, W <= 64, first layer
+// (uint8 dataset rows gathered through the batch index stream).  Everything else uses the
+// per-layer kernels (conv.hip).
+#include "common.h"
+#include <algorithm>
+
+namespace csa {
+
+constexpr int CP_THREADS = 256;
+constexpr int CP_MAXC2 = 64;
+constexpr int CP_MAXC1 = 32;
+constexpr size_t CP_LDS_MAX = 150 * 1024;
+
+__device__ long long* g_cp_dbg = nullptr;   // diagnostics: s_memtime stamps of block 0
+#define CP_STAMP(i)                                                                           \
+  do {                                                                                        \
+    if (g_cp_dbg && threadIdx.x == 0 && blockIdx.x == 0) g_cp_dbg[i] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+struct CPGeom {
+  int B, H, W, C0;                 // input
+  int KAh, KAw, PTA, PLA, C1;      // conv A (stride 1)
+  int H1, W1;                      // conv A output
+  int KBh, KBw, PTB, PLB, C2;      // conv B (stride 1)
+  int H2, W2;                      // conv B output
+  int pool;                        // 2x2 / stride 2 max-pool after conv B (+ act B)
+  int PH, PW;                      // unit output (pooled) size
+  int PR, nbands;                  // pooled rows per band
+};
+
+struct CPFwdArgs {
+  CPGeom g;
+  const uint8_t* img; const int64_t* idx; const int64_t* cursor;
+  const float* wA; const float* bA; int actA; float alphaA;
+  const float* wB; const float* bB; int actB; float alphaB;
+  float* y; uint8_t* argmax; float* stat; int nslab;
+};
+
+// Band tile extents (rows in conv-B-output coordinates and the derived c1 / x rows).
+struct CPBand {
+  int r2a, r2b;     // conv B output rows computed
+  int c1y0, T1H;    // c1 tile: rows c1y0 .. c1y0 + T1H (may extend outside [0, H1): zeros)
+  int T1W;          // c1 tile columns: c1 x = tx - PLB
+  int TXH, TXW;     // x tile: rows c1y0 - PTA + ty, cols tx - PLB - PLA
+};
+
+__device__ __forceinline__ CPBand cp_band(const CPGeom& g, int r2a, int r2b) {
+  CPBand t;
+  t.r2a = r2a; t.r2b = r2b;
+  t.c1y0 = r2a - g.PTB;
+  t.T1H = (r2b - r2a) + g.KBh - 1;
+  t.T1W = g.W2 + g.KBw - 1;
+  t.TXH = t.T1H + g.KAh - 1;
+  t.TXW = t.T1W + g.KAw - 1;
+  return t;
+}
+
+__device__ __forceinline__ const uint8_t* cp_image(const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                                                   int b, int B, long imsz) {
+  const int64_t* id = cursor ? idx + cursor[0] * B : idx;
+  return img + id[b] * imsz;
+}
+
+// x tile (uint8 -> /255, zero outside the image) into LDS [TXH][TXW][C0].
+__device__ __forceinline__ void cp_stage_x(const CPGeom& g, const CPBand& t, const uint8_t* src, float* s_x) {
+  const int n = t.TXH * t.TXW * g.C0;
+  const int y0 = t.c1y0 - g.PTA, x0 = -g.PLB - g.PLA;
+  const FastDiv dw(t.TXW * g.C0), dc(g.C0);
+  constexpr int U = 4;
+  for (int base = 0; base < n; base += CP_THREADS * U) {
+    int ok[U];
+    uint8_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * CP_THREADS + threadIdx.x;
+      int r, rem, xx, c;
+      dw.divmod(e < n ? e : 0, r, rem);
+      dc.divmod(rem, xx, c);
+      const int y = y0 + r, x = x0 + xx;
+      ok[u] = e < n && y >= 0 && y < g.H && x >= 0 && x < g.W;
+      v[u] = src[ok[u] ? ((long)y * g.W + x) * g.C0 + c : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * CP_THREADS + threadIdx.x;
+      if (e < n) s_x[e] = ok[u] ? (float)v[u] * (1.0f / 255.0f) : 0.f;
+    }
+  }
+}
+
+// Weights as a zero-padded [kpad][npad] LDS panel (the MFMA B operand), k = flattened
+// (i, j, cin) of the HWIO tensor.
+__device__ __forceinline__ void cp_stage_panel(float* dst, const float* w, int K, int N, int kpad, int npad) {
+  const FastDiv dn(npad);
+  for (int e = threadIdx.x; e < kpad * npad; e += CP_THREADS) {
+    int k, n;
+    dn.divmod(e, k, n);
+    dst[e] = (k < K && n < N) ? w[k * N + n] : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// In-LDS GEMM on v_mfma_f32_16x16x4_f32: D[m][n] = sum_k A(m, k) B(k, n) where both operands
+// are LDS gathers  A(m, k) = s[abase(m) + aoff[k]],  B(k, n) = s[bbase(n) + boff[k]]
+// (aoff / boff: per-k offset tables in LDS).  (m-tile, n-tile) pairs are dealt to the 4
+// waves; two accumulators per pair break the dependent-MFMA chain.  epi(tm, tn, acc) gets
+// the lane's D fragment: rows tm*16 + 4q + r, column tn*16 + (lane & 15).
+// Padding rows / columns read any valid address and are dropped by the epilogue; padded
+// k must make one operand zero (a zero panel row or an offset onto a zero cell).
+// 16x16x4 map: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15], D[4*(l>>4)+r][l&15].
+typedef float cp_f32x4 __attribute__((ext_vector_type(4)));
+
+template <class FA, class FB, class FE>
+__device__ __forceinline__ void cp_gemm(const float* s, int mt, int nt, int ksteps, const int* aoff, const int* boff,
+                                        FA abase, FB bbase, FE epi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, q = lane >> 4;
+  for (int pr = wave; pr < mt * nt; pr += CP_THREADS / 64) {
+    const int tm = pr / nt, tn = pr - tm * nt;
+    const float* pa = s + abase(tm * 16 + i16);
+    const float* pb = s + bbase(tn * 16 + i16);
+    cp_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    int ks = 0;
+    for (; ks + 4 <= ksteps; ks += 4) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = 4 * (ks + u) + q;
+        av[u] = pa[aoff[k]];
+        bv[u] = pb[boff[k]];
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc1, 0, 0, 0);
+    }
+    for (; ks < ksteps; ++ks) {
+      const int k = 4 * ks + q;
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[aoff[k]], pb[boff[k]], acc0, 0, 0, 0);
+    }
+    epi(tm, tn, acc0 + acc1, 0);
+  }
+}
+
+// c1 tile (post act A; zero outside [0, H1) x [0, W1)) into LDS [T1H][T1W][C1]:
+// a [tile pixels] x [C1] GEMM with K = taps of conv A (x tile gather x weight panel).
+__device__ __forceinline__ void cp_conv_a(const CPGeom& g, const CPBand& t, float* s, const float* s_x,
+                                          const float* s_pA, int kpadA, const int* offA, const int* offPA,
+                                          const float* bA, int actA, float alphaA, float* s_c1) {
+  const int npix = t.T1H * t.T1W;
+  const FastDiv dw(t.T1W);
+  cp_gemm(s, (npix + 15) >> 4, 1, kpadA >> 2, offA, offPA,
+          [&](int m) {
+            int ty, tx;
+            dw.divmod(m < npix ? m : 0, ty, tx);
+            return (int)(s_x - s) + (ty * t.TXW + tx) * g.C0;
+          },
+          [&](int n) { return (int)(s_pA - s) + n; },
+          [&](int tm, int, cp_f32x4 acc, int) {
+            const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+            if (c >= g.C1) return;
+            const float bias = bA ? bA[c] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = tm * 16 + 4 * q + r;
+              if (m >= npix) continue;
+              int ty, tx;
+              dw.divmod(m, ty, tx);
+              const int y = t.c1y0 + ty, x = tx - g.PLB;
+              const bool in = y >= 0 && y < g.H1 && x >= 0 && x < g.W1;
+              s_c1[m * g.C1 + c] = in ? act_fwd(acc[r] + bias, actA, alphaA) : 0.f;
+            }
+          });
+}
+
+// per-k offset tables of conv A: x tile offset of tap k = (i, j, c0) and its panel row
+__device__ __forceinline__ void cp_tables_a(const CPGeom& g, const CPBand& t, int kpadA, int* offA, int* offPA) {
+  const int KA = g.KAh * g.KAw * g.C0;
+  for (int k = threadIdx.x; k < kpadA; k += CP_THREADS) {
+    int o = 0;
+    if (k < KA) {
+      const int c0 = k % g.C0, ij = k / g.C0, i = ij / g.KAw, j = ij - i * g.KAw;
+      o = (i * t.TXW + j) * g.C0 + c0;
+    }
+    offA[k] = o;
+    offPA[k] = k * 16;
+  }
+}
+
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_stat[2 * CP_MAXC2];
+  __shared__ int s_offA[32], s_offPA[32];
+  const CPGeom& g = a.g;
+  const int b = blockIdx.x / g.nbands, band = blockIdx.x % g.nbands;
+  const int pr0 = band * g.PR, pr1 = min(g.PH, pr0 + g.PR);
+  const int r2a = g.pool ? 2 * pr0 : pr0, r2b = g.pool ? min(g.H2, 2 * pr1) : pr1;
+  const CPBand t = cp_band(g, r2a, r2b);
+  const int KA = g.KAh * g.KAw * g.C0, kpadA = (KA + 3) & ~3;
+  const int KB = g.KBh * g.KBw * g.C1, kpadB = (KB + 3) & ~3, c16 = (g.C2 + 15) & ~15;
+  const int pst = (c16 & 31) ? c16 : c16 + 16;          // panel row stride == 16 (mod 32)
+  float* s_pA = smem;                                   // [kpadA][16]
+  float* s_pB = s_pA + kpadA * 16;                      // [kpadB][pst]
+  int* s_offB = reinterpret_cast<int*>(s_pB + kpadB * pst);   // [kpadB] c1 tile offset of tap k
+  int* s_offPB = s_offB + kpadB;                               // [kpadB] panel row k * pst
+  float* s_x = reinterpret_cast<float*>(s_offPB + kpadB);
+  float* s_c1 = s_x + ((t.TXH * t.TXW * g.C0 + 3) & ~3);
+  CP_STAMP(0);
+  const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
+  cp_stage_x(g, t, src, s_x);
+  cp_stage_panel(s_pA, a.wA, KA, g.C1, kpadA, 16);
+  cp_stage_panel(s_pB, a.wB, KB, g.C2, kpadB, pst);
+  cp_tables_a(g, t, kpadA, s_offA, s_offPA);
+  for (int k = threadIdx.x; k < kpadB; k += CP_THREADS) {     // c1 tile offset of tap (i, j, c1)
+    int o = 0;
+    if (k < KB) {
+      const int c1 = k % g.C1, ij = k / g.C1, i = ij / g.KBw, j = ij - i * g.KBw;
+      o = (i * t.T1W + j) * g.C1 + c1;
+    }
+    s_offB[k] = o;
+    s_offPB[k] = k * pst;
+  }
+  for (int i = threadIdx.x; i < 2 * g.C2; i += CP_THREADS) s_stat[i] = 0.f;
+  __syncthreads();
+  CP_STAMP(1);
+  cp_conv_a(g, t, smem, s_x, s_pA, kpadA, s_offA, s_offPA, a.bA, a.actA, a.alphaA, s_c1);
+  __syncthreads();
+  CP_STAMP(2);
+
+  // conv B (+ act, + 2x2 max-pool): rows = (unit pixel, window position) when pooled —
+  // a lane's 4 D rows are one pooled pixel's 4 positions, so the pool is in registers
+  const int ow = g.pool ? g.PW : g.W2;
+  const int nunit = (g.pool ? (pr1 - pr0) : (r2b - r2a)) * ow;
+  const int nrows = g.pool ? 4 * nunit : nunit;
+  const FastDiv dow(ow);
+  cp_gemm(smem, (nrows + 15) >> 4, c16 >> 4, kpadB >> 2, s_offB, s_offPB,
+          [&](int m) {                                           // c1 tile offset of row m
+            const int mc = m < nrows ? m : 0;
+            int y2, x2;
+            if (g.pool) {
+              int py, px;
+              dow.divmod(mc >> 2, py, px);
+              y2 = 2 * (pr0 + py) + ((mc & 3) >> 1);
+              x2 = 2 * px + (mc & 1);
+              if (y2 >= g.H2 || x2 >= g.W2) { y2 = r2a; x2 = 0; }  // outside: dropped below
+            } else {
+              int py, px;
+              dow.divmod(mc, py, px);
+              y2 = r2a + py;
+              x2 = px;
+            }
+            return (int)(s_c1 - smem) + ((y2 - r2a) * t.T1W + x2) * g.C1;
+          },
+          [&](int n) { return (int)(s_pB - smem) + n; },
+          [&](int tm, int tn, cp_f32x4 acc, int) {
+            const int lane = threadIdx.x & 63, i16 = lane & 15, q = lane >> 4;
+            const int c = tn * 16 + i16;
+            const float bias = (a.bB && c < g.C2) ? a.bB[c] : 0.f;
+            float best = -INFINITY;
+            int am = 0;
+            float s1 = 0.f, s2 = 0.f;
+            if (g.pool) {
+              const int u = tm * 4 + q;                          // unit pixel of this lane
+              if (u < nunit && c < g.C2) {
+                int py, px;
+                dow.divmod(u, py, px);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int y2 = 2 * (pr0 + py) + (r >> 1), x2 = 2 * px + (r & 1);
+                  if (y2 >= g.H2 || x2 >= g.W2) continue;
+                  const float v = act_fwd(acc[r] + bias, a.actB, a.alphaB);
+                  if (v > best) { best = v; am = r; }
+                }
+                const long o = (((long)b * g.PH + pr0 + py) * g.PW + px) * g.C2 + c;
+                a.y[o] = best;
+                if (a.argmax) a.argmax[o] = (uint8_t)am;
+                s1 = best;
+                s2 = best * best;
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int u = tm * 16 + 4 * q + r;
+                if (u >= nunit || c >= g.C2) continue;
+                int py, px;
+                dow.divmod(u, py, px);
+                const float v = act_fwd(acc[r] + bias, a.actB, a.alphaB);
+                a.y[(((long)b * g.H2 + r2a + py) * g.W2 + px) * g.C2 + c] = v;
+                s1 += v;
+                s2 += v * v;
+              }
+            }
+            if (a.stat) {                                        // fold the 4 lane quads
+              s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
+              s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+              if (q == 0 && c < g.C2) { atomicAdd(&s_stat[c], s1); atomicAdd(&s_stat[g.C2 + c], s2); }
+            }
+          });
+  CP_STAMP(3);
+  if (a.stat) {
+    __syncthreads();
+    float* row = a.stat + (size_t)(blockIdx.x % a.nslab) * 2 * g.C2;
+    for (int i = threadIdx.x; i < 2 * g.C2; i += CP_THREADS) atomicAdd(&row[i], s_stat[i]);
+  }
+  CP_STAMP(4);
+}
+
+// --------------------------------------------------------------------------------------
+// Backward.
+struct CPBwdArgs {
+  CPGeom g;
+  const uint8_t* img; const int64_t* idx; const int64_t* cursor;
+  const float* wA; const float* bA; int actA; float alphaA;
+  const float* wB; int actB; float alphaB; int hasBiasB;
+  const float* dz;                  // grad wrt the BN output (or the unit output)
+  const float* y;                   // unit output (post act, post pool) = BN input
+  const uint8_t* argmax;
+  BNRef bn; int bn_on; const float* bwd_slab; int bwd_nslab;
+  float* dscale; float* doffset; float* run_mean; float* run_var; float momentum;
+  float* dwA; float* dbA; float* dwB; float* dbB; int stripes;
+};
+
+// LDS carve of the backward (float offsets), shared by the kernel and the host size check.
+struct CPBwdLayout {
+  int o2a, o2b, o1a, o1b;           // owned conv-B-output rows / owned c1 rows
+  int d2y0, D2H, D2W;               // zero-padded dc2 tile: rows d2y0 .., cols PLB-KBw+1 ..
+  int KA, kpadA, KB, kpadB, KD, kpadD, c16, n16a, n16b;
+  int npix2, kp2, npix1, kp1;       // owned pixels (conv B out / c1), padded to 4
+  int wA, pA, pB, x, c1, dc2, dc1, red, offs, end;
+};
+
+__host__ __device__ inline CPBwdLayout cp_bwd_layout(const CPGeom& g, int band, int TXH, int TXW, int T1H, int T1W) {
+  CPBwdLayout L;
+  const int pr0 = band * g.PR, pr1 = min(g.PH, pr0 + g.PR);
+  const bool last = band == g.nbands - 1;
+  L.o2a = g.pool ? 2 * pr0 : pr0;
+  L.o2b = g.pool ? (last ? g.H2 : 2 * pr1) : pr1;
+  L.o1a = L.o2a;
+  L.o1b = last ? g.H1 : L.o2b;
+  L.d2y0 = L.o1a + g.PTB - g.KBh + 1;
+  L.D2H = (L.o1b - L.o1a) + g.KBh - 1 + 1;            // + one zero row (padded pixels)
+  L.D2W = g.W1 + g.KBw - 1;
+  L.KA = g.KAh * g.KAw * g.C0; L.kpadA = (L.KA + 3) & ~3;
+  L.KB = g.KBh * g.KBw * g.C1; L.kpadB = (L.KB + 3) & ~3;
+  L.KD = g.KBh * g.KBw * g.C2; L.kpadD = (L.KD + 3) & ~3;
+  L.c16 = (g.C2 + 15) & ~15; L.n16a = (L.KA + 15) & ~15; L.n16b = (L.KB + 15) & ~15;
+  L.npix2 = (L.o2b - L.o2a) * g.W2; L.kp2 = (L.npix2 + 3) & ~3;
+  L.npix1 = (L.o1b - L.o1a) * g.W1; L.kp1 = (L.npix1 + 3) & ~3;
+  int o = 0;
+  L.pA = o; o += L.kpadA * 16;                        // conv A weight panel [kpadA][16]
+  L.pB = o; o += L.kpadB * L.c16;                     // conv B weights (HWIO, dense) + pad
+  L.x = o; o += (TXH * TXW * g.C0 + 3) & ~3;
+  L.c1 = o; o += (T1H * T1W * g.C1 + 3) & ~3;
+  L.dc2 = o; o += (L.D2H * L.D2W * g.C2 + 3) & ~3;
+  L.dc1 = o; o += ((L.npix1 + 1) * g.C1 + 3) & ~3;    // + one zero pixel row
+  L.red = o; o += (L.n16b * L.c16 + L.n16a * 16 + 4 * 16 * 16 + g.C2 + g.C1 + 3) & ~3;
+  L.offs = o; o += 2 * L.kpadA + L.kp2 * 2 + L.kpadD * 2 + L.kp1 * 2 + L.n16b + 16;
+  L.end = o;
+  (void)L.wA;
+  return L;
+}
+
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_bn[4 * CP_MAXC2];
+  __shared__ float s_ss[2 * CP_MAXC2];
+  const CPGeom& g = a.g;
+  const int b = blockIdx.x / g.nbands, band = blockIdx.x % g.nbands;
+  const int pr0 = band * g.PR;
+  const CPBand t0 = cp_band(g, 0, 0);
+  (void)t0;
+  const int o2a_ = g.pool ? 2 * pr0 : pr0;
+  const bool last_ = band == g.nbands - 1;
+  const int o2b_ = g.pool ? (last_ ? g.H2 : 2 * min(g.PH, pr0 + g.PR)) : min(g.PH, pr0 + g.PR);
+  const CPBand t = cp_band(g, o2a_, o2b_);            // c1 tile rows o2a - PTB ..
+  const CPBwdLayout L = cp_bwd_layout(g, band, t.TXH, t.TXW, t.T1H, t.T1W);
+  float* s_pA = smem + L.pA;
+  float* s_wB = smem + L.pB;
+  float* s_x = smem + L.x;
+  float* s_c1 = smem + L.c1;
+  float* s_dc2 = smem + L.dc2;
+  float* s_dc1 = smem + L.dc1;
+  float* s_red = smem + L.red;
+  int* s_offA = reinterpret_cast<int*>(smem + L.offs);      // conv A (recompute): x offsets
+  int* s_offPA = s_offA + L.kpadA;                           //                    panel rows
+  int* s_pix2 = s_offPA + L.kpadA;                           // dwB: pixel -> c1 tile offset
+  int* s_pixd = s_pix2 + L.kp2;                              //      pixel -> dc2 tile offset
+  int* s_offD = s_pixd + L.kp2;                              // dc1: k=(i,j,c2) -> dc2 offset
+  int* s_offW = s_offD + L.kpadD;                            //      k -> weight offset
+  int* s_pix1x = s_offW + L.kpadD;                           // dwA: pixel -> x tile offset
+  int* s_pix1d = s_pix1x + L.kp1;                            //      pixel -> dc1 offset
+  int* s_tapB = s_pix1d + L.kp1;                             // dwB: tap -> c1 tile offset
+  CP_STAMP(8);
+  const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
+  cp_stage_x(g, t, src, s_x);
+  cp_stage_panel(s_pA, a.wA, L.KA, g.C1, L.kpadA, 16);
+  for (int i = threadIdx.x; i < L.kpadB * L.c16; i += CP_THREADS) s_wB[i] = i < L.KB * g.C2 ? a.wB[i] : 0.f;
+  for (int i = threadIdx.x; i < L.D2H * L.D2W * g.C2; i += CP_THREADS) s_dc2[i] = 0.f;
+  for (int i = threadIdx.x; i < g.C1; i += CP_THREADS) s_dc1[L.npix1 * g.C1 + i] = 0.f;
+  cp_tables_a(g, t, L.kpadA, s_offA, s_offPA);
+  {
+    const FastDiv dw2(g.W2), dw1(g.W1);
+    const int zrow2 = ((L.D2H - 1) * L.D2W) * g.C2;           // the dc2 tile's zero row
+    for (int p = threadIdx.x; p < L.kp2; p += CP_THREADS) {
+      int yy, xx;
+      dw2.divmod(p < L.npix2 ? p : 0, yy, xx);
+      s_pix2[p] = (yy * t.T1W + xx) * g.C1;                   // y2 - o2a = yy
+      s_pixd[p] = p < L.npix2 ? ((L.o2a + yy - L.d2y0) * L.D2W + xx + g.KBw - 1 - g.PLB) * g.C2 : zrow2;
+    }
+    for (int k = threadIdx.x; k < L.kpadD; k += CP_THREADS) {
+      int od = 0, ow = 0;
+      if (k < L.KD) {
+        const int c2 = k % g.C2, ij = k / g.C2, i = ij / g.KBw, j = ij - i * g.KBw;
+        od = -(i * L.D2W + j) * g.C2 + c2;
+        ow = ij * g.C1 * g.C2 + c2;
+      } else {
+        ow = L.kpadB * L.c16 - 1 - (g.C1 - 1) * g.C2;   // -> zero pad of the weight area
+        if (ow < 0) ow = 0;
+      }
+      s_offD[k] = od;
+      s_offW[k] = ow;
+    }
+    for (int p = threadIdx.x; p < L.kp1; p += CP_THREADS) {
+      int yy, xx;
+      dw1.divmod(p < L.npix1 ? p : 0, yy, xx);
+      s_pix1x[p] = ((L.o1a + yy - t.c1y0) * t.TXW + xx + g.PLB) * g.C0;
+      s_pix1d[p] = (p < L.npix1 ? p : L.npix1) * g.C1;      // padded pixels -> the zero row
+    }
+    for (int k = threadIdx.x; k < L.n16b; k += CP_THREADS) {
+      int o = 0;
+      if (k < L.KB) {
+        const int c1 = k % g.C1, ij = k / g.C1, i = ij / g.KBw, j = ij - i * g.KBw;
+        o = (i * t.T1W + j) * g.C1 + c1;
+      }
+      s_tapB[k] = o;
+    }
+  }
+  // BatchNorm tables of the unit output and the backward sums (every block reduces the
+  // small slabs; block 0 writes the BN parameter gradients and running statistics)
+  if (a.bn_on) {
+    bn_reduce_to_lds(a.bn, s_bn, s_bn + CP_MAXC2, s_bn + 2 * CP_MAXC2, s_bn + 3 * CP_MAXC2, s_ss);
+    __syncthreads();
+    slab_sum_to_lds(a.bwd_slab, a.bwd_nslab, 2 * g.C2, s_ss);
+    if (blockIdx.x == 0)
+      for (int c = threadIdx.x; c < g.C2; c += CP_THREADS) {
+        a.doffset[c] = s_ss[c];
+        a.dscale[c] = s_ss[g.C2 + c];
+        if (a.run_mean) {
+          const float mean = s_bn[c];
+          const float var = 1.0f / (s_bn[CP_MAXC2 + c] * s_bn[CP_MAXC2 + c]) - a.bn.eps;
+          a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
+          a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var;
+        }
+      }
+  }
+  __syncthreads();
+  CP_STAMP(9);
+  // ---- route: dc2 (zero-padded tile) for conv-B-output rows [d2y0, d2y0 + D2H - 1)
+  {
+    const int n2a = max(0, L.d2y0), n2b = min(g.H2, L.d2y0 + L.D2H - 1);
+    const int ow = g.pool ? g.PW : g.W2;
+    const int ua = g.pool ? n2a / 2 : n2a, ub = g.pool ? min(g.PH, (n2b + 1) / 2) : n2b;   // unit rows
+    const int n = max(0, ub - ua) * ow * g.C2;
+    const float inv_n = a.bn_on ? 1.0f / a.bn.count : 0.f;
+    const long base = ((long)b * (g.pool ? g.PH : g.H2) + ua) * ow * g.C2;
+    const FastDiv dC(g.C2), dow(ow);
+    constexpr int U = 4;
+    for (int i0 = 0; i0 < n; i0 += CP_THREADS * U) {
+      float gz[U], yv[U];
+      int am[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * CP_THREADS + (int)threadIdx.x, n - 1);
+        gz[u] = a.dz[base + i];
+        yv[u] = a.y[base + i];
+        am[u] = g.pool ? (int)a.argmax[base + i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * CP_THREADS + (int)threadIdx.x;
+        if (i >= n) break;
+        int pix, c, ry, px;
+        dC.divmod(i, pix, c);
+        dow.divmod(pix, ry, px);
+        float gv = gz[u];
+        if (a.bn_on) {
+          const float xhat = (yv[u] - s_bn[c]) * s_bn[CP_MAXC2 + c];
+          gv = s_bn[2 * CP_MAXC2 + c] * (gv - s_ss[c] * inv_n - xhat * s_ss[g.C2 + c] * inv_n);
+        }
+        gv = act_bwd(gv, yv[u], yv[u], a.actB, a.alphaB);
+        const int y2 = g.pool ? 2 * (ua + ry) + (am[u] >> 1) : ua + ry;
+        const int x2 = g.pool ? 2 * px + (am[u] & 1) : px;
+        if (y2 >= n2a && y2 < n2b && x2 < g.W2)
+          s_dc2[((y2 - L.d2y0) * L.D2W + x2 + g.KBw - 1 - g.PLB) * g.C2 + c] = gv;
+      }
+    }
+  }
+  CP_STAMP(10);
+  // ---- c1 tile (rows o2a - PTB ..) recomputed from the input rows
+  cp_conv_a(g, t, smem, s_x, s_pA, L.kpadA, s_offA, s_offPA, a.bA, a.actA, a.alphaA, s_c1);
+  __syncthreads();
+  CP_STAMP(11);
+  // ---- weight gradient B: [taps (i, j, c1)] x [C2], K = owned conv-B-output pixels
+  float* s_rB = s_red;                                        // [n16b][c16]
+  float* s_rA = s_red + L.n16b * L.c16;                       // [4 waves][16][16] partials
+  float* s_bias = s_rA + 4 * 16 * 16;                         // [C2] + [C1]
+  cp_gemm(smem, L.n16b >> 4, L.c16 >> 4, L.kp2 >> 2, s_pix2, s_pixd,
+          [&](int m) { return L.c1 + s_tapB[m]; },
+          [&](int n) { return L.dc2 + n; },
+          [&](int tm, int tn, cp_f32x4 acc, int) {
+            const int lane = threadIdx.x & 63, i16 = lane & 15, q = lane >> 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              s_rB[(tm * 16 + 4 * q + r) * L.c16 + tn * 16 + i16] = acc[r];
+            }
+          });
+  // bias B: column sums of the owned dc2 pixels (4 threads per channel + LDS atomics)
+  for (int i = threadIdx.x; i < g.C2 + g.C1; i += CP_THREADS) s_bias[i] = 0.f;
+  CP_STAMP(12);
+  // ---- dc1 of the owned c1 pixels: [pixels] x [C1], K = (i, j, c2), then act A backward
+  {
+    const FastDiv dw1(g.W1);
+    cp_gemm(smem, (L.npix1 + 15) >> 4, 1, L.kpadD >> 2, s_offD, s_offW,
+            [&](int m) {
+              int yy, xx;
+              dw1.divmod(m < L.npix1 ? m : 0, yy, xx);
+              return L.dc2 + ((L.o1a + yy + g.PTB - L.d2y0) * L.D2W + xx + g.PLB + g.KBw - 1 - g.PLB) * g.C2;
+            },
+            [&](int n) { return L.pB + (n < g.C1 ? n : 0) * g.C2; },
+            [&](int tm, int, cp_f32x4 acc, int) {
+              const int lane = threadIdx.x & 63, c1 = lane & 15, q = lane >> 4;
+              if (c1 >= g.C1) return;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int m = tm * 16 + 4 * q + r;
+                if (m >= L.npix1) continue;
+                int yy, xx;
+                dw1.divmod(m, yy, xx);
+                float d = acc[r];
+                if (a.actA) {                                  // post-activation c1 decides act'
+                  const int ty = L.o1a + yy - t.c1y0;
+                  const float v = (ty >= 0 && ty < t.T1H) ? s_c1[(ty * t.T1W + xx + g.PLB) * g.C1 + c1] : 0.f;
+                  d = act_bwd(d, v, v, a.actA, a.alphaA);
+                }
+                s_dc1[m * g.C1 + c1] = d;
+              }
+            });
+  }
+  __syncthreads();
+  CP_STAMP(13);
+  // bias sums (dc2 over the owned conv-B pixels, dc1 over the owned c1 pixels)
+  {
+    const int per = CP_THREADS / (g.C2 + g.C1);
+    const int col = threadIdx.x % (g.C2 + g.C1), part = threadIdx.x / (g.C2 + g.C1);
+    if (per > 0 && part < per) {
+      float acc = 0.f;
+      if (col < g.C2) {
+        for (int p = part; p < L.npix2; p += per) acc += s_dc2[s_pixd[p] + col];
+      } else {
+        for (int p = part; p < L.npix1; p += per) acc += s_dc1[p * g.C1 + col - g.C2];
+      }
+      atomicAdd(&s_bias[col], acc);
+    }
+  }
+  // ---- weight gradient A: [taps (i, j, c0)] x [C1], K = owned c1 pixels split over the
+  // 4 waves (partials in LDS)
+  {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, q = lane >> 4;
+    const int kst = L.kp1 >> 2, per = (kst + 3) / 4, k0 = wave * per, k1 = min(kst, k0 + per);
+    const float* pa = s_x + s_offA[i16 < L.kpadA ? i16 : 0];
+    const float* pb = s_dc1 + (i16 < g.C1 ? i16 : 0);
+    cp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = k0; ks < k1; ++ks) {
+      const int p = 4 * ks + q;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s_pix1x[p]], pb[s_pix1d[p]], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s_rA[wave * 256 + (4 * q + r) * 16 + i16] = acc[r];
+  }
+  __syncthreads();
+  CP_STAMP(14);
+  // ---- one atomic per (workgroup, weight) into stripe blockIdx % S, in memory order
+  {
+    const int sidx = blockIdx.x % a.stripes;
+    const int nB = L.KB * g.C2;
+    for (int o = threadIdx.x; o < nB; o += CP_THREADS) {
+      const int tap = o / g.C2, c2 = o - tap * g.C2;
+      atomicAdd(&a.dwB[(long)sidx * nB + o], s_rB[tap * L.c16 + c2]);
+    }
+    if (a.hasBiasB)
+      for (int o = threadIdx.x; o < g.C2; o += CP_THREADS) atomicAdd(&a.dbB[(long)sidx * g.C2 + o], s_bias[o]);
+    const int nA = L.KA * g.C1;
+    for (int o = threadIdx.x; o < nA; o += CP_THREADS) {
+      const int tap = o / g.C1, c1 = o - tap * g.C1;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += s_rA[w * 256 + tap * 16 + c1];
+      atomicAdd(&a.dwA[(long)sidx * nA + o], v);
+    }
+    if (a.bA)
+      for (int o = threadIdx.x; o < g.C1; o += CP_THREADS) atomicAdd(&a.dbA[(long)sidx * g.C1 + o], s_bias[g.C2 + o]);
+  }
+  CP_STAMP(15);
+}
+
+static bool cp_geom(const int* v, CPGeom& g) {
+  g = CPGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15],
+             v[16], v[17], v[18], v[19], v[20], 0, 0};
+  if (g.C0 < 1 || g.C0 > 4 || g.C1 < 2 || g.C1 > CP_MAXC1 || g.C1 % 2 || g.C2 < 4 || g.C2 > CP_MAXC2 || g.C2 % 4) return false;
+  if (g.KAh > 5 || g.KAw > 5 || g.KBh > 5 || g.KBw > 5 || g.H > 64 || g.W > 64) return false;
+  if (g.W1 < 1 || g.H2 < 1 || g.W2 < 1) return false;
+  if (((g.KAh * g.KAw * g.C0 + 3) & ~3) > 32) return false;   // static conv-A offset tables
+  const int rows = g.pool ? g.PH : g.H2;
+  g.PR = g.pool ? 2 : 4;
+  g.nbands = (rows + g.PR - 1) / g.PR;
+  return true;
+}
+
+static size_t cp_lds(const CPGeom& g, bool bwd) {
+  size_t mx = 0;
+  for (int band = 0; band < g.nbands; ++band) {
+    const int pr0 = band * g.PR, pr1 = std::min(g.PH, pr0 + g.PR);
+    const bool last = band == g.nbands - 1;
+    const int r2a = g.pool ? 2 * pr0 : pr0;
+    const int r2b = bwd ? (g.pool ? (last ? g.H2 : 2 * pr1) : pr1) : (g.pool ? std::min(g.H2, 2 * pr1) : pr1);
+    const int T1H = (r2b - r2a) + g.KBh - 1, T1W = g.W2 + g.KBw - 1;
+    const int TXH = T1H + g.KAh - 1, TXW = T1W + g.KAw - 1;
+    size_t f;
+    if (bwd) {
+      f = cp_bwd_layout(g, band, TXH, TXW, T1H, T1W).end;
+    } else {
+      const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
+      const int kpadA = (KA + 3) & ~3, kpadB = (KB + 3) & ~3, c16 = (g.C2 + 15) & ~15;
+      const int pst = (c16 & 31) ? c16 : c16 + 16;
+      f = kpadA * 16 + kpadB * pst + 2 * kpadB + ((TXH * TXW * g.C0 + 3) & ~3) + ((T1H * T1W * g.C1 + 3) & ~3);
+      if (kpadA > 32) return (size_t)-1;             // offset tables are static [32]
+    }
+    mx = std::max(mx, f);
+  }
+  return mx * sizeof(float);
+}
+
+}  // namespace csa
+
+using namespace csa;
+
+CSA_API int csa_cp_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cp_dbg), &p, sizeof(p));
+}
+
+// geom = {B, H, W, C0, KAh, KAw, PTA, PLA, C1, H1, W1, KBh, KBw, PTB, PLB, C2, H2, W2, pool, PH, PW}
+// Returns 1 when the pair is inside the fused family (the launchers below accept it).
+CSA_API int csa_conv_pair_ok(const int* geom) {
+  CPGeom g;
+  if (!cp_geom(geom, g)) return 0;
+  return cp_lds(g, true) <= CP_LDS_MAX ? 1 : 0;
+}
+
+CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                              const float* wA, const float* bA, int actA, float alphaA, const float* wB,
+                              const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
+                              int nslab, hipStream_t st) {
+  CPFwdArgs a{};
+  if (!cp_geom(geom, a.g) || cp_lds(a.g, false) > CP_LDS_MAX) return -1;
+  a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
+  a.wB = wB; a.bB = bB; a.actB = actB; a.alphaB = alphaB; a.y = y; a.argmax = argmax; a.stat = stat;
+  a.nslab = nslab < 1 ? 1 : nslab;
+  static bool attr = hipFuncSetAttribute((const void*)conv_pair_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)CP_LDS_MAX) == hipSuccess;
+  if (!attr) return -3;
+  hipLaunchKernelGGL(conv_pair_fwd_kernel, dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CP_THREADS),
+                     cp_lds(a.g, false), st, a);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                              const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
+                              int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
+                              const float* bn_slab, int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                              const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
+                              float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
+                              float* dwB, float* dbB, int stripes, hipStream_t st) {
+  CPBwdArgs a{};
+  if (!cp_geom(geom, a.g) || cp_lds(a.g, true) > CP_LDS_MAX) return -1;
+  a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
+  a.wB = wB; a.actB = actB; a.alphaB = alphaB; a.hasBiasB = hasBiasB; a.dz = dz; a.y = y; a.argmax = argmax;
+  a.bn = BNRef{bn_slab, bn_nslab, a.g.C2, bn_count, bn_eps, bn_scale, bn_offset};
+  a.bn_on = bn_slab != nullptr; a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab;
+  a.dscale = dscale; a.doffset = doffset; a.run_mean = run_mean; a.run_var = run_var; a.momentum = momentum;
+  a.dwA = dwA; a.dbA = dbA; a.dwB = dwB; a.dbB = dbB; a.stripes = stripes < 1 ? 1 : stripes;
+  static bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)CP_LDS_MAX) == hipSuccess;
+  if (!attr) return -3;
+  hipLaunchKernelGGL(conv_pair_bwd_kernel, dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CP_THREADS),
+                     cp_lds(a.g, true), st, a);
+  return (int)hipGetLastError();
+}

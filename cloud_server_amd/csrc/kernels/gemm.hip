@@ -26,6 +26,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int KC = 64;        // K chunk staged per iteration (32 MFMAs); most waves need 1-2
 constexpr int LDS_PAD = 33;   // row stride of the 32-wide staging tiles (conflict-free)
 constexpr int MAXC = 128;     // max BatchNorm channels handled in LDS
+constexpr int BN_SLAB_ROWS = 16;   // BN-backward slab rows (atomically folded)
 
 // LDS tables shared by loaders/epilogues: [mean | rstd | a | b] x MAXC
 struct BNTables { const float *mean, *rstd, *a, *b; };
@@ -382,10 +383,12 @@ __device__ __forceinline__ void gemm_body(LA la, LB lb, EPI epi, int M, int N, i
   }
   GEMM_STAMP(7);
   if (EPI::NEEDS_LDS && bn_slab_out) {
+    // fold into one of BN_SLAB_ROWS rows (atomics; the caller zeroes the slab every step),
+    // so a consumer reduces 16 rows instead of one per workgroup
     __syncthreads();
-    const int slab_row = (tid.z * GY + tid.y) * GX + tid.x;
+    const int slab_row = ((tid.z * GY + tid.y) * GX + tid.x) % BN_SLAB_ROWS;
     for (int i = threadIdx.x; i < 2 * slab_C; i += blockDim.x)
-      bn_slab_out[(size_t)slab_row * 2 * slab_C + i] = s_acc[(i < slab_C) ? i : (MAXC + i - slab_C)];
+      atomicAdd(&bn_slab_out[(size_t)slab_row * 2 * slab_C + i], s_acc[(i < slab_C) ? i : (MAXC + i - slab_C)]);
   }
 }
 
@@ -444,7 +447,8 @@ static Plan plan_gemm(int M, int N, int K, bool allow_split) {
 }
 
 static int grid_slabs(const Plan& p, int M, int N) {
-  return ((N + 32 * p.wn - 1) / (32 * p.wn)) * ((M + 32 * p.wm - 1) / (32 * p.wm)) * p.splits;
+  const int g = ((N + 32 * p.wn - 1) / (32 * p.wn)) * ((M + 32 * p.wm - 1) / (32 * p.wm)) * p.splits;
+  return g < BN_SLAB_ROWS ? g : BN_SLAB_ROWS;
 }
 
 // Bind a plan's wave layout into a GemmProblem type and hand it to f.

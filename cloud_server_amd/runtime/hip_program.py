@@ -107,6 +107,7 @@ class HipProgram:
         self.gviews = eng.model.state.views(eng.flat_grad)
         self._lower()
         self._plan_fused()
+        self._plan_pair()
         self._alloc()
         self._plan_lowrank()
         self.zero_regions: List[torch.Tensor] = []
@@ -294,6 +295,42 @@ class HipProgram:
                 K = last.pool.out_shape.numel
             self.head_rg = int(self.lib.csa_head_part_rows(B, K))
 
+    # ------------------------------------------------------------------ conv pair
+    def _plan_pair(self) -> None:
+        """``conv [act] conv [act] [pool]`` on the raw images (the sample's conv1 -> conv2
+        -> pool) runs as ONE forward and ONE backward launch (conv_pair.hip): c1 stays in
+        LDS, the backward recomputes it and never writes dc2 / dc1."""
+        self.pair = None
+        if os.environ.get("CSA_CONV_PAIR_FUSE", "1") != "1" or len(self.units) < 2:
+            return
+        ua, ub = self.units[0], self.units[1]
+        if ua.kind != "conv" or ub.kind != "conv" or ua.pool is not None:
+            return
+        if ub.in_tf.norm is not None or ub.in_tf.act is not None:
+            return
+        la, lb = ua.layer, ub.layer
+        if tuple(la.spec.stride) != (1, 1) or tuple(lb.spec.stride) != (1, 1):
+            return
+        pool = 0
+        if ub.pool is not None:
+            ps = ub.pool.spec
+            if tuple(ps.kernel) != (2, 2) or tuple(ps.stride) != (2, 2) or ub.pool.pads[0] or ub.pool.pads[2]:
+                return
+            pool = 1
+        h, w = la.in_shape.hw
+        h1, w1 = la.out_shape.hw
+        h2, w2 = lb.out_shape.hw
+        ph, pw = ub.pool.out_shape.hw if pool else (h2, w2)
+        geom = [self.B, h, w, la.in_shape.c, la.spec.kh, la.spec.kw, la.pads[0], la.pads[2], la.spec.cout,
+                h1, w1, lb.spec.kh, lb.spec.kw, lb.pads[0], lb.pads[2], lb.spec.cout, h2, w2, pool, ph, pw]
+        if not self.lib.csa_conv_pair_ok(K.ints(geom)):
+            return
+        try:
+            _act_id(ua.act), _act_id(ub.act)
+        except Unsupported:
+            return
+        self.pair = geom
+
     # ------------------------------------------------------------------ lowering
     def _lower(self) -> None:
         layers = self.e.model.plan.layers
@@ -460,8 +497,7 @@ class HipProgram:
         for u in self.units:
             if u.in_tf.has_bn:
                 regs.append(u.in_tf.slab.view(-1))          # forward stats (atomic rows)
-                if u.kind == "conv" or u.fused:
-                    regs.append(u.in_tf.bwd_slab.view(-1))  # conv dgrad / fused dense fold rows atomically
+                regs.append(u.in_tf.bwd_slab.view(-1))      # every producer folds rows atomically
         # dense weight gradients produced without split-K are STORED whole every step (by the
         # fused dense backward, the separate wgrad or the lowrank wgrad), so the optimizer
         # skips re-zeroing them (keep ranges, float4-aligned: the flat layout aligns to 64)
@@ -541,7 +577,22 @@ class HipProgram:
         V, G = self.views, self.gviews
 
         # ---------------- forward ----------------
+        if self.pair is not None:
+            ua, ub = self.units[0], self.units[1]
+            nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
+            oslab = nt.slab if nt.has_bn else None
+            self._rc(lib.csa_conv_pair_fwd(
+                K.ints(self.pair), K.ptr(img), K.ptr(rows), K.ptr(cur),
+                K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
+                _act_id(ua.act), _alpha(ua.act),
+                K.ptr(V[f"{ub.layer.name}.weight"]), K.ptr(V.get(f"{ub.layer.name}.bias")) if ub.layer.spec.bias else None,
+                _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
+                self.lib.csa_conv_fwd_nslab(None, None), st), "conv_pair_fwd")
+            if oslab is not None and self.sync_bn:
+                e.sync.allreduce_tensors([oslab], tag="bnf1")
         for k, u in enumerate(self.units):
+            if self.pair is not None and k < 2:
+                continue
             lp, tf = u.layer, u.in_tf
             bn = self._bn_args(tf)
             in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
@@ -596,6 +647,13 @@ class HipProgram:
         # ---------------- backward ----------------
         for k in range(len(self.units) - 1, -1, -1):
             u = self.units[k]
+            if self.pair is not None and k < 2:
+                if k == 1:
+                    self._pair_bwd(st)
+                    self._grad_ready(1)
+                else:
+                    self._grad_ready(0)
+                continue
             lp, tf = u.layer, u.in_tf
             bn = self._bn_args(tf)
             in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
@@ -706,6 +764,33 @@ class HipProgram:
         else:
             e.after_backward_sync()
         self._optimizer(st)
+
+    def _pair_bwd(self, st) -> None:
+        e, lib = self.e, self.lib
+        ua, ub = self.units[0], self.units[1]
+        V, G = self.views, self.gviews
+        nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
+        if self.sync_bn and nt.has_bn:
+            e.sync.allreduce_tensors([nt.bwd_slab], tag="bnb2")
+        nbn = self._bn_args(nt)
+        dsc = G[f"{nt.norm.name}.scale"] if nt.has_bn else None
+        dof = G[f"{nt.norm.name}.offset"] if nt.has_bn else None
+        rm = rv = None
+        if nt.has_bn:
+            rm = getattr(self.model, f"bn{nt.norm.index}_mean")
+            rv = getattr(self.model, f"bn{nt.norm.index}_var")
+        rows, cur = e.stream.rows, e.stream.cursor
+        self._rc(lib.csa_conv_pair_bwd(
+            K.ints(self.pair), K.ptr(e.data.images), K.ptr(rows), K.ptr(cur),
+            K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
+            _act_id(ua.act), _alpha(ua.act), K.ptr(V[f"{ub.layer.name}.weight"]), 1 if ub.layer.spec.bias else 0,
+            _act_id(ub.act), _alpha(ub.act), K.ptr(ub.dy), K.ptr(ub.y), K.ptr(ub.argmax),
+            *nbn, K.ptr(nt.bwd_slab) if nt.has_bn else None, nt.bwd_nslab if nt.has_bn else 0,
+            K.ptr(dsc), K.ptr(dof), K.ptr(rm), K.ptr(rv), float(self.model.bn_momentum),
+            K.ptr(ua.dw_acc), K.ptr(ua.db_acc) if ua.layer.spec.bias else None,
+            K.ptr(ub.dw_acc), K.ptr(ub.db_acc) if ub.layer.spec.bias else None,
+            min(ua.wg_stripes, ub.wg_stripes), st), "conv_pair_bwd")
+        self._sync_bn_param_grads(nt)
 
     def _route_geom(self, u: Unit):
         lp, B = u.layer, self.B

@@ -50,6 +50,21 @@ CASES = {
         {"layer": "connect", "hidden": 100},
         {"layer": "active", "active_func": "sigmoid"},
     ],
+    "pair_relu_valid": [
+        {"layer": "conv", "filter": [3, 3, 6], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [3, 3, 8], "padding": "VALID", "isBias": "True"},
+        {"layer": "active", "active_func": "leaky_relu", "param": [0.1]},
+        {"layer": "pool"},
+        {"layer": "norm"},
+        {"layer": "connect", "hidden": 32},
+    ],
+    "pair_nopool": [
+        {"layer": "conv", "filter": [2, 2, 4]},
+        {"layer": "conv", "filter": [3, 3, 8]},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "connect", "hidden": 16},
+    ],
     "dense_only": [
         {"layer": "connect", "hidden": 128},
         {"layer": "active", "active_func": "relu"},
@@ -172,3 +187,12 @@ def test_fused_update_path_active_and_matches_unfused(monkeypatch):
         ma, mb = a.metrics_since(0), b.metrics_since(0)
         assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
         assert int(a.dstep.item()) == int(b.dstep.item()) == 5
+
+
+@pytest.mark.parametrize("name", ["sample", "pair_relu_valid", "pair_nopool"])
+def test_conv_pair_fused_active(name):
+    """The leading conv pair runs as the fused conv_pair kernels (one forward and one
+    backward launch) for these configs; numerics are pinned by test_step_matches_torch."""
+    ds = synthetic_mnist(200, seed=3)
+    eng = TrainEngine(_cfg(CASES[name]), ds, device="cuda", backend="hip", use_graph=False)
+    assert eng.program.pair is not None
