@@ -13,6 +13,10 @@ step (synchronous DP), so ``value`` is the whole-job samples/s.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         (N>1: torchrun --nproc-per-node N ... bench.py --gpus N)
+
+Multi-tenant (one GPU, K independent sample-config jobs; value = aggregate samples/s):
+        python bench.py --jobs K --pack graph   # one process, one graph with K branches
+        python bench.py --jobs K --pack procs   # K processes, one graph each
 """
 from __future__ import annotations
 
@@ -23,6 +27,115 @@ import sys
 import time
 
 BASELINE_SAMPLES_PER_S = 50 / 0.14209   # API.md:462-507 (mean of logged durations)
+
+
+def _sample_cfg(args):
+    from cloud_server_amd.models.dsl import SAMPLE_CONFIG, parse_train_config
+    cfg_json = dict(SAMPLE_CONFIG)
+    cfg_json["optimizer_name"] = args.optimizer
+    cfg_json["learning_rate"] = 1e-4 if args.optimizer == "AdagradOptimizer" else 0.01
+    cfg_json["options"] = {"batch_size": args.batch}
+    return parse_train_config(cfg_json)
+
+
+def _proc_job(rank, args, barrier, out_q):
+    """One packed job as its own process (own HIP context + graph)."""
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from cloud_server_amd.data.datasets import synthetic_mnist
+    from cloud_server_amd.runtime.engine import TrainEngine
+    cfg = _sample_cfg(args)
+    cfg.seed = rank
+    dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+    eng = TrainEngine(cfg, synthetic_mnist(60000, seed=rank), device=dev, backend=args.backend,
+                      use_graph=not args.no_graph)
+    for _ in range(args.warmup):
+        eng.step()
+    eng.sync_device()
+    barrier.wait()
+    for _ in range(args.steps):
+        eng.step()
+    eng.sync_device()
+    barrier.wait()
+    out_q.put((rank, eng.backend, eng.metrics_since(eng.host_step - min(args.steps, 100))["loss"]))
+
+
+def bench_packed(args) -> int:
+    """K independent jobs on ONE GPU; value = aggregate samples/s of all jobs."""
+    if args.gpus != 1:
+        raise SystemExit("--jobs packs jobs onto one GPU; run it with --gpus 1")
+    K = args.jobs
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if args.pack == "procs":
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")        # the parent never touches the GPU
+        barrier, out_q = ctx.Barrier(K + 1), ctx.Queue()
+        procs = [ctx.Process(target=_proc_job, args=(r, args, barrier, out_q)) for r in range(K)]
+        for p in procs:
+            p.start()
+        barrier.wait()
+        t0 = time.perf_counter()
+        barrier.wait()
+        dt = time.perf_counter() - t0
+        res = [out_q.get(timeout=600) for _ in range(K)]
+        for p in procs:
+            p.join()
+        if any(p.exitcode != 0 for p in procs):
+            raise SystemExit("a packed job process failed")
+        backend = res[0][1]
+        loss = sum(r[2] for r in res) / K
+    else:
+        import torch
+        from cloud_server_amd.data.datasets import synthetic_mnist
+        from cloud_server_amd.runtime.engine import TrainEngine
+        from cloud_server_amd.runtime.multijob import PackedJobs
+        dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+        engs = []
+        for r in range(K):
+            cfg = _sample_cfg(args)
+            cfg.seed = r
+            engs.append(TrainEngine(cfg, synthetic_mnist(60000, seed=r), device=dev,
+                                    backend=args.backend, use_graph=not args.no_graph))
+        pack = PackedJobs(engs)
+        for _ in range(args.warmup):
+            pack.step()
+        pack.sync_device()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pack.step()
+        pack.sync_device()
+        dt = time.perf_counter() - t0
+        backend = engs[0].backend
+        loss = sum(e.metrics_since(e.host_step - min(args.steps, 100))["loss"] for e in engs) / K
+    total = args.batch * K * args.steps / dt
+    out = {
+        "metric": "train_samples_per_s",
+        "value": round(total, 1),
+        "unit": "samples/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt * 1e3 / args.steps, 5),     # one step of EVERY job
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(total / BASELINE_SAMPLES_PER_S, 2),
+        "dtype": "fp32",
+        "data": "synthetic (MNIST-shaped 28x28 uint8, 60k samples per job, HBM-resident)",
+        "config": {
+            "model": "reference sample CNN (API.md:306-332), 2,276,218 params",
+            "jobs": K,
+            "pack": args.pack,
+            "per_job_batch": args.batch,
+            "global_batch": args.batch * K,
+            "seq_len": None,
+            "optimizer": args.optimizer,
+            "parallelism": f"{K} independent jobs / 1 GPU",
+            "backend": backend,
+        },
+        "final_loss": round(loss, 4),
+    }
+    print(json.dumps(out), flush=True)
+    return 0
 
 
 def main() -> int:
@@ -37,23 +150,22 @@ def main() -> int:
     ap.add_argument("--strategy", default="auto", choices=["auto", "allreduce", "ps", "lowrank"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--optimizer", default="AdagradOptimizer")
+    ap.add_argument("--jobs", type=int, default=1, help="independent jobs packed on one GPU")
+    ap.add_argument("--pack", default="graph", choices=["graph", "procs"])
     args = ap.parse_args()
+    if args.jobs > 1:
+        return bench_packed(args)
 
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from cloud_server_amd.data.datasets import synthetic_mnist
-    from cloud_server_amd.models.dsl import SAMPLE_CONFIG, parse_train_config
     from cloud_server_amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
     from cloud_server_amd.runtime.engine import TrainEngine
 
     ctx = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
     if args.strategy == "auto":
         args.strategy = "lowrank" if ctx.world > 1 else "allreduce"
-    cfg_json = dict(SAMPLE_CONFIG)
-    cfg_json["optimizer_name"] = args.optimizer
-    cfg_json["learning_rate"] = 1e-4 if args.optimizer == "AdagradOptimizer" else 0.01
-    cfg_json["options"] = {"batch_size": args.batch}
-    cfg = parse_train_config(cfg_json)
+    cfg = _sample_cfg(args)
     ds = synthetic_mnist(60000, seed=0)   # MNIST-shaped synthetic data (no network here)
     eng = TrainEngine(cfg, ds, device=ctx.device, ctx=ctx, backend=args.backend,
                       use_graph=not args.no_graph, strategy=args.strategy)

@@ -19,6 +19,8 @@ local defaults.
 | CSA_CORS_ORIGINS      | (none)                          | comma list of allowed CORS origins ("*" = any) |
 | CSA_HEARTBEAT_S       | 900                             | a running job silent this long is killed + failed |
 | CSA_ENABLE_DEMO       | 0                               | mount the demo "bills" routes (off, as in the reference) |
+| CSA_PACK_JOBS         | 1                               | single-GPU jobs on one GPU share a packed host process |
+| CSA_SLOTS_PER_GPU     | 4 packed / 1 unpacked           | concurrent jobs per GPU (profiles/r2_multitenant.md) |
 """
 from __future__ import annotations
 
@@ -48,6 +50,12 @@ class Settings:
                                                              if o.strip()])
     heartbeat_s: float = field(default_factory=lambda: float(_env("CSA_HEARTBEAT_S", "900")))
     enable_demo: bool = field(default_factory=lambda: _env("CSA_ENABLE_DEMO", "0") == "1")
+    # measured on one MI355X (bench.py --jobs K): K jobs packed as branches of one graph
+    # give 1.44x / 1.92x / 2.07x aggregate at K = 2 / 4 / 8, K separate processes give
+    # 0.75x / 0.68x / 0.69x — so pack, 4 per GPU (8 adds 8% for 2x per-job latency), and
+    # without packing run one job per GPU at a time
+    pack_jobs: bool = field(default_factory=lambda: _env("CSA_PACK_JOBS", "1") == "1")
+    slots_per_gpu: int = field(default_factory=lambda: int(_env("CSA_SLOTS_PER_GPU", "0")))
 
     def __post_init__(self):
         if not self.db_path:
@@ -55,6 +63,8 @@ class Settings:
         if self.gpus is None:
             g = _env("CSA_GPUS", "")
             self.gpus = [int(x) for x in g.split(",") if x.strip()] if g else None
+        if self.slots_per_gpu <= 0:
+            self.slots_per_gpu = 4 if self.pack_jobs else 1
         os.makedirs(self.storage_root, exist_ok=True)
 
     # ---- workspace layout, per user and model; no global scratch ----

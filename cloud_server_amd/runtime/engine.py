@@ -151,7 +151,9 @@ class TrainEngine:
         self.dstep.add_(1)
 
     # ---------------- host API ----------------
-    def _capture(self) -> None:
+    def _warm_up(self) -> None:
+        """Run the program twice off-graph (allocator, autotuning, RCCL comms), then undo
+        the warm-up's effect on the model state so capture starts from step 0's state."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         saved = (self.flat.clone(), self.slots.clone(), self.dstep.clone(),
@@ -165,6 +167,9 @@ class TrainEngine:
         self.flat.copy_(saved[0]); self.slots.copy_(saved[1])
         self.dstep.copy_(saved[2]); self.stream.cursor.copy_(saved[3])
         self.program.reset_after_warmup() if hasattr(self.program, "reset_after_warmup") else None
+
+    def _capture(self) -> None:
+        self._warm_up()
         g = torch.cuda.CUDAGraph()
         # thread_local: the RCCL watchdog thread queries events of earlier collectives while
         # this thread captures; in "global" mode that query aborts the process

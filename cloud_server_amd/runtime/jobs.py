@@ -8,6 +8,10 @@ C29; apps/construction/views.py:97-146) — with a local manager:
   follows ``queued -> running -> (paused | stopped | failed | done)``;
 * placement by the native GPU-slot scheduler (``runtime.scheduler``), several small jobs
   per GPU, data-parallel jobs over several GPUs;
+* packing (``settings.pack_jobs``): the single-GPU jobs placed on one GPU all run in that
+  GPU's host process (``runtime.gpu_host``) as branches of one HIP graph — measured
+  ~1.9x aggregate at 4 jobs, where 4 separate processes lose throughput
+  (profiles/r2_multitenant.md);
 * executors: ``process`` (default; one worker process per rank, started by a launcher
   process that is spawned before this process touches the GPU, so no process that
   initialised HIP ever forks/execs), ``thread`` and ``inline`` (tests, CPU);
@@ -99,7 +103,7 @@ def _free_port() -> int:
 
 class JobManager:
     def __init__(self, settings, db: Database, executor: Optional[str] = None,
-                 ngpu: Optional[int] = None, slots_per_gpu: int = 4):
+                 ngpu: Optional[int] = None, slots_per_gpu: Optional[int] = None):
         self.settings = settings
         self.db = db
         self.executor = executor or settings.executor
@@ -107,7 +111,12 @@ class JobManager:
             ngpu = self._count_gpus()
         self.ngpu = ngpu
         self.use_cpu = ngpu == 0
+        if slots_per_gpu is None:
+            slots_per_gpu = int(getattr(settings, "slots_per_gpu", 0) or 1)
+        self.pack = bool(getattr(settings, "pack_jobs", False)) and self.executor == "process"
+        self.slots_per_gpu = slots_per_gpu
         self.sched = make_scheduler(max(ngpu, 1), slots_per_gpu if ngpu else 2)
+        self.hosts: Dict[int, Dict[str, Any]] = {}     # packed host per GPU: spool, alive, jobs
         self.max_restarts = int(os.environ.get("CSA_MAX_RESTARTS", "2"))
         self.running: Dict[int, Dict[str, Any]] = {}
         self._lock = threading.RLock()
@@ -256,7 +265,8 @@ class JobManager:
             if now - last > limit and not info.get("killed"):
                 info["killed"] = True
                 info["kill_reason"] = f"no heartbeat for {now - last:.0f}s"
-                self._req.put(("kill", jid))
+                # a packed job shares its host process: a hung host takes its jobs along
+                self._req.put(("kill", self._host_id(info["host"]) if "host" in info else jid))
 
     def _admit(self) -> None:
         while True:
@@ -295,10 +305,11 @@ class JobManager:
             else:
                 threading.Thread(target=body, name=f"job-{jid}", daemon=True).start()
             return
-        env = dict(os.environ)
-        env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(os.path.dirname(os.path.dirname(
-            os.path.abspath(__file__))))] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+        env = self._worker_env()
         n = len(info["gpus"])
+        if self.pack and n == 1:
+            self._launch_packed(jid, info, env)
+            return
         if not self.use_cpu:
             env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, info["gpus"]))
         mod = ["-m", "cloud_server_amd.runtime.worker", "--model-dir", mdir, "--datatype", datatype,
@@ -314,15 +325,95 @@ class JobManager:
         info["launched"] = time.time()
         self._req.put(("launch", jid, argv, env, mdir, os.path.join(mdir, "worker.log")))
 
+    def _worker_env(self) -> Dict[str, str]:
+        env = dict(os.environ)
+        env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__))))] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+        return env
+
+    # ---- packed hosts: one process per GPU hosting its single-GPU jobs ----
+    @staticmethod
+    def _host_id(gpu: int) -> int:
+        return -(gpu + 1)             # launcher process key (job ids are positive)
+
+    def _launch_packed(self, jid: int, info: Dict[str, Any], env: Dict[str, str]) -> None:
+        gpu = info["gpus"][0]
+        with self._lock:
+            h = self.hosts.get(gpu)
+            if h is None or not h["alive"]:
+                spool = os.path.join(self.settings.storage_root, "gpu_hosts", f"gpu{gpu}")
+                os.makedirs(os.path.join(spool, "inbox"), exist_ok=True)
+                os.makedirs(os.path.join(spool, "done"), exist_ok=True)
+                h = {"spool": spool, "alive": True, "jobs": set()}
+                self.hosts[gpu] = h
+                if not self.use_cpu:
+                    env["HIP_VISIBLE_DEVICES"] = str(gpu)
+                env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+                argv = [sys.executable, "-m", "cloud_server_amd.runtime.gpu_host", "--spool", spool,
+                        "--device", "cpu" if self.use_cpu else "cuda:0",
+                        "--backend", self.settings.train_backend]
+                self._req.put(("launch", self._host_id(gpu), argv, env, spool, os.path.join(spool, "host.log")))
+            h["jobs"].add(jid)
+            info["host"] = gpu
+            info["launched"] = time.time()
+            inbox = os.path.join(h["spool"], "inbox")
+            tmp = os.path.join(inbox, f".{jid}.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"jid": jid, "model_dir": info["mdir"], "datatype": info["datatype"]}, f)
+            os.replace(tmp, os.path.join(inbox, f"{jid}.json"))
+
+    def _poll_hosts(self) -> None:
+        with self._lock:
+            hosts = list(self.hosts.items())
+        for gpu, h in hosts:
+            d = os.path.join(h["spool"], "done")
+            try:
+                names = [n for n in os.listdir(d) if n.endswith(".json")]
+            except OSError:
+                continue
+            for n in names:
+                p = os.path.join(d, n)
+                try:
+                    with open(p) as f:
+                        rec = json.load(f)
+                    os.remove(p)
+                except (OSError, json.JSONDecodeError):
+                    continue
+                jid = int(rec["jid"])
+                with self._lock:
+                    h["jobs"].discard(jid)
+                self._exited(jid, int(rec.get("rc", 1)))
+
+    def _host_exited(self, hid: int, rc: int) -> None:
+        gpu = -hid - 1
+        self._poll_hosts()                          # jobs that ended cleanly first
+        with self._lock:
+            h = self.hosts.get(gpu)
+            if h is None:
+                return
+            h["alive"] = False
+            orphans = list(h["jobs"])
+            h["jobs"].clear()
+        for jid in orphans:                         # the host died under them
+            with self._lock:
+                info = self.running.get(jid)
+            if info is not None and not info.get("kill_reason"):
+                info["kill_reason"] = f"gpu host exit code {rc}"
+            self._exited(jid, rc or 1)
+
     def _reap(self) -> None:
         if self._launcher is None:
             return
+        self._poll_hosts()
         while True:
             try:
                 _, jid, rc = self._resp.get_nowait()
             except queue.Empty:
                 return
-            self._exited(jid, rc)
+            if jid < 0:
+                self._host_exited(jid, rc)
+            else:
+                self._exited(jid, rc)
 
     def _exited(self, jid: int, rc: int) -> None:
         with self._lock:

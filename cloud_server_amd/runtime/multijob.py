@@ -1,0 +1,86 @@
+"""Multi-tenant packing: K independent training jobs sharing one MI355X.
+
+The reference ran exactly one job cluster-wide and killed the previous one on every
+submit (apps/construction/views.py:128-129); SURVEY §2.3 names packing as the real
+throughput lever, because one B=50 step of the sample CNN occupies only part of the 256
+CUs for ~126 µs and is bound by kernel latency, not by HBM or MFMA throughput.
+
+Two ways of sharing the card are provided (both measured by ``bench.py --jobs K``):
+
+* ``PackedJobs`` (in-process): each job keeps its own engine (weights, optimizer slots,
+  HBM-resident data, batch stream, metric ring), and ONE HIP graph holds a step of every
+  job as K independent branches forked onto K streams.  A replay is one
+  ``hipGraphLaunch`` and the branches' kernels overlap on the CUs, so the per-kernel
+  latency of one job hides behind the work of the others.
+* K processes (``runtime.jobs`` slot scheduler): each job is its own process with its own
+  HIP context and graph; the hardware queues interleave their launches.
+
+Every job's numerics are exactly those of a lone run: branches share no buffers, and each
+branch is the same kernel sequence its own engine would capture.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+
+from .engine import TrainEngine
+from ..utils.tracing import trace_range
+
+
+class PackedJobs:
+    def __init__(self, engines: Sequence[TrainEngine]):
+        if not engines:
+            raise ValueError("no jobs to pack")
+        devs = {e.device for e in engines}
+        if len(devs) != 1:
+            raise ValueError("packed jobs must share one device")
+        self.engines: List[TrainEngine] = list(engines)
+        self.device = engines[0].device
+        self.cuda = self.device.type == "cuda"
+        if any(e.ctx.enabled for e in engines):
+            raise ValueError("packed jobs are single-GPU jobs (no data-parallel group)")
+        self.graph = None
+        self.host_step = 0
+
+    def _capture(self) -> None:
+        for e in self.engines:
+            e._warm_up()
+        main = torch.cuda.current_stream(self.device)
+        streams = [torch.cuda.Stream(self.device) for _ in self.engines]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            cap = torch.cuda.current_stream(self.device)
+            for e, s in zip(self.engines, streams):
+                s.wait_stream(cap)            # fork: each job a branch of the graph
+                with torch.cuda.stream(s):
+                    e.program.run()
+            for s in streams:
+                cap.wait_stream(s)            # join
+        self.graph = g
+        self._streams = streams
+        del main
+
+    def step(self) -> None:
+        """One step of every job."""
+        for e in self.engines:
+            e.stream.before_step()
+        with trace_range("csa.packed_step"):
+            if self.cuda:
+                if self.graph is None:
+                    self._capture()
+                self.graph.replay()
+            else:
+                for e in self.engines:
+                    e.program.run()
+        for e in self.engines:
+            e.host_step += 1
+        self.host_step += 1
+
+    def sync_device(self) -> None:
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+
+    @property
+    def samples_per_step(self) -> int:
+        return sum(e.cfg.batch_size * e.ctx.world for e in self.engines)

@@ -182,113 +182,165 @@ class _MetricLog:
             self.fm.close()
 
 
+class JobRun:
+    """One training job's bookkeeping around an engine: resume, logging, heartbeats,
+    checkpoints, control actions, fault hooks and the final evaluation.  ``run_job``
+    drives it with the job's own engine; ``runtime.gpu_host`` drives several of them
+    with one packed graph (``runtime.multijob``), calling ``after_step`` for each job
+    after every packed step."""
+
+    def __init__(self, model_dir: str, config: Dict[str, Any], datatype: str = "file",
+                 device: Optional[str] = None, ctx: Optional[DistContext] = None,
+                 backend: str = "auto", data: Optional[tuple] = None):
+        self.model_dir = model_dir
+        self.ctx = ctx = ctx or DistContext()
+        self.chief = chief = ctx.is_chief
+        self.cfg = cfg = parse_train_config(config)
+        if device is None:
+            device = str(ctx.device) if ctx.enabled else ("cuda" if torch.cuda.is_available() else "cpu")
+        if chief:
+            write_status(model_dir, state="running", pid=os.getpid(), device=device, world=ctx.world)
+        self.ckpter = None
+        self.mlog = None
+        try:
+            train, self.test = data if data is not None else load_job_data(model_dir, datatype, cfg.ratio)
+            self.eng = eng = TrainEngine(cfg, train, device=device, ctx=ctx, backend=backend,
+                                         strategy=config.get("options", {}).get("strategy", "allreduce")
+                                         if isinstance(config.get("options"), dict) else "allreduce")
+            last = ckpt.latest(model_dir)
+            if last is not None:
+                ckpt.restore_engine(eng, ckpt.load(last[1]))
+            self.fault_at = _fault_step(ctx.rank, model_dir)                       # raise (crash) at this step
+            self.hang_at = int(os.environ.get("CSA_HANG_AT_STEP", "-1"))   # stop making progress (watchdog tests)
+            self.log_every = max(1, cfg.log_every)
+            # control / time-checkpoint decisions: every log point on one rank (a file stat); under
+            # data parallel they are a broadcast (a sync point), so every ~2000 steps
+            self.ctl_every = 1 if not ctx.enabled else max(1, 2000 // self.log_every)
+            self.ctl_path = os.path.join(model_dir, CONTROL)
+            self.ckpter = ckpt.AsyncCheckpointer(eng, model_dir)
+            self.mlog = _MetricLog(eng, chief, os.path.join(model_dir, RESULT),
+                                   os.path.join(model_dir, METRICS), ctx.world)
+        except Exception as exc:
+            self.fail(exc)
+            raise
+        self.t_ckpt = self.t_status = time.time()
+        self.int_start = eng.host_step
+        self.nlog = 0
+        self.state = "done"
+
+    # ---- the step loop, split so a packed host can interleave several jobs ----
+    def pending(self) -> bool:
+        return self.eng.host_step < self.cfg.iter
+
+    def before_step(self) -> None:
+        """Fault hooks for the step about to run (``eng.host_step``)."""
+        step = self.eng.host_step
+        if step == self.fault_at:
+            raise RuntimeError(f"injected fault at step {step} (rank {self.ctx.rank})")
+        if step == self.hang_at:
+            while True:
+                time.sleep(1.0)
+
+    def step(self) -> None:
+        eng, ctx = self.eng, self.ctx
+        step = eng.host_step
+        if ctx.enabled and eng.device.type == "cuda" and step % (self.ctl_every * self.log_every) == 1:
+            eng.probe_comm()            # per-rank collective time for metrics.jsonl
+        else:
+            eng.step()
+
+    def after_step(self) -> str:
+        """Bookkeeping after step ``host_step - 1`` ran; returns "" to continue, or the
+        state that ends the loop ("stopped" / "paused")."""
+        eng = self.eng
+        step = eng.host_step - 1
+        if step % self.log_every != 0:
+            return ""
+        # reference: the accuracy logged for step s is the batch of step s evaluated
+        # with the pre-update weights — exactly this step's forward pass
+        with trace_range("csa.log"):
+            self.mlog.mark(step, self.int_start)
+        self.int_start = eng.host_step
+        now = time.time()
+        if self.chief and (now - self.t_status > 1.0 or self.nlog == 0):
+            write_status(self.model_dir, step=eng.host_step, heartbeat=now)     # watchdog liveness
+            self.t_status = now
+        self.nlog += 1
+        if self.cfg.ckpt_every > 0 and step > 0 and step % self.cfg.ckpt_every == 0:
+            self.ckpter.save(self.chief)
+            self.t_ckpt = now
+        if self.nlog % self.ctl_every:
+            return ""
+        action = ""
+        if self.chief:
+            action = read_control(self.model_dir) if os.path.exists(self.ctl_path) else ""
+            if not action and self.cfg.ckpt_secs > 0 and now - self.t_ckpt >= self.cfg.ckpt_secs:
+                action = "ckpt"         # Supervisor(save_model_secs=60), construct_distribute.py:391
+        action = _agree(self.ctx, action)
+        if action == "ckpt":
+            with trace_range("csa.ckpt"):
+                self.ckpter.save(self.chief)
+            self.t_ckpt = now
+        elif action == "stop":
+            self.state = "stopped"
+            return "stopped"
+        elif action == "pause":
+            self.ckpter.save(self.chief)
+            self.ckpter.wait()
+            if self.chief:
+                write_status(self.model_dir, state="paused", step=eng.host_step)
+            self.state = "paused"
+            return "paused"
+        return ""
+
+    def finish(self) -> Dict[str, Any]:
+        eng, state, chief = self.eng, self.state, self.chief
+        eng.sync_device()
+        # a peer wait that timed out after the last log step left this rank's gradient
+        # un-reduced: fail before evaluating / checkpointing diverged parameters
+        eng.sync.check_agreed()
+        self.mlog.close()
+        final_acc = None
+        if state == "done":
+            final_acc = eng.evaluate(self.test) if len(self.test) else self.mlog.last_acc
+            if chief:
+                with open(os.path.join(self.model_dir, RESULT), "a") as f:
+                    f.write("final_accuracy:%f\n\n" % final_acc)
+        if state != "paused":
+            self.ckpter.save(chief)
+        self.ckpter.wait()
+        if chief:
+            write_status(self.model_dir, state=state, step=eng.host_step, final_accuracy=final_acc,
+                         backend=eng.backend, fallback=eng.fallback_reason)
+        return {"state": state, "step": eng.host_step, "final_accuracy": final_acc, "backend": eng.backend}
+
+    def fail(self, exc: BaseException) -> None:
+        if self.chief:
+            step = self.eng.host_step if hasattr(self, "eng") else 0
+            write_status(self.model_dir, state="failed", step=step, error=repr(exc),
+                         trace=traceback.format_exc()[-4000:])
+        try:
+            if self.ckpter is not None:
+                self.ckpter.wait()      # never leave a half-written checkpoint thread behind
+        except Exception:
+            pass
+
+
 def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",
             device: Optional[str] = None, ctx: Optional[DistContext] = None,
             backend: str = "auto", data: Optional[tuple] = None) -> Dict[str, Any]:
     """Train to ``config['iter']`` steps (resuming if a checkpoint exists).  Returns a
     summary dict.  Only rank 0 writes result/metrics/checkpoints."""
-    ctx = ctx or DistContext()
-    chief = ctx.is_chief
-    cfg = parse_train_config(config)
-    if device is None:
-        device = str(ctx.device) if ctx.enabled else ("cuda" if torch.cuda.is_available() else "cpu")
-    if chief:
-        write_status(model_dir, state="running", pid=os.getpid(), device=device, world=ctx.world)
-    train, test = data if data is not None else load_job_data(model_dir, datatype, cfg.ratio)
-    eng = TrainEngine(cfg, train, device=device, ctx=ctx, backend=backend,
-                      strategy=config.get("options", {}).get("strategy", "allreduce")
-                      if isinstance(config.get("options"), dict) else "allreduce")
-    last = ckpt.latest(model_dir)
-    if last is not None:
-        ckpt.restore_engine(eng, ckpt.load(last[1]))
-    fault_at = _fault_step(ctx.rank, model_dir)                                 # raise (crash) at this step
-    hang_at = int(os.environ.get("CSA_HANG_AT_STEP", "-1"))       # stop making progress (watchdog tests)
-    log_every = max(1, cfg.log_every)
-    # control / time-checkpoint decisions: every log point on one rank (a file stat); under
-    # data parallel they are a broadcast (a sync point), so every ~2000 steps
-    ctl_every = 1 if not ctx.enabled else max(1, 2000 // log_every)
-    ctl_path = os.path.join(model_dir, CONTROL)
-    ckpter = ckpt.AsyncCheckpointer(eng, model_dir)
-    mlog = _MetricLog(eng, chief, os.path.join(model_dir, RESULT), os.path.join(model_dir, METRICS), ctx.world)
-    t_ckpt = t_status = time.time()
-    int_start = eng.host_step
-    nlog = 0
-    state = "done"
+    job = JobRun(model_dir, config, datatype, device=device, ctx=ctx, backend=backend, data=data)
     try:
-        while eng.host_step < cfg.iter:
-            step = eng.host_step
-            if step == fault_at:
-                raise RuntimeError(f"injected fault at step {step} (rank {ctx.rank})")
-            if step == hang_at:
-                while True:
-                    time.sleep(1.0)
-            if ctx.enabled and eng.device.type == "cuda" and step % (ctl_every * log_every) == 1:
-                eng.probe_comm()            # per-rank collective time for metrics.jsonl
-            else:
-                eng.step()
-            if step % log_every != 0:
-                continue
-            # reference: the accuracy logged for step s is the batch of step s evaluated
-            # with the pre-update weights — exactly this step's forward pass
-            with trace_range("csa.log"):
-                mlog.mark(step, int_start)
-            int_start = eng.host_step
-            now = time.time()
-            if chief and (now - t_status > 1.0 or nlog == 0):
-                write_status(model_dir, step=eng.host_step, heartbeat=now)     # watchdog liveness
-                t_status = now
-            nlog += 1
-            if cfg.ckpt_every > 0 and step > 0 and step % cfg.ckpt_every == 0:
-                ckpter.save(chief)
-                t_ckpt = now
-            if nlog % ctl_every:
-                continue
-            action = ""
-            if chief:
-                action = read_control(model_dir) if os.path.exists(ctl_path) else ""
-                if not action and cfg.ckpt_secs > 0 and now - t_ckpt >= cfg.ckpt_secs:
-                    action = "ckpt"         # Supervisor(save_model_secs=60), construct_distribute.py:391
-            action = _agree(ctx, action)
-            if action == "ckpt":
-                with trace_range("csa.ckpt"):
-                    ckpter.save(chief)
-                t_ckpt = now
-            elif action == "stop":
-                state = "stopped"
+        while job.pending():
+            job.before_step()
+            job.step()
+            if job.after_step():
                 break
-            elif action == "pause":
-                ckpter.save(chief)
-                ckpter.wait()
-                if chief:
-                    write_status(model_dir, state="paused", step=eng.host_step)
-                state = "paused"
-                break
-        eng.sync_device()
-        # a peer wait that timed out after the last log step left this rank's gradient
-        # un-reduced: fail before evaluating / checkpointing diverged parameters
-        eng.sync.check_agreed()
-        mlog.close()
-        final_acc = None
-        if state == "done":
-            final_acc = eng.evaluate(test) if len(test) else mlog.last_acc
-            if chief:
-                with open(os.path.join(model_dir, RESULT), "a") as f:
-                    f.write("final_accuracy:%f\n\n" % final_acc)
-        if state != "paused":
-            ckpter.save(chief)
-        ckpter.wait()
-        if chief:
-            write_status(model_dir, state=state, step=eng.host_step, final_accuracy=final_acc,
-                         backend=eng.backend, fallback=eng.fallback_reason)
-        return {"state": state, "step": eng.host_step, "final_accuracy": final_acc, "backend": eng.backend}
+        return job.finish()
     except Exception as exc:
-        if chief:
-            write_status(model_dir, state="failed", step=eng.host_step, error=repr(exc),
-                         trace=traceback.format_exc()[-4000:])
-        try:
-            ckpter.wait()           # never leave a half-written checkpoint thread behind
-        except Exception:
-            pass
+        job.fail(exc)
         raise
 
 

@@ -82,14 +82,82 @@ def test_job_manager_process_executor_on_gpu(tmp_path):
             Image.fromarray(ds.images[i].reshape(28, 28)).save(os.path.join(mdir, "data", f"{i}.png"))
             tags[f"{i}.png"] = str(int(ds.labels[i]))
         json.dump(tags, open(os.path.join(mdir, "tag.json"), "w"))
-        jid = jm.submit(uid, "m", "file", _cfg(200))
-        state = jm.wait(jid, 400)
-        log = open(os.path.join(mdir, "worker.log")).read() if os.path.exists(os.path.join(mdir, "worker.log")) else ""
-        assert state == "done", log[-3000:]
-        st = jm.status(jid)
-        assert st["gpu"] == "0" and st["progress"]["backend"] == "hip"
+        os.makedirs(s.model_dir(uid, "m2"))
+        os.symlink(os.path.join(mdir, "data"), os.path.join(s.model_dir(uid, "m2"), "data"))
+        json.dump(tags, open(os.path.join(s.model_dir(uid, "m2"), "tag.json"), "w"))
+        # two jobs on one GPU: packed into that GPU's host process (settings.pack_jobs)
+        jids = [jm.submit(uid, "m", "file", _cfg(200)), jm.submit(uid, "m2", "file", _cfg(300))]
+        hlog = os.path.join(s.storage_root, "gpu_hosts", "gpu0", "host.log")
+        for jid in jids:
+            state = jm.wait(jid, 400)
+            log = open(hlog).read() if os.path.exists(hlog) else ""
+            assert state == "done", log[-3000:]
+            st = jm.status(jid)
+            assert st["gpu"] == "0" and st["progress"]["backend"] == "hip"
+        assert jm.status(jids[1])["progress"]["step"] == 300
     finally:
         jm.shutdown()
+
+
+def test_packed_hip_jobs_match_solo():
+    """K jobs as branches of one graph (runtime.multijob) train exactly like solo jobs
+    (atomic split-K sums: fp32 reassociation tolerance)."""
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    from cloud_server_amd.runtime.multijob import PackedJobs
+
+    def eng(seed):
+        c = _cfg(100, seed=seed)
+        c.update(optimizer_name="AdagradOptimizer", learning_rate=1e-3)
+        return TrainEngine(parse_train_config(c), synthetic_mnist(2000, seed=seed), device="cuda:0", backend="hip")
+
+    solo = [eng(s) for s in (1, 2, 3)]
+    for e in solo:
+        for _ in range(20):
+            e.step()
+    packed = [eng(s) for s in (1, 2, 3)]
+    assert all(e.backend == "hip" for e in solo + packed)
+    pack = PackedJobs(packed)
+    for _ in range(20):
+        pack.step()
+    pack.sync_device()
+    for a, b in zip(solo, packed):
+        torch.testing.assert_close(b.flat, a.flat, rtol=1e-3, atol=1e-4)
+        ma, mb = a.metrics_since(0), b.metrics_since(0)
+        assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, abs(ma["loss"]))
+
+
+def test_production_job_loop_matches_bench_throughput(tmp_path):
+    """The trainer loop (logging every 100 steps from the device metric ring, time-based
+    async checkpoints, control polling) keeps >= 90% of the bare engine's step rate."""
+    import time
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    c = json.loads(json.dumps(SAMPLE_CONFIG))
+    c.update(iter=20000, learning_rate=1e-4, optimizer_name="AdagradOptimizer")
+    c["options"] = dict(batch_size=50, ckpt_secs=1)        # several async checkpoints in the run
+    ds = synthetic_mnist(20000, seed=0)
+    e = TrainEngine(parse_train_config(c), ds, device="cuda:0", backend="hip")
+    for _ in range(200):
+        e.step()
+    e.sync_device()
+    t0 = time.perf_counter()
+    for _ in range(4000):
+        e.step()
+    e.sync_device()
+    bench = 50 * 4000 / (time.perf_counter() - t0)
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    t0 = time.perf_counter()
+    out = run_job(mdir, c, device="cuda:0", backend="hip", data=ds.split(0.95))
+    wall = time.perf_counter() - t0
+    assert out["state"] == "done" and out["backend"] == "hip"
+    rows = [json.loads(l) for l in open(os.path.join(mdir, "metrics.jsonl"))]
+    sps = sorted(r["samples_per_s"] for r in rows[5:])
+    median = sps[len(sps) // 2]
+    print(f"bench {bench:.0f} samples/s, job loop median {median:.0f} samples/s, "
+          f"{len(rows)} log lines, wall {wall:.1f}s, checkpoints kept {len(ckpt.list_checkpoints(mdir))}")
+    assert median >= 0.9 * bench, (median, bench)
 
 
 def test_node_status_reports_gpus_on_device():
