@@ -40,6 +40,7 @@ import time
 import zipfile
 from typing import Any, Dict, List, Optional
 
+import torch
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, Response
 from starlette.concurrency import run_in_threadpool
@@ -91,12 +92,19 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
     settings = settings or get_settings()
     db = Database(settings.db_path)
     jobs = JobManager(settings, db, executor=executor, ngpu=ngpu)
-    infer = InferenceService(device=inference_device or "cpu")
+    dev = inference_device or getattr(settings, "infer_device", "auto")
+    if dev == "auto":
+        try:                        # device_count() does not initialise HIP on this image
+            dev = "cuda:0" if torch.cuda.device_count() > 0 else "cpu"
+        except Exception:
+            dev = "cpu"
+    infer = InferenceService(device=dev)
 
     @contextlib.asynccontextmanager
     async def lifespan(_app):
         yield
         jobs.shutdown()
+        infer.close()
 
     app = FastAPI(title="cloud_server_amd", version="1.0", lifespan=lifespan)
     app.state.settings, app.state.db, app.state.jobs, app.state.infer = settings, db, jobs, infer
@@ -568,9 +576,12 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         if not os.path.isdir(mdir):
             return J(dict(FAIL_NO_MODEL))
         idir = os.path.join(mdir, "infer")
-        os.makedirs(idir, exist_ok=True)
-        with open(os.path.join(idir, os.path.basename(up.filename) or "image"), "wb") as out:
-            out.write(up.data)
+
+        def keep_upload():
+            os.makedirs(idir, exist_ok=True)
+            with open(os.path.join(idir, os.path.basename(up.filename) or "image"), "wb") as out:
+                out.write(up.data)
+        await run_in_threadpool(keep_upload)
         prep = str(request.query_params.get("prep", f.get("prep", "reference")))
         return J(await infer.predict_async(mdir, up.data, prep=prep))
 

@@ -19,6 +19,7 @@ local defaults.
 | CSA_CORS_ORIGINS      | (none)                          | comma list of allowed CORS origins ("*" = any) |
 | CSA_HEARTBEAT_S       | 900                             | a running job silent this long is killed + failed |
 | CSA_ENABLE_DEMO       | 0                               | mount the demo "bills" routes (off, as in the reference) |
+| CSA_INFER_DEVICE      | auto (cuda:0 when a GPU exists)  | device of the inference service (HIP forward) |
 | CSA_PACK_JOBS         | 1                               | single-GPU jobs on one GPU share a packed host process |
 | CSA_SLOTS_PER_GPU     | 4 packed / 1 unpacked           | concurrent jobs per GPU (profiles/r2_multitenant.md) |
 """
@@ -54,6 +55,7 @@ class Settings:
     # give 1.44x / 1.92x / 2.07x aggregate at K = 2 / 4 / 8, K separate processes give
     # 0.75x / 0.68x / 0.69x — so pack, 4 per GPU (8 adds 8% for 2x per-job latency), and
     # without packing run one job per GPU at a time
+    infer_device: str = field(default_factory=lambda: _env("CSA_INFER_DEVICE", "auto"))
     pack_jobs: bool = field(default_factory=lambda: _env("CSA_PACK_JOBS", "1") == "1")
     slots_per_gpu: int = field(default_factory=lambda: int(_env("CSA_SLOTS_PER_GPU", "0")))
 

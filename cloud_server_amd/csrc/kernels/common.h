@@ -129,7 +129,7 @@ __device__ __forceinline__ void slab_sum_to_lds(const float* slab, int nslab, in
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int r = r0 + u * per;
-          v[u] = slab[(size_t)(r < nslab ? r : lane_row) * C2 + col];
+          v[u] = slab[(size_t)(r < nslab ? r : 0) * C2 + col];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) pin(v[u]);

@@ -307,17 +307,20 @@ __global__ __launch_bounds__(IMG_THREADS) void resize_kernel(const uint8_t* __re
 }
 
 // ------------------------------------------------------------------ inference prep (C28)
-// [N, 20, 20] grayscale (already bicubic-resized by the decoder) -> [N, 784] float:
-// centred in a 28x28 canvas at offset 4, > 150 -> 254 else 0, / 255
-// (construct_inference.py:312-330).
-__global__ __launch_bounds__(256) void infer_prep_kernel(const uint8_t* __restrict__ in, float* __restrict__ out,
+// [N, 20, 20] grayscale (already bicubic-resized by the decoder) -> [N, 784]: centred in
+// a 28x28 canvas at offset 4, > 150 -> 254 else 0 (construct_inference.py:312-330).
+// float output: / 255 (the model input);  uint8 output: the 0 / 254 canvas itself, which
+// the HIP forward kernels read like a dataset image (u8 / 255: the same float input).
+template <class T>
+__global__ __launch_bounds__(256) void infer_prep_kernel(const uint8_t* __restrict__ in, T* __restrict__ out,
                                                          long total) {
+  constexpr float hi = sizeof(T) == 1 ? 254.f : 254.f / 255.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long n = i / 784;
     const int r = (int)(i - n * 784), y = r / 28 - 4, x = r % 28 - 4;
     float v = 0.f;
-    if (y >= 0 && y < 20 && x >= 0 && x < 20) v = in[n * 400 + y * 20 + x] > 150 ? 254.f / 255.f : 0.f;
-    out[i] = v;
+    if (y >= 0 && y < 20 && x >= 0 && x < 20) v = in[n * 400 + y * 20 + x] > 150 ? hi : 0.f;
+    out[i] = (T)v;
   }
 }
 
@@ -417,6 +420,13 @@ CSA_API int csa_img_resize(const uint8_t* in, uint8_t* out, int N, int h, int w,
 CSA_API int csa_img_infer_prep(const uint8_t* in, float* out, int N, hipStream_t st) {
   if (N <= 0) return -1;
   const long total = (long)N * 784;
-  hipLaunchKernelGGL(infer_prep_kernel, dim3(grid_for(total)), dim3(256), 0, st, in, out, total);
+  hipLaunchKernelGGL(infer_prep_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, in, out, total);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_infer_prep_u8(const uint8_t* in, uint8_t* out, int N, hipStream_t st) {
+  if (N <= 0) return -1;
+  const long total = (long)N * 784;
+  hipLaunchKernelGGL(infer_prep_kernel<uint8_t>, dim3(grid_for(total)), dim3(256), 0, st, in, out, total);
   return (int)hipGetLastError();
 }

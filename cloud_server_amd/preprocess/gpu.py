@@ -35,6 +35,7 @@ _SIGS = {
     "csa_img_salt_pepper": (C.c_int, [K.P, K.I, K.I, K.I, K.P, K.I, K.P]),
     "csa_img_resize": (C.c_int, [K.P, K.P, K.I, K.I, K.I, K.I, K.P, K.P, K.P, K.P, K.P]),
     "csa_img_infer_prep": (C.c_int, [K.P, K.P, K.I, K.P]),
+    "csa_img_infer_prep_u8": (C.c_int, [K.P, K.P, K.I, K.P]),
 }
 _bound = False
 

@@ -549,6 +549,9 @@ class HipProgram:
         if not tf.has_bn:
             return (None, 0, 0.0, 0.0, None, None)
         name = tf.norm.name
+        if self._eval_bn:
+            return (K.ptr(tf.eval_slab), 1, 1.0, float(tf.norm.spec.epsilon),
+                    K.ptr(self.views[f"{name}.scale"]), K.ptr(self.views[f"{name}.offset"]))
         return (K.ptr(tf.slab), tf.nslab, tf.count, float(tf.norm.spec.epsilon),
                 K.ptr(self.views[f"{name}.scale"]), K.ptr(self.views[f"{name}.offset"]))
 
@@ -570,57 +573,9 @@ class HipProgram:
         # this step's dataset rows = stream.rows[cursor]; the kernels resolve the cursor on
         # device and the optimizer launch advances it (no torch index/add launches).
         rows, cur = e.stream.rows, e.stream.cursor
-        if self.__dict__.get("x_dense_in") is not None:
-            idx = rows.index_select(0, cur).view(-1)
-            self.x_dense_in.copy_(e.data.images.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
         img = e.data.images
         V, G = self.views, self.gviews
-
-        # ---------------- forward ----------------
-        if self.pair is not None:
-            ua, ub = self.units[0], self.units[1]
-            nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
-            oslab = nt.slab if nt.has_bn else None
-            self._rc(lib.csa_conv_pair_fwd(
-                K.ints(self.pair), K.ptr(img), K.ptr(rows), K.ptr(cur),
-                K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
-                _act_id(ua.act), _alpha(ua.act),
-                K.ptr(V[f"{ub.layer.name}.weight"]), K.ptr(V.get(f"{ub.layer.name}.bias")) if ub.layer.spec.bias else None,
-                _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
-                self.lib.csa_conv_fwd_nslab(None, None), st), "conv_pair_fwd")
-            if oslab is not None and self.sync_bn:
-                e.sync.allreduce_tensors([oslab], tag="bnf1")
-        for k, u in enumerate(self.units):
-            if self.pair is not None and k < 2:
-                continue
-            lp, tf = u.layer, u.in_tf
-            bn = self._bn_args(tf)
-            in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
-            next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
-            if u.kind == "conv":
-                oslab = next_tf.slab if next_tf.has_bn else None
-                raw = u.x is None
-                self._rc(lib.csa_conv_fwd(
-                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
-                    K.ptr(V[f"{lp.name}.weight"]), K.ptr(V.get(f"{lp.name}.bias")) if lp.spec.bias else None,
-                    K.ptr(u.y), K.ptr(u.argmax), K.ptr(oslab),
-                    self._conv_geom(lp, B), self._pool_geom(u), *bn, in_act, in_alpha,
-                    _act_id(u.act), _alpha(u.act), K.ptr(cur) if raw else None, st), "conv_fwd")
-                if oslab is not None and self.sync_bn:
-                    e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
-            else:
-                fin, fout = lp.in_shape.numel, lp.spec.hidden
-                if u.xt is not None:
-                    self._rc(lib.csa_bn_act_apply(
-                        K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha, st),
-                        "bn_act_apply")
-                    self._rc(lib.csa_dense_fwd(
-                        K.ptr(u.xt), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
-                        B, fout, fin, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, st), "dense_fwd")
-                else:
-                    self._rc(lib.csa_dense_fwd(
-                        K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
-                        B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
+        self._forward(st)
 
         self._lowrank_gather_inputs()
 
@@ -764,6 +719,103 @@ class HipProgram:
         else:
             e.after_backward_sync()
         self._optimizer(st)
+
+    # ------------------------------------------------------------------ forward
+    _eval_bn = False          # predict: BN with running statistics (no batch-stat slabs)
+
+    def _forward(self, st) -> None:
+        """Every unit's forward launch (the first half of ``run``; ``predict`` reuses it)."""
+        e, lib, B = self.e, self.lib, self.B
+        rows, cur = e.stream.rows, e.stream.cursor
+        if self.__dict__.get("x_dense_in") is not None:
+            idx = rows.index_select(0, cur).view(-1)
+            self.x_dense_in.copy_(e.data.images.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
+        img = e.data.images
+        V = self.views
+        # ---------------- forward ----------------
+        if self.pair is not None:
+            ua, ub = self.units[0], self.units[1]
+            nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
+            oslab = nt.slab if nt.has_bn and not self._eval_bn else None
+            self._rc(lib.csa_conv_pair_fwd(
+                K.ints(self.pair), K.ptr(img), K.ptr(rows), K.ptr(cur),
+                K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
+                _act_id(ua.act), _alpha(ua.act),
+                K.ptr(V[f"{ub.layer.name}.weight"]), K.ptr(V.get(f"{ub.layer.name}.bias")) if ub.layer.spec.bias else None,
+                _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
+                self.lib.csa_conv_fwd_nslab(None, None), st), "conv_pair_fwd")
+            if oslab is not None and self.sync_bn:
+                e.sync.allreduce_tensors([oslab], tag="bnf1")
+        for k, u in enumerate(self.units):
+            if self.pair is not None and k < 2:
+                continue
+            lp, tf = u.layer, u.in_tf
+            bn = self._bn_args(tf)
+            in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
+            next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
+            if u.kind == "conv":
+                oslab = next_tf.slab if next_tf.has_bn and not self._eval_bn else None
+                raw = u.x is None
+                self._rc(lib.csa_conv_fwd(
+                    None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
+                    K.ptr(V[f"{lp.name}.weight"]), K.ptr(V.get(f"{lp.name}.bias")) if lp.spec.bias else None,
+                    K.ptr(u.y), K.ptr(u.argmax), K.ptr(oslab),
+                    self._conv_geom(lp, B), self._pool_geom(u), *bn, in_act, in_alpha,
+                    _act_id(u.act), _alpha(u.act), K.ptr(cur) if raw else None, st), "conv_fwd")
+                if oslab is not None and self.sync_bn:
+                    e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
+            else:
+                fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if u.xt is not None:
+                    self._rc(lib.csa_bn_act_apply(
+                        K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha, st),
+                        "bn_act_apply")
+                    self._rc(lib.csa_dense_fwd(
+                        K.ptr(u.xt), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
+                        B, fout, fin, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, st), "dense_fwd")
+                else:
+                    self._rc(lib.csa_dense_fwd(
+                        K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
+                        B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
+
+
+    def predict_logits_into(self, logits: torch.Tensor) -> None:
+        """Forward-only pass over this program's input rows -> ``logits`` [B, 10] (graph
+        capturable; ``serve.hip_infer`` captures it per batch bucket).  BatchNorm uses the
+        running statistics unless the model normalises with batch statistics in eval
+        (``bn_mode == "batch"``), exactly as ``DigitNet.forward`` in eval mode."""
+        st = K.stream()
+        self._eval_bn = self.model.bn_mode != "batch"
+        # split-K forward outputs (and, with batch statistics, the forward BN slabs) are
+        # atomic accumulators that the training step's optimizer launch re-zeroes
+        for u in self.units:
+            if u.kind == "dense" and u.splits_fwd > 1:
+                u.y.zero_()
+            if not self._eval_bn and u.in_tf.has_bn:
+                u.in_tf.slab.zero_()
+        try:
+            if self._eval_bn:
+                for tf in [u.in_tf for u in self.units] + [self.head_tf]:
+                    if tf.has_bn:
+                        # a 1-row slab whose {sum, sumsq} / count=1 IS {mean, var + mean^2}
+                        if getattr(tf, "eval_slab", None) is None:
+                            tf.eval_slab = torch.zeros(1, 2, tf.slab.shape[2], device=self.e.device)
+                        rm = getattr(self.model, f"bn{tf.norm.index}_mean")
+                        rv = getattr(self.model, f"bn{tf.norm.index}_var")
+                        tf.eval_slab[0, 0].copy_(rm)
+                        torch.addcmul(rv, rm, rm, out=tf.eval_slab[0, 1])
+            self._forward(st)
+        finally:
+            self._eval_bn = False
+        last = self.units[-1]
+        hin = last.y.view(self.B, -1)
+        Kh = hin.shape[1]
+        if self.lib.csa_dense_fwd_splits(self.B, 10, Kh) > 1:
+            logits.zero_()
+        self._rc(self.lib.csa_dense_fwd(
+            K.ptr(hin), K.ptr(self.views["head.weight"]), K.ptr(self.views["head.bias"]), K.ptr(logits),
+            self.B, 10, Kh, None, 0, 0, 0.0, 0.0, None, None,
+            _act_id(self.head_tf.act), _alpha(self.head_tf.act), st), "head_fwd")
 
     def _pair_bwd(self, st) -> None:
         e, lib = self.e, self.lib

@@ -376,3 +376,45 @@ def test_tracing_ranges_wired(monkeypatch):
     assert calls.count("csa.step") == 2
     assert tracing.enabled() == any(os.path.exists(os.path.join("/opt/rocm/lib", n))
                                     for n in ("librocprofiler-sdk-roctx.so.1", "libroctx64.so.4"))
+
+
+def test_inference_micro_batcher_groups_concurrent_requests(tmp_path):
+    """Requests queued while a batch runs are served by ONE forward (serve.inference)."""
+    import threading
+    from cloud_server_amd.serve.inference import _Batcher
+    gate = threading.Event()
+    sizes = []
+
+    def fn(xs):
+        gate.wait(5)
+        sizes.append(len(xs))
+        return xs[:, 0] * 2
+
+    b = _Batcher(fn)
+    futs = [b.submit(np.array([i], np.int64)) for i in range(10)]
+    time.sleep(0.1)
+    gate.set()
+    assert [f.result(5) for f in futs] == [2 * i for i in range(10)]
+    assert sum(sizes) == 10 and len(sizes) <= 2
+    b.close()
+
+
+def test_inference_service_async_path_cpu(tmp_path):
+    import asyncio
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    run_job(mdir, dict(SMALL, iter=10), device="cpu", backend="torch", data=_data())
+    svc = InferenceService(device="cpu")
+    imgs = []
+    for i in range(6):
+        b = io.BytesIO()
+        Image.fromarray(synthetic_mnist(6, seed=9).images[i].reshape(28, 28)).save(b, format="PNG")
+        imgs.append(b.getvalue())
+
+    async def go():
+        return await asyncio.gather(*[svc.predict_async(mdir, im, prep="mnist") for im in imgs])
+    out = asyncio.run(go())
+    sync = [svc.predict(mdir, im, prep="mnist") for im in imgs]
+    assert out == sync and all(o["result"] == "success" for o in out)
+    assert svc.latency_ms()["n"] == 12
+    svc.close()
