@@ -163,10 +163,15 @@ def main() -> int:
     from cloud_server_amd.runtime.engine import TrainEngine
 
     ctx = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
-    if args.strategy == "auto":
-        args.strategy = "lowrank" if ctx.world > 1 else "allreduce"
     cfg = _sample_cfg(args)
     ds = synthetic_mnist(60000, seed=0)   # MNIST-shaped synthetic data (no network here)
+    tuning = {}
+    if args.strategy == "auto":
+        # N > 1: time lowrank (all-gather the dense GEMM operands, W x fc1 wgrad FLOPs) vs
+        # allreduce (9.1 MB gradient, one-/two-shot xGMI or RCCL per bucket) on a few real
+        # steps and keep the faster (parallel/strategy.py; same answer on every rank)
+        from cloud_server_amd.parallel.strategy import pick_strategy
+        args.strategy, tuning = pick_strategy(cfg, ds, ctx, backend=args.backend)
     eng = TrainEngine(cfg, ds, device=ctx.device, ctx=ctx, backend=args.backend,
                       use_graph=not args.no_graph, strategy=args.strategy)
 
@@ -217,6 +222,7 @@ def main() -> int:
                                or ("rccl" if ctx.world > 1 else "none"),
                 "xgmi": eng.sync.xgmi_reason,
                 "collective_tuning_us": eng.sync.xgmi_tuning,
+                "strategy_tuning_ms_per_step": tuning,
             },
             "final_loss": round(m["loss"], 4),
             "final_batch_accuracy": round(m["accuracy"], 4),

@@ -11,6 +11,16 @@
 //   * all-gather  — copy the world slots of its chunk into the rank-major output;
 //   * all-reduce  — sum the world slots of its chunk (fp32) into the in/out tensor.
 //
+// One-shot all-reduce sends (W-1) x the message out of every GPU: right for small,
+// latency-bound messages.  For large ones (a whole 9.1 MB gradient: 63.7 MB of egress at
+// W=8) the TWO-SHOT all-reduce (op 2) sends 2 (W-1)/W x the message instead:
+//   phase 1 (reduce-scatter): shard j of the message goes ONLY to rank j, which sums the
+//     W contributions of its shard in fixed rank order;
+//   phase 2 (all-gather): rank j pushes its reduced shard to every peer.
+// Block b owns sub-chunk b of EVERY shard in both phases, so the shard a block reduces is
+// exactly the one it broadcasts: no cross-block dependency on either side.  Same flag /
+// epoch / parity protocol, one flag array per phase; bitwise identical on every rank.
+//
 // Protocol details
 //   * receive buffers and flags are allocated uncached (hipDeviceMallocUncached), so a
 //     reader never hits a stale L2 line written by a peer (XCD/L2 non-coherence);
@@ -39,8 +49,9 @@ struct XgSeg { const char* src; char* dst; long bytes; long off; };
 struct XgArgs {
   int op, rank, world, nseg;
   long msg_bytes, slot_bytes;
-  char* buf[XG_MAXR];           // rank r's receive buffer [2][world][slot_bytes] (mapped)
-  unsigned* flags[XG_MAXR];     // rank r's flags [2][XG_MAXB][XG_MAXR] (mapped)
+  char* buf[XG_MAXR];           // rank r's receive buffer [2][world][slot_bytes] (mapped);
+                                // two-shot: [2 parity][2 phase][world][shard] in the same bytes
+  unsigned* flags[XG_MAXR];     // rank r's flags [2 phase][2 parity][XG_MAXB][XG_MAXR] (mapped)
   XgSeg seg[XG_MAXSEG];
   unsigned* seq; unsigned* done; int* err;
   unsigned long long timeout_ticks;
@@ -53,6 +64,112 @@ __device__ __forceinline__ int xg_find(const XgArgs& a, long off) {
   return s;
 }
 
+// Publish this block's stores of one phase, then raise its flags (value e) in every rank.
+__device__ __forceinline__ void xg_publish(const XgArgs& a, long fidx, unsigned e) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    for (int p = 0; p < a.world; ++p)
+      __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wait (bounded) until every source raised flag value e at fidx in this rank; returns
+// false (and poisons the channel) on timeout.  Every thread must call.
+__device__ __forceinline__ bool xg_wait(const XgArgs& a, long fidx, unsigned e, int* s_abort) {
+  if (threadIdx.x == 0) {
+    const unsigned* f = a.flags[a.rank] + fidx;
+    const unsigned long long t0 = wall_clock64();
+    for (int r = 0; r < a.world && !*s_abort; ++r) {
+      while (__hip_atomic_load(f + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+        if (wall_clock64() - t0 > a.timeout_ticks) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  return !*s_abort;
+}
+
+__device__ __forceinline__ const char* xg_src(const XgArgs& a, long off) {
+  const XgSeg& s = a.seg[xg_find(a, off)];
+  return s.src + (off - s.off);
+}
+
+__device__ __forceinline__ char* xg_dst(const XgArgs& a, long off) {
+  const XgSeg& s = a.seg[xg_find(a, off)];
+  return s.dst + (off - s.off);
+}
+
+// Two-shot fp32 sum all-reduce (op 2): see the header comment.
+__device__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
+  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x, W = a.world;
+  const int par = e & 1u;
+  const long units = a.msg_bytes >> 4;
+  const long S = (units + W - 1) / W;                 // 16-byte units per shard
+  const long shard = S << 4;
+  const long per = (S + nb - 1) / nb;
+  const long v0 = b * per < S ? b * per : S;
+  const long v1 = v0 + per < S ? v0 + per : S;
+  const long area0 = ((long)par * 2 + 0) * W * shard;   // phase-1 slots [src][shard]
+  const long area1 = ((long)par * 2 + 1) * W * shard;   // phase-2 slots [owner][shard]
+  const long f1 = ((long)(0 * 2 + par) * XG_MAXB + b) * XG_MAXR;
+  const long f2 = ((long)(1 * 2 + par) * XG_MAXB + b) * XG_MAXR;
+
+  // phase 1: my contribution to shard p -> rank p's slot [my rank]
+  for (long v = v0 + t; v < v1; v += blockDim.x) {
+#pragma unroll
+    for (int p = 0; p < XG_MAXR; ++p) {
+      if (p >= W) break;
+      const long u = p * S + v;
+      if (u < units) {
+        const uint4 x = *reinterpret_cast<const uint4*>(xg_src(a, u << 4));
+        *reinterpret_cast<uint4*>(a.buf[p] + area0 + (long)a.rank * shard + (v << 4)) = x;
+      }
+    }
+  }
+  xg_publish(a, f1, e);
+  if (!xg_wait(a, f1, e, s_abort)) return;
+
+  // reduce my shard's sub-chunk (fixed rank order), push the sum to every rank's slot [me]
+  const char* mine0 = a.buf[a.rank] + area0;
+  for (long v = v0 + t; v < v1; v += blockDim.x) {
+    const long u = (long)a.rank * S + v;
+    if (u >= units) break;
+    float4 x[XG_MAXR];
+#pragma unroll
+    for (int r = 0; r < XG_MAXR; ++r)
+      if (r < W) x[r] = *reinterpret_cast<const float4*>(mine0 + (long)r * shard + (v << 4));
+    float4 acc = x[0];
+#pragma unroll
+    for (int r = 1; r < XG_MAXR; ++r)
+      if (r < W) { acc.x += x[r].x; acc.y += x[r].y; acc.z += x[r].z; acc.w += x[r].w; }
+#pragma unroll
+    for (int p = 0; p < XG_MAXR; ++p)
+      if (p < W) *reinterpret_cast<float4*>(a.buf[p] + area1 + (long)a.rank * shard + (v << 4)) = acc;
+  }
+  xg_publish(a, f2, e);
+  if (!xg_wait(a, f2, e, s_abort)) return;
+
+  // phase 2 consume: every owner's reduced sub-chunk -> the output
+  const char* mine1 = a.buf[a.rank] + area1;
+  for (long v = v0 + t; v < v1; v += blockDim.x) {
+    uint4 x[XG_MAXR];
+#pragma unroll
+    for (int r = 0; r < XG_MAXR; ++r)
+      if (r < W && r * S + v < units) x[r] = *reinterpret_cast<const uint4*>(mine1 + (long)r * shard + (v << 4));
+#pragma unroll
+    for (int r = 0; r < XG_MAXR; ++r)
+      if (r < W && r * S + v < units) *reinterpret_cast<uint4*>(xg_dst(a, (r * S + v) << 4)) = x[r];
+  }
+}
+
 __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   __shared__ int s_abort;
   const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
@@ -61,6 +178,9 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   if (s_abort) return;
   const unsigned e = *a.seq + 1u;
   const int par = e & 1u;
+  if (a.op == 2) {
+    xg_twoshot(a, e, &s_abort);
+  } else {
   // this block's chunk of the packed per-rank message, in 16-byte units
   const long units = a.msg_bytes >> 4;
   const long per = (units + nb - 1) / nb;
@@ -136,6 +256,7 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
       }
     }
   }
+  }
 
   // 4) the last block to finish advances the epoch for the next call on this channel
   __syncthreads();
@@ -191,6 +312,10 @@ CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* con
     off += seg_bytes[i];
   }
   if (off > slot_bytes) return -3;
+  if (op == 2) {                // [2 parity][2 phase][world][shard] must fit the slot area
+    const long S = ((off >> 4) + world - 1) / world;
+    if (4L * world * (S << 4) > 2L * world * slot_bytes + 64L * world) return -4;
+  }
   a.msg_bytes = off;
   for (int r = 0; r < world; ++r) {
     a.buf[r] = static_cast<char*>(bufs[r]);

@@ -30,7 +30,7 @@ from __future__ import annotations
 
 import contextlib
 import os
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -138,8 +138,15 @@ class GradSync:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         choice = ch if flag.item() else None
         if choice is not None and self.xgmi_mode == "auto":
-            xg_us, rc_us = self._time_paths(ch, srcs, dsts)
-            self.xgmi_tuning[tag] = {"bytes": nbytes, "xgmi_us": round(xg_us, 2), "rccl_us": round(rc_us, 2)}
+            times = self._time_paths(ch, srcs, dsts)
+            rc_us = times.pop("rccl")
+            proto = min(times, key=times.get)
+            xg_us = times[proto]
+            self.xgmi_tuning[tag] = {"bytes": nbytes, "rccl_us": round(rc_us, 2),
+                                     **{f"{k}_us": round(v, 2) for k, v in times.items()}}
+            if dsts is None:
+                ch.protocol = proto       # all-reduce: the faster xGMI protocol
+                self.xgmi_tuning[tag]["protocol"] = proto
             # a peer wait that timed out during the timing poisons the channel (and would
             # make it look fast): every rank then drops it and stays on RCCL
             healthy = torch.tensor([0 if ch.error() else 1], dtype=torch.int32, device=self.ctx.device)
@@ -154,16 +161,21 @@ class GradSync:
         self._choice[tag] = choice
         return choice
 
-    def _time_paths(self, ch, srcs, dsts) -> Tuple[float, float]:
+    def _time_paths(self, ch, srcs, dsts) -> Dict[str, float]:
+        """µs per call of each candidate (max over ranks): all-reduce sites time the
+        one-shot and two-shot xGMI protocols and RCCL; gather sites xGMI and RCCL."""
         dev = self.ctx.device
         ss = [torch.zeros_like(t) for t in srcs]
         sd = None if dsts is None else [torch.empty_like(d) for d in dsts]
 
-        def xg():
+        def one():
             if sd is None:
-                ch.all_reduce(ss)
+                ch.all_reduce(ss, protocol="oneshot")
             else:
                 ch.all_gather(list(zip(ss, sd)))
+
+        def two():
+            ch.all_reduce(ss, protocol="twoshot")
 
         def rc():
             for i, t in enumerate(ss):
@@ -172,8 +184,11 @@ class GradSync:
                 else:
                     dist.all_gather_into_tensor(sd[i], t)
 
+        cands = {"oneshot" if sd is None else "xgmi": one, "rccl": rc}
+        if sd is None and self.ctx.world > 2:
+            cands["twoshot"] = two
         out = []
-        for fn in (xg, rc):
+        for fn in cands.values():
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
@@ -197,7 +212,7 @@ class GradSync:
             del g
         t = torch.tensor(out, dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t[0]), float(t[1])
+        return {k: float(v) for k, v in zip(cands, t.tolist())}
 
     @property
     def grad_scale(self) -> float:

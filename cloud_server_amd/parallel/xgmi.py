@@ -29,7 +29,11 @@ import torch.distributed as dist
 
 from ..ops import fused as K
 
-OP_GATHER, OP_ALLREDUCE = 0, 1
+OP_GATHER, OP_ALLREDUCE, OP_ALLREDUCE_2SHOT = 0, 1, 2
+# default protocol crossover (per-rank message bytes) until the start-up tuner measured
+# both on the real links: one-shot below (one flag round trip), two-shot above (2 (W-1)/W
+# of the message leaves each GPU instead of (W-1) x)
+TWO_SHOT_MIN_BYTES = int(os.environ.get("CSA_XGMI_TWOSHOT_KB", "256")) * 1024
 
 
 def _aligned(t: torch.Tensor) -> bool:
@@ -47,7 +51,8 @@ class XgmiChannel:
         self.timeout_s = timeout_s
         hb = self.lib.csa_xgmi_handle_bytes()
         nblk = self.lib.csa_xgmi_max_blocks()
-        sizes = (2 * world * self.slot_bytes, 2 * nblk * 8 * 4)
+        # receive slots (+ slack: two-shot shards round up to 16 B) and per-phase flags
+        sizes = (2 * world * self.slot_bytes + 64 * world, 2 * 2 * nblk * 8 * 4)
         self._local: List[int] = []
         self._opened: List[int] = []
         # every failure is agreed on collectively (all ranks raise together), so a rank
@@ -97,6 +102,8 @@ class XgmiChannel:
         # workgroups per call (0: one per ~8 KB of the per-rank message, at most 256)
         kb = int(os.environ.get("CSA_XGMI_BLOCK_KB", "0"))
         self.nblocks = 0 if kb <= 0 else max(1, min(nblk, -(-self.slot_bytes // (kb * 1024))))
+        # all-reduce protocol: None = by size (TWO_SHOT_MIN_BYTES); the tuner pins it
+        self.protocol: Optional[str] = os.environ.get("CSA_XGMI_PROTOCOL") or None
 
     # ---------------------------------------------------------------- calls
     def _run(self, op: int, srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
@@ -114,9 +121,15 @@ class XgmiChannel:
         """``out`` = rank-major concatenation of every rank's ``local`` (per pair)."""
         self._run(OP_GATHER, [p[0] for p in pairs], [p[1] for p in pairs])
 
-    def all_reduce(self, tensors: Sequence[torch.Tensor]) -> None:
-        """In-place fp32 SUM over ranks (identical bits on every rank: fixed rank order)."""
-        self._run(OP_ALLREDUCE, tensors, tensors)
+    def all_reduce(self, tensors: Sequence[torch.Tensor], protocol: Optional[str] = None) -> None:
+        """In-place fp32 SUM over ranks (identical bits on every rank: fixed rank order).
+        ``protocol``: "oneshot" (push everything to everyone), "twoshot" (reduce-scatter +
+        all-gather), default the channel's pinned choice or the size crossover."""
+        p = protocol or self.protocol
+        if p is None:
+            nbytes = sum(t.numel() * t.element_size() for t in tensors)
+            p = "twoshot" if nbytes >= TWO_SHOT_MIN_BYTES and self.world > 2 else "oneshot"
+        self._run(OP_ALLREDUCE_2SHOT if p == "twoshot" else OP_ALLREDUCE, tensors, tensors)
 
     def fits(self, tensors: Sequence[torch.Tensor]) -> bool:
         return (len(tensors) <= 8 and all(_aligned(t) for t in tensors)
@@ -181,10 +194,13 @@ def self_test(comm: XgmiComm) -> bool:
         ch.all_gather([(x, out)])
         want = torch.cat([torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * k for k in range(W)])
         y = x.clone()
-        ch.all_reduce([y])
+        ch.all_reduce([y], protocol="oneshot")
+        y2 = x.clone()
+        ch.all_reduce([y2], protocol="twoshot")
         torch.cuda.synchronize(dev)
-        ok = (ch.error() == 0 and torch.equal(out, want)
-              and torch.equal(y, W * torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * sum(range(W))))
+        want_sum = W * torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * sum(range(W))
+        ok = (ch.error() == 0 and torch.equal(out, want) and torch.equal(y, want_sum)
+              and torch.equal(y2, want_sum))
         ch.close()
     except Exception:
         ok = False

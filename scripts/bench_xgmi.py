@@ -14,8 +14,11 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SIZES = [("lowrank remainder all-reduce", 1, 25 * 1024), ("lowrank gather (fc1+fc2 rows)", 0, 886000),
-         ("allreduce bucket 1 MB", 1, 1 << 20), ("allreduce full grad 9.1 MB", 1, 9104880)]
+# (name, op, bytes): op 0 all-gather, 1 one-shot all-reduce, 2 two-shot all-reduce
+SIZES = [("lowrank remainder AR one-shot", 1, 25 * 1024), ("lowrank remainder AR two-shot", 2, 25 * 1024),
+         ("lowrank gather (fc1+fc2 rows)", 0, 886000),
+         ("AR bucket 1 MB one-shot", 1, 1 << 20), ("AR bucket 1 MB two-shot", 2, 1 << 20),
+         ("AR full grad 9.1 MB one-shot", 1, 9104880), ("AR full grad 9.1 MB two-shot", 2, 9104880)]
 
 
 def worker(rank, world, port, q):
@@ -30,8 +33,11 @@ def worker(rank, world, port, q):
         n = nbytes // 16 * 4
         x = torch.randn(n, device=dev)
         out = torch.empty(world * n, device=dev)
-        ch = comm.channel(name, x.nbytes)
-        call = (lambda: ch.all_gather([(x, out)])) if op == 0 else (lambda: ch.all_reduce([x]))
+        ch = comm.channel(name.rsplit(" ", 1)[0], x.nbytes)
+        if op == 0:
+            call = lambda: ch.all_gather([(x, out)])
+        else:
+            call = lambda: ch.all_reduce([x], protocol="oneshot" if op == 1 else "twoshot")
         st = torch.cuda.Stream(dev)
         with torch.cuda.stream(st):
             for _ in range(3):
