@@ -66,6 +66,16 @@ _SIGS = {
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),
     "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),
+    # standalone BatchNorm / activation / max-pool units (norm_pool.hip)
+    "csa_bn_slab_rows": (I, []),
+    "csa_bn_stats": (I, [P, L, I, P, I, P]),
+    "csa_bn_finalize": (I, [P, I, I, F, F, P, P, P, P, F, I, P, P]),
+    "csa_bn_apply": (I, [P, P, L, I, P, I, F, P]),
+    "csa_bn_bwd_reduce": (I, [P, P, P, L, I, P, I, F, P, I, P]),
+    "csa_bn_bwd_finalize": (I, [P, I, I, F, F, P, P, P, P]),
+    "csa_bn_bwd_apply": (I, [P, P, P, P, L, I, P, P, I, F, P]),
+    "csa_maxpool_fwd": (I, [P, P, P, P, P]),
+    "csa_maxpool_bwd": (I, [P, P, P, P, P]),
     "csa_xgmi_alloc": (I, [L, C.POINTER(P), P]),
     "csa_xgmi_open": (I, [P, C.POINTER(P)]),
     "csa_xgmi_close": (I, [P]),

@@ -158,6 +158,7 @@ class TrainEngine:
         s.wait_stream(torch.cuda.current_stream(self.device))
         saved = (self.flat.clone(), self.slots.clone(), self.dstep.clone(),
                  self.stream.cursor.clone())
+        bufs = [(b, b.clone()) for b in self.model.buffers()]     # BN running statistics
         with torch.cuda.stream(s):
             for _ in range(2):      # warm up allocator / autotuning / RCCL comms off-graph
                 self.program.run()
@@ -166,6 +167,8 @@ class TrainEngine:
         # undo the warm-up's effect on the model state
         self.flat.copy_(saved[0]); self.slots.copy_(saved[1])
         self.dstep.copy_(saved[2]); self.stream.cursor.copy_(saved[3])
+        for b, v in bufs:
+            b.copy_(v)
         self.program.reset_after_warmup() if hasattr(self.program, "reset_after_warmup") else None
 
     def _capture(self) -> None:

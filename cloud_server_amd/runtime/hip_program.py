@@ -18,9 +18,12 @@ max-pool routing; ``csa_conv_dgrad``; ``csa_conv_wgrad`` as an implicit MFMA GEM
 then gradient all-reduce (data parallel) and ONE fused optimizer launch which also
 zeroes next step's atomic accumulators and updates BN running statistics.
 
-Patterns outside this family (e.g. a 2-D norm after a dense layer, a standalone pool
-after a norm, a norm directly before the head) raise ``Unsupported``; the engine then
-uses ``TorchProgram`` for that job.
+Layer orders the consumer transform cannot express — a 2-D norm after a dense layer, a
+norm over > 128 channels or directly before the head, a pool that does not directly
+follow a conv, act/norm sequences like ``act norm`` — become **standalone units**
+(``norm_pool.hip``): ``bn`` (materialised ``[norm] [act]``: stats -> finalize -> apply,
+with its own backward) and ``pool`` (max pool + gather-form backward).  So every DSL the
+reference accepts (construct_distribute.py:155-165, 208-265) lowers to HIP kernels.
 """
 from __future__ import annotations
 
@@ -85,6 +88,7 @@ class Unit:
     wg_stripes: int = 1                     # conv: weight-gradient accumulator stripes
     dw_acc: Optional[torch.Tensor] = None   # conv: [stripes][taps*Cout] (or the flat-grad view)
     db_acc: Optional[torch.Tensor] = None   # conv: [stripes][Cout] (or the flat-grad view)
+    norm: Optional[LayerPlan] = None        # bn unit: the norm layer (None: activation only)
 
 
 class HipProgram:
@@ -115,9 +119,6 @@ class HipProgram:
         self._zero_now()
         self._plan_grad_buckets()
         self.opt_segments = self._opt_segments()
-        nfold = sum(1 + (u.db_acc is not None) for u in self.units if u.kind == "conv" and u.wg_stripes > 1)
-        if nfold + (2 if self.head_rg else 0) > 8:
-            raise Unsupported("more than 8 striped gradients")
 
     # ------------------------------------------------------------------ DP overlap
     def _plan_grad_buckets(self) -> None:
@@ -335,52 +336,92 @@ class HipProgram:
     def _lower(self) -> None:
         layers = self.e.model.plan.layers
         units: List[Unit] = []
-        pending = Transform()
+        pending: List[LayerPlan] = []            # norm / act layers since the last unit
+
+        def as_transform(consumer: str) -> Optional[Transform]:
+            """``pending`` as a transform the consumer applies while loading, or None."""
+            tf = Transform()
+            for lp in pending:
+                if isinstance(lp.spec, NormSpec):
+                    if tf.norm is not None or tf.act is not None:
+                        return None              # norm after norm / act
+                    tf.norm = lp
+                else:
+                    if tf.act is not None:
+                        return None              # two activations in a row
+                    tf.act = lp.spec
+            if tf.norm is not None:
+                # the forward statistics come from a conv unit's epilogue, the tables live
+                # in LDS (<= 128 channels), and the head has no BN-apply prologue
+                if (consumer == "head" or not units or units[-1].kind != "conv"
+                        or not tf.norm.in_shape.is_spatial or tf.norm.in_shape.c > 128):
+                    return None
+            return tf
+
+        def materialise() -> None:
+            """``pending`` as standalone units: [norm][act] groups and lone activations."""
+            i = 0
+            while i < len(pending):
+                lp = pending[i]
+                if isinstance(lp.spec, NormSpec):
+                    nxt = pending[i + 1] if i + 1 < len(pending) else None
+                    act = nxt.spec if nxt is not None and isinstance(nxt.spec, ActSpec) else None
+                    units.append(Unit("bn", lp, act=act, norm=lp))
+                    i += 2 if act is not None else 1
+                else:
+                    units.append(Unit("bn", lp, act=lp.spec))
+                    i += 1
+            pending.clear()
+
         i = 0
         while i < len(layers):
             lp = layers[i]
             sp = lp.spec
-            if isinstance(sp, ConvSpec):
-                u = Unit("conv", lp, in_tf=pending)
-                pending = Transform()
+            if isinstance(sp, (ConvSpec, DenseSpec)):
+                kind = "conv" if isinstance(sp, ConvSpec) else "dense"
+                if kind == "conv" and (lp.in_shape.c > 128 or sp.cout > 128):
+                    raise Unsupported("conv with more than 128 channels")   # conv.hip tiling
+                tf = as_transform(kind)
+                if tf is None:
+                    materialise()
+                    tf = Transform()
+                pending.clear()
+                u = Unit(kind, lp, in_tf=tf)
                 j = i + 1
-                if j < len(layers) and isinstance(layers[j].spec, ActSpec):
-                    u.act = layers[j].spec
-                    j += 1
-                if j < len(layers) and isinstance(layers[j].spec, PoolSpec):
-                    u.pool = layers[j]
-                    j += 1
+                if kind == "conv":
+                    if j < len(layers) and isinstance(layers[j].spec, ActSpec):
+                        u.act = layers[j].spec
+                        j += 1
+                    if j < len(layers) and isinstance(layers[j].spec, PoolSpec):
+                        u.pool = layers[j]
+                        j += 1
                 units.append(u)
                 i = j
-            elif isinstance(sp, DenseSpec):
-                units.append(Unit("dense", lp, in_tf=pending))
-                pending = Transform()
-                i += 1
-            elif isinstance(sp, NormSpec):
-                if pending.norm is not None or pending.act is not None:
-                    raise Unsupported("norm after norm/act")
-                if not lp.in_shape.is_spatial or not units or units[-1].kind != "conv":
-                    raise Unsupported("norm must follow a conv unit")
-                if lp.in_shape.c > 128:
-                    raise Unsupported("norm over > 128 channels")
-                pending.norm = lp
-                i += 1
-            elif isinstance(sp, ActSpec):
-                if pending.act is not None:
-                    raise Unsupported("two activations in a row")
-                pending.act = sp
-                _act_id(sp)
-                i += 1
             elif isinstance(sp, PoolSpec):
-                raise Unsupported("pool not directly after a conv")
+                materialise()                    # pool(act(norm(x))): the transform first
+                units.append(Unit("pool", lp))
+                i += 1
+            elif isinstance(sp, (NormSpec, ActSpec)):
+                if isinstance(sp, ActSpec):
+                    _act_id(sp)
+                pending.append(lp)
+                i += 1
             else:  # pragma: no cover
                 raise Unsupported(str(sp))
-        if pending.norm is not None:
-            raise Unsupported("norm directly before the head")
+        tf = as_transform("head")
+        if tf is None:
+            materialise()
+            tf = Transform()
         if not units:
             raise Unsupported("no conv/dense layers")
         self.units = units
-        self.head_tf = pending
+        self.head_tf = tf
+
+    @staticmethod
+    def _bn_channels(u: Unit) -> int:
+        """Channel count of a bn unit: C of an NHWC tensor, the features of a 2-D one."""
+        sh = u.layer.in_shape
+        return sh.c if sh.is_spatial else sh.numel
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self) -> None:
@@ -389,12 +430,28 @@ class HipProgram:
         prev: Optional[Unit] = None
         for u in self.units:
             u.x = prev.y if prev is not None else None
-            if prev is None and u.kind == "dense":
-                # first layer dense: materialise the gathered float input once per step
+            if prev is None and u.kind != "conv":
+                # first unit reads no raw images: materialise the gathered float input once
+                # per step (NHWC [B, 28, 28, 1] for a bn / pool unit)
                 self.x_dense_in = torch.zeros(B, u.layer.in_shape.numel, **f32)
-                u.x = self.x_dense_in
+                ish = u.layer.in_shape
+                u.x = (self.x_dense_in if u.kind == "dense" or not ish.is_spatial
+                       else self.x_dense_in.view(B, ish.hw[0], ish.hw[1], ish.c))
             lp = u.layer
-            if u.kind == "conv":
+            if u.kind == "bn":
+                u.y = torch.zeros_like(u.x)
+                C_ = self._bn_channels(u)
+                if u.norm is not None:
+                    R = self.lib.csa_bn_slab_rows()
+                    u.bn_tab = torch.zeros(4, C_, **f32)
+                    u.bn_slab = torch.zeros(R, 2, C_, **f32)
+                    u.bn_bslab = torch.zeros(R, 2, C_, **f32)
+                    u.bn_k = torch.zeros(2, C_, **f32)
+            elif u.kind == "pool":
+                ph, pw = lp.out_shape.hw
+                u.y = torch.zeros(B, ph, pw, lp.out_shape.c, **f32)
+                u.argmax = torch.zeros(B, ph, pw, lp.out_shape.c, device=dev, dtype=torch.uint8)
+            elif u.kind == "conv":
                 oh, ow = lp.out_shape.hw
                 if u.pool is not None:
                     ph, pw = u.pool.out_shape.hw
@@ -453,6 +510,7 @@ class HipProgram:
         regs: List[torch.Tensor] = []
         flat: List[torch.Tensor] = []
         self.stripe_bufs: List[torch.Tensor] = []
+        fold_budget = 8 - (2 if self.head_rg else 0)
         for k, u in enumerate(self.units):
             lp = u.layer
             if u.kind == "dense":
@@ -469,10 +527,17 @@ class HipProgram:
                 if self.lib.csa_dense_wgrad_splits(B, fin, fout) > 1:
                     flat.append(self.gviews[f"{lp.name}.weight"].view(-1))
                     flat.append(self.gviews[f"{lp.name}.bias"])
-            else:
-                # conv weight gradients: S stripes on one GPU (folded by the optimizer),
-                # accumulated straight into the flat gradient under data parallelism
-                S = 1 if self.e.ctx.enabled else self.WGRAD_STRIPES
+            elif u.kind == "bn":
+                if u.norm is not None:        # atomic stat rows (forward and backward)
+                    regs += [u.bn_slab.view(-1), u.bn_bslab.view(-1)]
+            elif u.kind == "conv":
+                # conv weight gradients: S stripes on one GPU (folded by the optimizer:
+                # at most 8 folds, the head's partials included), otherwise accumulated
+                # straight into the flat gradient (data parallelism, or beyond that budget)
+                nf = 1 + (1 if lp.spec.bias else 0)
+                S = 1 if self.e.ctx.enabled or fold_budget < nf else self.WGRAD_STRIPES
+                if S > 1:
+                    fold_budget -= nf
                 u.wg_stripes = S
                 nw = self.gviews[f"{lp.name}.weight"].numel()
                 if S > 1:       # zeroed by the optimizer's fold (their only reader)
@@ -514,12 +579,13 @@ class HipProgram:
                     lo = offs[n]
                     self.keep_ranges.append((lo, lo + (self.gviews[n].numel() // 4) * 4))
         self.ps_mode = self.e.sync.strategy == "ps" and self.e.ctx.enabled
-        self.zero_regions = regs + (flat if self.ps_mode else [])
-        if len(self.zero_regions) > 16:
-            raise Unsupported("too many accumulator regions")
+        regions = regs + (flat if self.ps_mode else [])
+        # the optimizer's zero list holds 16; any further accumulators are cleared at the
+        # start of the step instead (one fill launch each, inside the same graph)
+        self.zero_regions, self.zero_early = regions[:16], regions[16:]
 
     def _zero_now(self) -> None:
-        for r in self.zero_regions + self.stripe_bufs:
+        for r in self.zero_regions + self.zero_early + self.stripe_bufs:
             r.zero_()
         self.e.flat_grad.zero_()
 
@@ -575,6 +641,8 @@ class HipProgram:
         rows, cur = e.stream.rows, e.stream.cursor
         img = e.data.images
         V, G = self.views, self.gviews
+        for r in self.zero_early:
+            r.zero_()
         self._forward(st)
 
         self._lowrank_gather_inputs()
@@ -608,6 +676,10 @@ class HipProgram:
                     self._grad_ready(1)
                 else:
                     self._grad_ready(0)
+                continue
+            if u.kind in ("bn", "pool"):
+                self._standalone_bwd(u, self.units[k - 1] if k > 0 else None, st)
+                self._grad_ready(k)
                 continue
             lp, tf = u.layer, u.in_tf
             bn = self._bn_args(tf)
@@ -749,6 +821,9 @@ class HipProgram:
         for k, u in enumerate(self.units):
             if self.pair is not None and k < 2:
                 continue
+            if u.kind in ("bn", "pool"):
+                self._standalone_fwd(u, st)
+                continue
             lp, tf = u.layer, u.in_tf
             bn = self._bn_args(tf)
             in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
@@ -779,6 +854,78 @@ class HipProgram:
                         B, fout, fin, *self._bn_args_c(tf), in_act, in_alpha, st), "dense_fwd")
 
 
+    # ------------------------------------------------------------------ standalone units
+    def _pool_geom_full(self, u: Unit):
+        lp = u.layer
+        sp = lp.spec
+        h, w = lp.in_shape.hw
+        oh, ow = lp.out_shape.hw
+        return K.ints([self.B, h, w, lp.in_shape.c, sp.kernel[0], sp.kernel[1], sp.stride[0], sp.stride[1],
+                       lp.pads[0], lp.pads[2], oh, ow])
+
+    def _standalone_fwd(self, u: Unit, st) -> None:
+        lib = self.lib
+        if u.kind == "pool":
+            self._rc(lib.csa_maxpool_fwd(K.ptr(u.x), K.ptr(u.y), K.ptr(u.argmax), self._pool_geom_full(u), st),
+                     "maxpool_fwd")
+            return
+        n = u.x.numel()
+        C_ = self._bn_channels(u)
+        act, alpha = _act_id(u.act), _alpha(u.act)
+        if u.norm is None:
+            self._rc(lib.csa_bn_apply(K.ptr(u.x), K.ptr(u.y), n, C_, None, act, alpha, st), "act_apply")
+            return
+        nm = u.norm.name
+        rm = getattr(self.model, f"bn{u.norm.index}_mean")
+        rv = getattr(self.model, f"bn{u.norm.index}_var")
+        eps = float(u.norm.spec.epsilon)
+        if self._eval_bn:
+            self._rc(lib.csa_bn_finalize(None, 0, C_, 1.0, eps, K.ptr(self.views[f"{nm}.scale"]),
+                                         K.ptr(self.views[f"{nm}.offset"]), K.ptr(rm), K.ptr(rv), 0.0, 1,
+                                         K.ptr(u.bn_tab), st), "bn_finalize(eval)")
+        else:
+            R = u.bn_slab.shape[0]
+            self._rc(lib.csa_bn_stats(K.ptr(u.x), n // C_, C_, K.ptr(u.bn_slab), R, st), "bn_stats")
+            if self.sync_bn:
+                self.e.sync.allreduce_tensors([u.bn_slab], tag=f"bns{u.norm.index}")
+            upd = self.model.training and not getattr(self, "_predicting", False)
+            self._rc(lib.csa_bn_finalize(K.ptr(u.bn_slab), R, C_, float(n // C_ * self.W), eps,
+                                         K.ptr(self.views[f"{nm}.scale"]), K.ptr(self.views[f"{nm}.offset"]),
+                                         K.ptr(rm) if upd else None, K.ptr(rv) if upd else None,
+                                         float(self.model.bn_momentum), 0, K.ptr(u.bn_tab), st), "bn_finalize")
+        self._rc(lib.csa_bn_apply(K.ptr(u.x), K.ptr(u.y), n, C_, K.ptr(u.bn_tab), act, alpha, st), "bn_apply")
+
+    def _standalone_bwd(self, u: Unit, prev: Optional[Unit], st) -> None:
+        lib = self.lib
+        dx = prev.dy if prev is not None else None
+        if u.kind == "pool":
+            if dx is not None:
+                self._rc(lib.csa_maxpool_bwd(K.ptr(u.dy), K.ptr(u.argmax), K.ptr(dx), self._pool_geom_full(u), st),
+                         "maxpool_bwd")
+            return
+        n = u.x.numel()
+        C_ = self._bn_channels(u)
+        act, alpha = _act_id(u.act), _alpha(u.act)
+        if u.norm is None:
+            if dx is not None:
+                self._rc(lib.csa_bn_bwd_apply(K.ptr(u.x), K.ptr(u.y), K.ptr(u.dy), K.ptr(dx), n, C_, None, None,
+                                              act, alpha, st), "act_bwd")
+            return
+        nm = u.norm.name
+        R = u.bn_bslab.shape[0]
+        self._rc(lib.csa_bn_bwd_reduce(K.ptr(u.x), K.ptr(u.y), K.ptr(u.dy), n // C_, C_, K.ptr(u.bn_tab), act, alpha,
+                                       K.ptr(u.bn_bslab), R, st), "bn_bwd_reduce")
+        if self.sync_bn:
+            self.e.sync.allreduce_tensors([u.bn_bslab], tag=f"bnbs{u.norm.index}")
+        # under SyncBN the slab is already the global sum, so the parameter gradients are
+        # scaled by 1/world before the gradient all-reduce adds them up again
+        self._rc(lib.csa_bn_bwd_finalize(K.ptr(u.bn_bslab), R, C_, float(n // C_ * self.W), 1.0 / self.W,
+                                         K.ptr(self.gviews[f"{nm}.scale"]), K.ptr(self.gviews[f"{nm}.offset"]),
+                                         K.ptr(u.bn_k), st), "bn_bwd_finalize")
+        if dx is not None:
+            self._rc(lib.csa_bn_bwd_apply(K.ptr(u.x), K.ptr(u.y), K.ptr(u.dy), K.ptr(dx), n, C_, K.ptr(u.bn_tab),
+                                          K.ptr(u.bn_k), act, alpha, st), "bn_bwd_apply")
+
     def predict_logits_into(self, logits: torch.Tensor) -> None:
         """Forward-only pass over this program's input rows -> ``logits`` [B, 10] (graph
         capturable; ``serve.hip_infer`` captures it per batch bucket).  BatchNorm uses the
@@ -786,6 +933,7 @@ class HipProgram:
         (``bn_mode == "batch"``), exactly as ``DigitNet.forward`` in eval mode."""
         st = K.stream()
         self._eval_bn = self.model.bn_mode != "batch"
+        self._predicting = True
         # split-K forward outputs (and, with batch statistics, the forward BN slabs) are
         # atomic accumulators that the training step's optimizer launch re-zeroes
         for u in self.units:
@@ -793,6 +941,8 @@ class HipProgram:
                 u.y.zero_()
             if not self._eval_bn and u.in_tf.has_bn:
                 u.in_tf.slab.zero_()
+            if not self._eval_bn and u.kind == "bn" and u.norm is not None:
+                u.bn_slab.zero_()
         try:
             if self._eval_bn:
                 for tf in [u.in_tf for u in self.units] + [self.head_tf]:
@@ -807,6 +957,7 @@ class HipProgram:
             self._forward(st)
         finally:
             self._eval_bn = False
+            self._predicting = False
         last = self.units[-1]
         hin = last.y.view(self.B, -1)
         Kh = hin.shape[1]

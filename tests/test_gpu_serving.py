@@ -133,3 +133,39 @@ def test_inference_endpoint_on_gpu_latency_and_batching(trained, tmp_path):
               f"{b1 - b0} forward batches, accuracy {acc:.3f}")
         assert all(r.status_code == 200 for r in rs) and acc > 0.85
         assert b1 - b0 < 256
+
+
+@pytest.mark.parametrize("layers", [
+    [{"layer": "conv", "filter": [3, 3, 6], "isBias": "True"}, {"layer": "pool"},
+     {"layer": "connect", "hidden": 64}, {"layer": "norm"}, {"layer": "active", "active_func": "relu"},
+     {"layer": "connect", "hidden": 32}, {"layer": "norm"}],
+    [{"layer": "conv", "filter": [3, 3, 8]}, {"layer": "norm"}, {"layer": "active", "active_func": "relu"},
+     {"layer": "pool"}, {"layer": "connect", "hidden": 24}],
+])
+def test_hip_predict_standalone_units_use_running_stats(layers):
+    """Eval-mode forward of standalone BN / pool units (running statistics) == the eager
+    model in eval mode."""
+    import copy
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    from cloud_server_amd.serve.hip_infer import _Bucket
+    c = copy.deepcopy(SAMPLE_CONFIG)
+    c["net_config"]["middle_layer"] = layers
+    c.update(optimizer_name="AdamOptimizer", learning_rate=1e-3)
+    c["options"] = dict(batch_size=50)
+    cfg = parse_train_config(c)
+    ds = synthetic_mnist(1000, seed=2)
+    eng = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for _ in range(30):
+        eng.step()
+    torch.cuda.synchronize()
+    state = eng.model.export_state()
+    b = _Bucket(cfg, state, 64, torch.device("cuda:0"), "mnist")
+    assert {u.kind for u in b.eng.program.units} & {"bn", "pool"}
+    x = ds.images[:64]
+    pred = b.run(x)
+    net = b.eng.model
+    with torch.no_grad():
+        ref = net(torch.from_numpy(x.astype(np.float32) / 255.0).cuda())
+    torch.testing.assert_close(b.logits, ref, rtol=1e-3, atol=1e-3 * ref.abs().max().item())
+    assert (pred == ref.argmax(1).cpu().numpy()).mean() >= 0.98

@@ -70,12 +70,66 @@ CASES = {
         {"layer": "active", "active_func": "relu"},
         {"layer": "connect", "hidden": 64},
     ],
+    # standalone units (norm_pool.hip): 2-D BatchNorm after a dense layer and before the
+    # head, pool after norm + act, act -> norm -> act, > 128 BN channels, pool first,
+    # five biased convs (more striped weight gradients than the optimizer folds)
+    "dense_norm_head": [
+        {"layer": "conv", "filter": [3, 3, 6], "isBias": "True"},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 64},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "connect", "hidden": 32},
+        {"layer": "norm"},
+    ],
+    "pool_after_norm_act": [
+        {"layer": "conv", "filter": [3, 3, 8]},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool"},
+        {"layer": "active", "active_func": "sigmoid"},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "leaky_relu", "param": [0.2]},
+        {"layer": "connect", "hidden": 24},
+    ],
+    "wide_norm_pool_first": [
+        {"layer": "pool"},
+        {"layer": "conv", "filter": [3, 3, 16], "isBias": "True"},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool", "kernel": [3, 3], "stride": [2, 2]},
+        {"layer": "connect", "hidden": 160},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "connect", "hidden": 16},
+    ],
+    "five_biased_convs": [
+        {"layer": "conv", "filter": [3, 3, 4], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [3, 3, 6], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool"},
+        {"layer": "conv", "filter": [3, 3, 8], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [3, 3, 8], "isBias": "True"},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [3, 3, 10], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 32},
+    ],
 }
+STANDALONE = {"dense_norm_head": ("bn",), "pool_after_norm_act": ("bn", "pool"),
+              "wide_norm_pool_first": ("bn", "pool")}
 
 
-def _run_one(cfg, backend, ds):
+def _run_one(cfg, backend, ds, name=None):
     eng = TrainEngine(cfg, ds, device="cuda", backend=backend, use_graph=False)
     assert eng.backend == backend, eng.fallback_reason
+    if backend == "hip" and name in STANDALONE:      # the pattern lowered to standalone units
+        kinds = {u.kind for u in eng.program.units}
+        assert set(STANDALONE[name]) <= kinds, kinds
     w0 = eng.flat.clone()
     eng.step()
     torch.cuda.synchronize()
@@ -87,16 +141,20 @@ def _run_one(cfg, backend, ds):
 def test_step_matches_torch(name, loss):
     ds = synthetic_mnist(400, seed=3)
     cfg = _cfg(CASES[name], loss=loss, lr=0.5)
-    eh, w0h, w1h = _run_one(cfg, "hip", ds)
+    eh, w0h, w1h = _run_one(cfg, "hip", ds, name)
     et, w0t, w1t = _run_one(cfg, "torch", ds)
     assert torch.equal(w0h, w0t)
     gh = (w0h - w1h) / cfg.effective_lr
     gt = (w0t - w1t) / cfg.effective_lr
+    # a gradient that is exactly 0 in exact arithmetic (e.g. a bias followed, through any
+    # per-batch-constant path, by a BatchNorm: the batch mean cancels it) is pure fp32
+    # summation noise in both programs: bound it against the model's largest gradient
+    gmax = gt.abs().max().item()
     for k in eh.model.state.shapes:
         a, b = eh.model.state.view(k, gh), et.model.state.view(k, gt)
         scale = b.abs().max().item() + 1e-6
         err = (a - b).abs().max().item()
-        assert err <= 2e-3 * scale + 1e-6, f"{name}/{loss} grad {k}: err {err:.3e} scale {scale:.3e}"
+        assert err <= 2e-3 * scale + 1e-6 + 1e-5 * gmax, f"{name}/{loss} grad {k}: err {err:.3e} scale {scale:.3e}"
     mh, mt = eh.metrics_since(0), et.metrics_since(0)
     assert abs(mh["loss"] - mt["loss"]) < 1e-4 * max(1, abs(mt["loss"]))
     assert mh["accuracy"] == mt["accuracy"]
