@@ -491,7 +491,8 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         mdir = settings.model_dir(u["id"], model)
         try:
             os.makedirs(mdir, exist_ok=True)
-            pipeline.copy_dataset(os.path.join(settings.storage_root, r["file_path"]), os.path.join(mdir, "data"))
+            await run_in_threadpool(pipeline.copy_dataset, os.path.join(settings.storage_root, r["file_path"]),
+                                    os.path.join(mdir, "data"))
             tag = os.path.join(mdir, "tag.json")
             if ops:
                 if not os.path.exists(tag):

@@ -424,3 +424,39 @@ def test_browser_auth_pages_and_admin(client):
     r = client.get("/admin/")
     assert r.status_code == 200 and "Site administration" in r.text and "users" in r.text
     assert uid
+
+
+def test_event_loop_free_during_slow_preprocess(client, monkeypatch):
+    """A slow /preprocess/ (dataset copy + pipeline run in the threadpool) does not stall
+    other requests: GET /data/list/ answers in < 100 ms while it runs."""
+    import asyncio
+    import time
+    import httpx
+    from cloud_server_amd.preprocess import pipeline
+    h = _auth(client)
+    zb, tags, _ = _digit_zip(8)
+    r = _mp(client, "/data/list/", {"file_type": "zip", "file_class": "picture"},
+            {"file": ("d.zip", zb, "application/zip")}, h)
+    pk = r.json()["data_id"]
+    real = pipeline.copy_dataset
+
+    def slow_copy(src, dst):
+        time.sleep(1.5)
+        return real(src, dst)
+    monkeypatch.setattr(pipeline, "copy_dataset", slow_copy)
+
+    async def go():
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=client.app), base_url="http://t") as ac:
+            body, ct = encode_multipart({"dataId": str(pk), "modelName": "m"}, {})
+            slow = asyncio.create_task(ac.post("/preprocess/", content=body, headers={**h, "Content-Type": ct}))
+            await asyncio.sleep(0.2)             # the copy is now sleeping in a worker thread
+            t0 = time.perf_counter()
+            lst = await ac.get("/data/list/", headers=h)
+            dt = time.perf_counter() - t0
+            done_early = slow.done()
+            res = await slow
+            return lst, dt, done_early, res
+    lst, dt, done_early, res = asyncio.run(go())
+    assert lst.status_code == 200 and len(lst.json()) == 1
+    assert not done_early and res.json()["message"] == "success", res.text
+    assert dt < 0.1, dt
