@@ -1,0 +1,513 @@
+// Register-direct f32 MFMA kernels for the skinny dense layers of the training step
+// (gfx950).  The reference's dense layers (construct_distribute.py:168-182, 252-264) are
+// [B=50] x [in] x [out] GEMMs: one dimension is the tiny batch, the weights are the only
+// big operand.  The LDS-staged split-K GEMM (gemm.hip) spends most of its 7-20 us per
+// launch in staging, barriers and the intra-WG K reduction; here operands go straight
+// from global memory (L2) into MFMA registers:
+//
+//   * dd_fwd    Y[M][N]  (+)= act(X)[M][K] . W[K][N] + b      ("NN")
+//   * dd_dgrad  dX[M][F]  = dY[M][N] . W[F][N]^T, epilogue through the forward input
+//               transform: dz = act'(g), per-channel {sum dz, sum dz*xhat} (BN backward)
+//   * dd_wgrad  dW[F][N] = act(X)^T[F][M] . dY[M][N] (K = batch), epilogue either the
+//               plain gradient store or the OPTIMIZER UPDATE itself (optim_common.h):
+//               W, its slots and the bias are updated in place and the gradient never
+//               exists in memory.
+//
+// MFMA v_mfma_f32_32x32x2_f32 (cdna_hip_programming.md §3):
+//   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31];
+//   D: reg r of lane l is D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
+// K-contiguous operands ("row of A" / "row of W^T") are loaded as ONE float4 per lane
+// covering k0+4h..k0+4h+3 (h = l>>5) and fed over 4 MFMA steps, step s taking component
+// s: step s multiplies k = k0+4h+s from both operands, so the sum over k is complete
+// (the k order inside the 8-block is permuted, the products are the same).
+// Each wave owns a 64-row (two 32-row sub-tiles) x 32-column output tile: the 32x8 B
+// fragment is loaded once for both sub-tiles.  The 4 waves of a workgroup split the
+// workgroup's K range; their partials meet in LDS in fixed wave order.
+#include "common.h"
+#include "optim_common.h"
+
+namespace csa {
+
+typedef float dd_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int DD_THREADS = 256;
+constexpr int DD_WAVES = 4;
+constexpr int DD_SLAB_ROWS = 16;      // BN-backward slab rows (same contract as gemm.hip)
+constexpr int DD_MAXC = 128;
+constexpr int DD_U = 4;               // 8-k blocks whose loads are in flight together
+
+// diagnostics: block-0 phase stamps [0..3] + the earliest block start [4] and the latest
+// block end [5] of a launch (s_memtime ticks); null disables
+__device__ long long* g_dd_dbg = nullptr;
+#define DD_STAMP(i)                                                                           \
+  do {                                                                                        \
+    if (g_dd_dbg && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) \
+      g_dd_dbg[i] = (long long)__builtin_amdgcn_s_memtime();                                  \
+  } while (0)
+#define DD_SPAN_BEGIN()                                                                       \
+  do {                                                                                        \
+    if (g_dd_dbg && threadIdx.x == 0)                                                         \
+      atomicMin((unsigned long long*)&g_dd_dbg[4], (unsigned long long)__builtin_amdgcn_s_memtime()); \
+  } while (0)
+#define DD_SPAN_END()                                                                         \
+  do {                                                                                        \
+    if (g_dd_dbg && threadIdx.x == 0)                                                         \
+      atomicMax((unsigned long long*)&g_dd_dbg[5], (unsigned long long)__builtin_amdgcn_s_memtime()); \
+  } while (0)
+
+__device__ __forceinline__ int dd_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ void dd_pin4(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void dd_pin(float& v) { asm volatile("" : "+v"(v)); }
+
+__device__ __forceinline__ float dd_c(const float4& v, int s) {
+  return s == 0 ? v.x : (s == 1 ? v.y : (s == 2 ? v.z : v.w));
+}
+
+// Sum the DD_WAVES partial tiles (2 x 16 values per lane) in fixed wave order; every
+// thread then owns 8 of the tile's 2048 values: returns them with their (row, col).
+struct DDTile { float v[8]; int row[8]; int col[8]; };
+
+__device__ __forceinline__ DDTile dd_reduce(float* s_red, const dd_f32x16& a0, const dd_f32x16& a1) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // layout [wave][v = 0..31][lane]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s_red[(w * 32 + r) * 64 + lane] = a0[r];
+    s_red[(w * 32 + 16 + r) * 64 + lane] = a1[r];
+  }
+  __syncthreads();
+  DDTile out;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int idx = t + q * DD_THREADS;          // 0..2047
+    const int v = idx >> 6, ln = idx & 63;
+    float s = s_red[(0 * 32 + v) * 64 + ln];
+#pragma unroll
+    for (int ww = 1; ww < DD_WAVES; ++ww) s += s_red[(ww * 32 + v) * 64 + ln];
+    out.v[q] = s;
+    out.row[q] = (v >> 4) * 32 + dd_row(v & 15, ln);
+    out.col[q] = ln & 31;
+  }
+  return out;
+}
+
+// K range of wave w inside the workgroup's slice [k0, k1): contiguous, multiple of 8.
+__device__ __forceinline__ void dd_wave_range(int k0, int k1, int& a, int& b) {
+  const int w = threadIdx.x >> 6;
+  const int n8 = (k1 - k0 + 7) >> 3;
+  const int per = (n8 + DD_WAVES - 1) / DD_WAVES;
+  a = min(k1, k0 + w * per * 8);
+  b = min(k1, a + per * 8);
+}
+
+// ------------------------------------------------------------------ forward
+struct DDFwd {
+  const float* x; const float* w; const float* bias; float* y;
+  int M, N, K, act; float alpha; int ksplit, kper;   // kper: K per workgroup (multiple of 8)
+};
+
+template <bool V4>
+__global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
+  __shared__ float s_red[DD_WAVES * 32 * 64];
+  DD_STAMP(0);
+  DD_SPAN_BEGIN();
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+  const int nt = blockIdx.x, mb = blockIdx.y, ks = blockIdx.z;
+  const int n0 = nt * 32, m0 = mb * 64;
+  const int kg0 = ks * a.kper, kg1 = min(a.K, kg0 + a.kper);
+  int ka, kb;
+  dd_wave_range(kg0, kg1, ka, kb);
+  const int mA = min(m0 + i, a.M - 1), mB = min(m0 + 32 + i, a.M - 1);
+  const float vA = m0 + i < a.M ? 1.f : 0.f, vB = m0 + 32 + i < a.M ? 1.f : 0.f;
+  const int n = min(n0 + i, a.N - 1);
+  const float* xa = a.x + (long)mA * a.K;
+  const float* xb = a.x + (long)mB * a.K;
+  dd_f32x16 acc0 = {}, acc1 = {};
+  // DD_U blocks of 8 k per iteration: every load of the group is in flight before the
+  // first MFMA (a wave's whole K range is 1-2 memory round trips, not one per block)
+  for (int k = ka; k < kb; k += 8 * DD_U) {
+    float4 pa[DD_U], pb[DD_U];
+    float bw[DD_U][4];
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+      const int kk = k + 8 * u + 4 * h;
+      if (V4) {                    // branch-free: clamped float4 (terms past kb get B = 0)
+        const int kc = min(kk, a.K - 4);
+        pa[u] = *reinterpret_cast<const float4*>(xa + kc);
+        pb[u] = *reinterpret_cast<const float4*>(xb + kc);
+      } else {
+        float t0[4], t1[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kc = min(kk + s, a.K - 1);
+          t0[s] = xa[kc];
+          t1[s] = xb[kc];
+        }
+        pa[u] = make_float4(t0[0], t0[1], t0[2], t0[3]);
+        pb[u] = make_float4(t1[0], t1[1], t1[2], t1[3]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bw[u][s] = a.w[(long)min(kk + s, a.K - 1) * a.N + n];
+    }
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+      dd_pin4(pa[u]);
+      dd_pin4(pb[u]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dd_pin(bw[u][s]);
+    }
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int kk = k + 8 * u + 4 * h + s;
+        float xa_s = dd_c(pa[u], s), xb_s = dd_c(pb[u], s);
+        if (a.act != ACT_NONE) { xa_s = act_fwd(xa_s, a.act, a.alpha); xb_s = act_fwd(xb_s, a.act, a.alpha); }
+        const float b = kk < kb ? bw[u][s] : 0.f;     // outside this wave's range: no term
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa_s * vA, b, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xb_s * vB, b, acc1, 0, 0, 0);
+      }
+    }
+  }
+  DD_STAMP(1);
+  const DDTile t = dd_reduce(s_red, acc0, acc1);
+  DD_STAMP(2);
+  // the bias is read BEFORE the first atomic: vmcnt is in order, so a load issued after
+  // an atomic waits for it (one serial round trip per element otherwise)
+  const int nb_ = n0 + (threadIdx.x & 31);        // every value of a thread shares its column
+  float bias = (a.bias && ks == 0) ? a.bias[min(nb_, a.N - 1)] : 0.f;
+  dd_pin(bias);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int m = m0 + t.row[q], nn = n0 + t.col[q];
+    if (m >= a.M || nn >= a.N) continue;
+    const float v = t.v[q] + bias;
+    float* p = a.y + (long)m * a.N + nn;
+    if (a.ksplit > 1) atomicAdd(p, v); else *p = v;
+  }
+  DD_STAMP(3);
+  DD_SPAN_END();
+}
+
+// ------------------------------------------------------------------ dgrad
+struct DDDgrad {
+  const float* dy; const float* w; float* dx;
+  int M, F, N; int ksplit, kper;
+  const float* x; int act; float alpha;            // forward input (pre transform) + act
+  BNRef bn; float* bwd_slab;                       // bn.slab == null: no BatchNorm
+};
+
+template <bool V4>
+__global__ __launch_bounds__(DD_THREADS) void dd_dgrad_kernel(DDDgrad a) {
+  __shared__ float s_red[DD_WAVES * 32 * 64];
+  __shared__ float s_bn[4 * DD_MAXC + 2 * DD_MAXC];
+  __shared__ float s_acc[2 * DD_MAXC];
+  DD_STAMP(0);
+  DD_SPAN_BEGIN();
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+  const int ft = blockIdx.x, mb = blockIdx.y, ks = blockIdx.z;
+  const int f0 = ft * 32, m0 = mb * 64;
+  const bool has_bn = a.bn.slab != nullptr;
+  if (has_bn) {
+    bn_reduce_to_lds(a.bn, s_bn, s_bn + DD_MAXC, s_bn + 2 * DD_MAXC, s_bn + 3 * DD_MAXC, s_bn + 4 * DD_MAXC);
+    for (int c = threadIdx.x; c < 2 * DD_MAXC; c += DD_THREADS) s_acc[c] = 0.f;
+  }
+  const int kg0 = ks * a.kper, kg1 = min(a.N, kg0 + a.kper);
+  int ka, kb;
+  dd_wave_range(kg0, kg1, ka, kb);
+  const int mA = min(m0 + i, a.M - 1), mB = min(m0 + 32 + i, a.M - 1);
+  const float vA = m0 + i < a.M ? 1.f : 0.f, vB = m0 + 32 + i < a.M ? 1.f : 0.f;
+  const int f = min(f0 + i, a.F - 1);
+  const float* ya = a.dy + (long)mA * a.N;
+  const float* yb = a.dy + (long)mB * a.N;
+  const float* wr = a.w + (long)f * a.N;
+  dd_f32x16 acc0 = {}, acc1 = {};
+  for (int k = ka; k < kb; k += 8 * DD_U) {
+    float4 pa[DD_U], pb[DD_U], pw[DD_U];
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+      const int kk = k + 8 * u + 4 * h;
+      if (V4) {                    // branch-free: clamped float4 (terms past kb get W = 0)
+        const int kc = min(kk, a.N - 4);
+        pa[u] = *reinterpret_cast<const float4*>(ya + kc);
+        pb[u] = *reinterpret_cast<const float4*>(yb + kc);
+        pw[u] = *reinterpret_cast<const float4*>(wr + kc);
+      } else {
+        float t0[4], t1[4], t2[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kc = min(kk + s, a.N - 1);
+          t0[s] = ya[kc];
+          t1[s] = yb[kc];
+          t2[s] = wr[kc];
+        }
+        pa[u] = make_float4(t0[0], t0[1], t0[2], t0[3]);
+        pb[u] = make_float4(t1[0], t1[1], t1[2], t1[3]);
+        pw[u] = make_float4(t2[0], t2[1], t2[2], t2[3]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+      dd_pin4(pa[u]);
+      dd_pin4(pb[u]);
+      dd_pin4(pw[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float w = k + 8 * u + 4 * h + s < kb ? dd_c(pw[u], s) : 0.f;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(dd_c(pa[u], s) * vA, w, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(dd_c(pb[u], s) * vB, w, acc1, 0, 0, 0);
+      }
+    }
+  }
+  DD_STAMP(1);
+  const DDTile t = dd_reduce(s_red, acc0, acc1);
+  DD_STAMP(2);
+  // epilogue: forward inputs first (all loads in flight), then the transform backward
+  const int C = has_bn ? a.bn.C : 1;
+  float xv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int m = min(m0 + t.row[q], a.M - 1), ff = min(f0 + t.col[q], a.F - 1);
+    xv[q] = (a.x && (a.act != ACT_NONE || has_bn)) ? a.x[(long)m * a.F + ff] : 0.f;
+  }
+  float sd = 0.f, sdx = 0.f;
+  const int ff = f0 + (threadIdx.x & 31);         // every value of a thread shares its column
+  const int ch = has_bn ? ff % C : 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int m = m0 + t.row[q];
+    if (m >= a.M || ff >= a.F) continue;
+    float d = t.v[q];
+    if (a.act != ACT_NONE || has_bn) {
+      const float z = has_bn ? xv[q] * s_bn[2 * DD_MAXC + ch] + s_bn[3 * DD_MAXC + ch] : xv[q];
+      d = act_bwd(d, z, act_fwd(z, a.act, a.alpha), a.act, a.alpha);   // linear in the partial
+      if (has_bn) {
+        sd += d;
+        sdx += d * (xv[q] - s_bn[ch]) * s_bn[DD_MAXC + ch];
+      }
+    }
+    float* p = a.dx + (long)m * a.F + ff;
+    if (a.ksplit > 1) atomicAdd(p, d); else *p = d;
+  }
+  if (has_bn) {
+    if (ff < a.F) {
+      atomicAdd(&s_acc[ch], sd);
+      atomicAdd(&s_acc[DD_MAXC + ch], sdx);
+    }
+    __syncthreads();
+    float* row = a.bwd_slab + (size_t)(((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) % DD_SLAB_ROWS) * 2 * C;
+    for (int c = threadIdx.x; c < 2 * C; c += DD_THREADS)
+      atomicAdd(&row[c], s_acc[c < C ? c : DD_MAXC + c - C]);
+  }
+  DD_STAMP(3);
+  DD_SPAN_END();
+}
+
+// ------------------------------------------------------------------ wgrad (+ update)
+// One wave: 32 features x 32 outputs, K = batch in steps of 2 (2x the waves of a 32x64
+// tile: at one wave per SIMD every memory round trip is exposed, so parallelism wins
+// over A-fragment reuse, which L2 serves anyway).  Workgroup = 4 waves along the output
+// dimension (128 columns).
+struct DDWgrad {
+  const float* x; const float* dy; int M, F, N; int act; float alpha; float gscale;
+  float* dw; float* db;                         // store mode (opt < 0)
+  float* w; float* b; float* sw0; float* sw1; float* sb0; float* sb1;   // update mode
+  int opt; float lr; const int64_t* step;
+  int ftiles, ntiles;                           // ntiles: 128-column groups
+};
+
+constexpr int DD_KC = 32;   // MFMA k-steps (x2 batch rows) per register chunk
+
+__global__ __launch_bounds__(DD_THREADS) void dd_wgrad_kernel(DDWgrad a) {
+  DD_STAMP(0);
+  DD_SPAN_BEGIN();
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const int nw = a.ftiles * a.ntiles;
+  if ((int)blockIdx.x >= nw) {
+    // bias blocks: 64 columns x 4 batch quarters per block, all loads of a thread in
+    // flight at once, quarters summed in LDS in fixed order
+    __shared__ float s_b[DD_WAVES][64];
+    const int n = ((int)blockIdx.x - nw) * 64 + lane;
+    const int nc = min(n, a.N - 1);
+    const int per = (a.M + DD_WAVES - 1) / DD_WAVES;
+    const int m0 = w * per;
+    float v[16];
+    float g = 0.f;
+    for (int c = 0; c < per; c += 16) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = a.dy[(long)min(m0 + c + u, a.M - 1) * a.N + nc];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) dd_pin(v[u]);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) g += (c + u < per && m0 + c + u < a.M) ? v[u] : 0.f;
+    }
+    s_b[w][lane] = g;
+    __syncthreads();
+    if (w != 0 || n >= a.N) return;
+    g = (s_b[0][lane] + s_b[1][lane] + s_b[2][lane] + s_b[3][lane]) * a.gscale;
+    if (a.opt < 0) {
+      a.db[n] = g;
+    } else {
+      const float lr = opt_step_lr(a.opt, a.lr, a.step);
+      float wv = a.b[n], s0 = a.sb0 ? a.sb0[n] : 0.f, s1 = a.sb1 ? a.sb1[n] : 0.f;
+      opt_update(a.opt, lr, wv, g, s0, s1);
+      a.b[n] = wv;
+      if (a.sb0) a.sb0[n] = s0;
+      if (a.sb1) a.sb1[n] = s1;
+    }
+    return;
+  }
+  const int ft = (int)blockIdx.x / a.ntiles, ng = (int)blockIdx.x % a.ntiles;
+  const int f0 = ft * 32, n0 = ng * 128 + w * 32;
+  if (n0 >= a.N) return;
+  const int f = min(f0 + i, a.F - 1);
+  const int nn = n0 + i, nc = min(nn, a.N - 1);
+  // update mode: this lane's 16 weights and slots are requested BEFORE the K loop, so
+  // their HBM latency overlaps the gradient GEMM
+  const bool upd = a.opt >= 0;
+  const int ns = upd ? opt_nslots(a.opt) : 0;
+  float wv[16], s0[16], s1[16];
+  if (upd) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long idx = (long)min(f0 + dd_row(r, lane), a.F - 1) * a.N + nc;
+      wv[r] = a.w[idx];
+      s0[r] = ns > 0 ? a.sw0[idx] : 0.f;
+      s1[r] = ns > 1 ? a.sw1[idx] : 0.f;
+    }
+  }
+  dd_f32x16 acc = {};
+  for (int c0 = 0; c0 < a.M; c0 += 2 * DD_KC) {
+    float xa[DD_KC], ya[DD_KC];
+#pragma unroll
+    for (int s = 0; s < DD_KC; ++s) {
+      const int m = min(c0 + 2 * s + h, a.M - 1);
+      xa[s] = a.x[(long)m * a.F + f];
+      ya[s] = a.dy[(long)m * a.N + nc];
+    }
+#pragma unroll
+    for (int s = 0; s < DD_KC; ++s) {
+      dd_pin(xa[s]);
+      dd_pin(ya[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < DD_KC; ++s) {
+      if (c0 + 2 * s >= a.M) break;              // wave-uniform
+      const float ok = c0 + 2 * s + h < a.M ? 1.f : 0.f;
+      float xv = a.act != ACT_NONE ? act_fwd(xa[s], a.act, a.alpha) : xa[s];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv * ok, ya[s], acc, 0, 0, 0);
+    }
+  }
+  DD_STAMP(1);
+  // epilogue: D[row f][col n]; lanes 0-31 consecutive columns (coalesced rows of W)
+  if (!upd) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ff = f0 + dd_row(r, lane);
+      if (ff < a.F && nn < a.N) a.dw[(long)ff * a.N + nn] = acc[r] * a.gscale;
+    }
+    return;
+  }
+  const float lr = opt_step_lr(a.opt, a.lr, a.step);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dd_pin(wv[r]);
+    dd_pin(s0[r]);
+    dd_pin(s1[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ff = f0 + dd_row(r, lane);
+    if (ff >= a.F || nn >= a.N) continue;
+    const long idx = (long)ff * a.N + nn;
+    opt_update(a.opt, lr, wv[r], acc[r] * a.gscale, s0[r], s1[r]);
+    a.w[idx] = wv[r];
+    if (ns > 0) a.sw0[idx] = s0[r];
+    if (ns > 1) a.sw1[idx] = s1[r];
+  }
+  DD_STAMP(3);
+  DD_SPAN_END();
+}
+
+// K slices: enough workgroups for ~1 wave per SIMD (1024), each wave >= 16 k.
+static int dd_splits(int tiles, int K) {
+  int ks = (1024 / DD_WAVES + tiles - 1) / tiles;
+  const int maxks = (K + 8 * DD_WAVES * 2 - 1) / (8 * DD_WAVES * 2);   // >= 16 k per wave
+  ks = ks < 1 ? 1 : ks;
+  ks = ks > maxks ? maxks : ks;
+  return ks < 1 ? 1 : ks;
+}
+
+static int dd_kper(int K, int ks) { return (((K + ks - 1) / ks) + 7) & ~7; }
+
+}  // namespace csa
+
+using namespace csa;
+
+CSA_API int csa_dd_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dd_dbg), &p, sizeof(p));
+}
+
+CSA_API int csa_dd_fwd_splits(int M, int N, int K) {
+  return dd_splits(((N + 31) / 32) * ((M + 63) / 64), K);
+}
+
+// Y[M][N] (+)= act(X)[M][K] . W[K][N] + bias.  Y must be zeroed when splits > 1.
+CSA_API int csa_dd_fwd(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
+                       int act, float alpha, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return -1;
+  const int nt = (N + 31) / 32, mb = (M + 63) / 64;
+  int ks = dd_splits(nt * mb, K);
+  const int kper = dd_kper(K, ks);
+  ks = (K + kper - 1) / kper;
+  DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper};
+  if (K % 4 == 0) hipLaunchKernelGGL(dd_fwd_kernel<true>, dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
+  else hipLaunchKernelGGL(dd_fwd_kernel<false>, dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_dd_dgrad_splits(int M, int F, int N) {
+  return dd_splits(((F + 31) / 32) * ((M + 63) / 64), N);
+}
+
+CSA_API int csa_dd_dgrad_slabs() { return DD_SLAB_ROWS; }
+
+// dX[M][F] = dY[M][N] . W[F][N]^T through the forward input transform's backward (act,
+// BatchNorm: bwd_slab [16][2][C] gets {sum dz, sum dz*xhat}).  dX zeroed when splits > 1.
+CSA_API int csa_dd_dgrad(const float* dY, const float* W, float* dX, int M, int F, int N,
+                         const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C,
+                         float bn_count, float bn_eps, const float* bn_scale, const float* bn_offset,
+                         float* bwd_slab, hipStream_t st) {
+  if (M <= 0 || F <= 0 || N <= 0) return -1;
+  if (bn_slab && (bn_C > DD_MAXC || bn_C <= 0 || !bwd_slab)) return -1;
+  const int ft = (F + 31) / 32, mb = (M + 63) / 64;
+  int ks = dd_splits(ft * mb, N);
+  const int kper = dd_kper(N, ks);
+  ks = (N + kper - 1) / kper;
+  DDDgrad a{dY, W, dX, M, F, N, ks, kper, x_fwd, act, alpha,
+            BNRef{bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset}, bwd_slab};
+  if (N % 4 == 0) hipLaunchKernelGGL(dd_dgrad_kernel<true>, dim3(ft, mb, ks), dim3(DD_THREADS), 0, st, a);
+  else hipLaunchKernelGGL(dd_dgrad_kernel<false>, dim3(ft, mb, ks), dim3(DD_THREADS), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// dW[F][N] = act(X)^T . dY * gscale, db = colsum(dY) * gscale (opt < 0), or the optimizer
+// update of W / b and their slots with that gradient (opt >= 0; step = the device step
+// counter after this step's increment).
+CSA_API int csa_dd_wgrad(const float* X, const float* dY, int M, int F, int N, int act, float alpha, float gscale,
+                         float* dW, float* db, float* W, float* b, float* sW0, float* sW1, float* sb0, float* sb1,
+                         int opt, float lr, const int64_t* step, hipStream_t st) {
+  if (M <= 0 || F <= 0 || N <= 0) return -1;
+  if (opt < 0 && (!dW || !db)) return -2;
+  if (opt >= 0 && (!W || !b || (opt_nslots(opt) > 0 && (!sW0 || !sb0)) || (opt_nslots(opt) > 1 && (!sW1 || !sb1))))
+    return -3;
+  DDWgrad a{X, dY, M, F, N, act, alpha, gscale, dW, db, W, b, sW0, sW1, sb0, sb1, opt, lr, step,
+            (F + 31) / 32, (N + 127) / 128};
+  const int nb = a.ftiles * a.ntiles + (N + 63) / 64;
+  hipLaunchKernelGGL(dd_wgrad_kernel, dim3(nb), dim3(DD_THREADS), 0, st, a);
+  return (int)hipGetLastError();
+}

@@ -41,7 +41,7 @@ __device__ __forceinline__ void opt_update(int opt, float lr, float& w, float g,
   }
 }
 
-__device__ __forceinline__ int opt_nslots(int opt) {
+__host__ __device__ __forceinline__ int opt_nslots(int opt) {
   return opt == OPT_SGD ? 0 : (opt == OPT_ADAGRAD ? 1 : 2);
 }
 

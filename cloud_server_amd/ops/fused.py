@@ -66,6 +66,14 @@ _SIGS = {
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),
     "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),
+    # register-direct MFMA dense kernels (dense_direct.hip)
+    "csa_dd_debug": (I, [P]),
+    "csa_dd_fwd_splits": (I, [I, I, I]),
+    "csa_dd_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
+    "csa_dd_dgrad_splits": (I, [I, I, I]),
+    "csa_dd_dgrad_slabs": (I, []),
+    "csa_dd_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P]),
+    "csa_dd_wgrad": (I, [P, P, I, I, I, I, F, F, P, P, P, P, P, P, P, P, I, F, P, P]),
     # standalone BatchNorm / activation / max-pool units (norm_pool.hip)
     "csa_bn_slab_rows": (I, []),
     "csa_bn_stats": (I, [P, L, I, P, I, P]),

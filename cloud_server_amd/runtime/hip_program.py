@@ -295,6 +295,25 @@ class HipProgram:
             if last.kind == "conv" and last.pool is not None:
                 K = last.pool.out_shape.numel
             self.head_rg = int(self.lib.csa_head_part_rows(B, K))
+        # register-direct MFMA dense kernels (dense_direct.hip): forward, input gradient and
+        # weight gradient; on one GPU the weight-gradient launch applies the optimizer update
+        # itself (the head advanced the step counter), so dW never exists in memory
+        # (lowrank data parallelism forms its dense weight gradients from gathered operands
+        # on a side stream: those layers keep the LDS-staged kernels)
+        # CSA_DENSE_DIRECT: "fwd" (default) = forward GEMMs only, "1" = forward + backward
+        # (+ in-kernel update), "0" = off — measured per launch in profiles/r2_dense_direct.md
+        mode = os.environ.get("CSA_DENSE_DIRECT", "fwd")
+        direct = mode in ("1", "fwd") and not (e.ctx.enabled and e.sync.strategy == "lowrank")
+        for u in self.units:
+            u.direct = u.direct_bwd = u.direct_update = False
+            if u.kind != "dense" or u.fused or not direct:
+                continue
+            fin = u.layer.in_shape.numel
+            if u.in_tf.has_bn and fin % 4:
+                continue                         # BN'd input not materialised: LDS-staged GEMM
+            u.direct = True
+            u.direct_bwd = mode == "1"
+            u.direct_update = bool(u.direct_bwd and self.fused and self.head_rg)
 
     # ------------------------------------------------------------------ conv pair
     def _plan_pair(self) -> None:
@@ -479,6 +498,8 @@ class HipProgram:
                 C = src.y.shape[3]
                 if u.kind == "dense" and u.fused:
                     nb = self.lib.csa_dense_bwd_update_slabs(u.layer.in_shape.numel)
+                elif u.kind == "dense" and u.direct_bwd:
+                    nb = self.lib.csa_dd_dgrad_slabs()
                 elif u.kind == "dense":
                     nb = self.lib.csa_dense_dgrad_slabs(B, u.layer.in_shape.numel, u.layer.spec.hidden)
                 else:
@@ -515,11 +536,16 @@ class HipProgram:
             lp = u.layer
             if u.kind == "dense":
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
-                u.splits_fwd = self.lib.csa_dense_fwd_splits(B, fout, fin)
+                u.splits_fwd = (self.lib.csa_dd_fwd_splits(B, fout, fin) if u.direct
+                                else self.lib.csa_dense_fwd_splits(B, fout, fin))
                 if u.splits_fwd > 1:
                     regs.append(u.y)
                 if u.fused:
                     continue                     # plain stores; W never has a gradient buffer
+                if u.direct_bwd:
+                    if k > 0 and self.lib.csa_dd_dgrad_splits(B, fin, fout) > 1:
+                        regs.append(self.units[k - 1].dy)
+                    continue                     # wgrad: whole stores or the update itself
                 if k > 0:
                     tfm = u.in_tf.has_bn or u.in_tf.act is not None
                     if self.lib.csa_dense_dgrad_splits(B, fin, fout, int(tfm)) > 1:
@@ -569,11 +595,11 @@ class HipProgram:
         self.keep_ranges = []
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind != "dense" or u.fused:
+            if u.kind != "dense" or u.fused or u.direct_update:
                 continue
             fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
             m = B * (self.e.ctx.world if u in getattr(self, "lr_units", []) else 1)
-            if self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
+            if (u.direct_bwd and u not in getattr(self, "lr_units", [])) or self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
                 for p in ("weight", "bias"):
                     n = f"{u.layer.name}.{p}"
                     lo = offs[n]
@@ -693,6 +719,10 @@ class HipProgram:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
                 if u.fused:
                     self._dense_bwd_update(u, prev, st)
+                    continue
+                if u.direct_bwd and u not in self.lr_units:
+                    self._dense_bwd_direct(u, prev, st)
+                    self._grad_ready(k)
                     continue
                 if (prev is not None and u not in self.lr_units and not self.wsplit
                         and self._dense_bwd_fused(u, prev, st)):
@@ -845,6 +875,13 @@ class HipProgram:
                     self._rc(lib.csa_bn_act_apply(
                         K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha, st),
                         "bn_act_apply")
+                if u.direct:
+                    xin = u.xt if u.xt is not None else u.x.view(B, -1)
+                    act = (0, 0.0) if u.xt is not None else (in_act, in_alpha)
+                    self._rc(lib.csa_dd_fwd(
+                        K.ptr(xin), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
+                        B, fout, fin, act[0], act[1], st), "dd_fwd")
+                elif u.xt is not None:
                     self._rc(lib.csa_dense_fwd(
                         K.ptr(u.xt), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]), K.ptr(u.y),
                         B, fout, fin, None, 0, 0, 0.0, 0.0, None, None, 0, 0.0, st), "dense_fwd")
@@ -1061,6 +1098,39 @@ class HipProgram:
             raise RuntimeError(f"dense_bwd failed: {rc}")
         return rc > 0
 
+    def _dense_bwd_direct(self, u: Unit, prev: Optional[Unit], st) -> None:
+        """Dense backward on the register-direct kernels: input gradient (through the
+        forward transform's backward) first — it reads the OLD weights — then the weight
+        gradient, or on one GPU the optimizer update of W / b in the same launch."""
+        e, lib, B = self.e, self.lib, self.B
+        lp, tf = u.layer, u.in_tf
+        fin, fout = lp.in_shape.numel, lp.spec.hidden
+        V, G = self.views, self.gviews
+        if prev is not None:
+            self._rc(lib.csa_dd_dgrad(
+                K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
+                K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
+                K.ptr(tf.bwd_slab) if tf.has_bn else None, st), "dd_dgrad")
+        xin = u.xt if u.xt is not None else u.x.view(B, -1)
+        act = (0, 0.0) if u.xt is not None else (_act_id(tf.act), _alpha(tf.act))
+        if u.direct_update:
+            offs = self.model.state.offsets
+            ow, ob = offs[f"{lp.name}.weight"], offs[f"{lp.name}.bias"]
+            sl = e.slots
+            s0 = sl[0] if sl.shape[0] > 0 else None
+            s1 = sl[1] if sl.shape[0] > 1 else None
+            self._rc(lib.csa_dd_wgrad(
+                K.ptr(xin), K.ptr(u.dy), B, fin, fout, act[0], act[1], 1.0, None, None,
+                K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
+                K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
+                K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
+                e.opt_id, float(e.lr), K.ptr(e.dstep), st), "dd_wgrad(update)")
+        else:
+            self._rc(lib.csa_dd_wgrad(
+                K.ptr(xin), K.ptr(u.dy), B, fin, fout, act[0], act[1], 1.0,
+                K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+                None, None, None, None, None, None, -1, 0.0, None, st), "dd_wgrad")
+
     def _dense_bwd_update(self, u: Unit, prev: Optional[Unit], st) -> None:
         """Dense backward + optimizer update of W / b in one launch (dense_update.hip)."""
         e, lib, B = self.e, self.lib, self.B
@@ -1091,7 +1161,7 @@ class HipProgram:
         ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
         skip = set()
         for u in self.units:
-            if u.kind == "dense" and u.fused:
+            if u.kind == "dense" and (u.fused or u.direct_update):
                 skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
         if not skip:
             return []

@@ -112,6 +112,20 @@ def main() -> int:
                 else:
                     print(f"{i:2d} {name}: stage+bn {t[9]-t[8]} route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} "
                           f"dc1 {t[13]-t[12]} dwA {t[14]-t[13]} atomics {t[15]-t[14]}")
+    if os.environ.get("MB_DD"):
+        dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name.startswith("csa_dd_"):
+                for _ in range(3):
+                    dbg.zero_()
+                    dbg[4] = 2 ** 62
+                    eng.program.lib.csa_dd_debug(dbg.data_ptr())
+                    fn(*args)
+                    torch.cuda.synchronize()
+                    eng.program.lib.csa_dd_debug(None)
+                t = dbg.tolist()
+                print(f"{i:2d} {name}: block0 loop {t[1]-t[0]} reduce {t[2]-t[1]} epilogue {t[3]-t[2]} "
+                      f"| block0 total {t[3]-t[0]} | all blocks span {t[5]-t[4]}  first start->b0 start {t[0]-t[4]}")
     for i, (name, fn, args) in enumerate(rec.calls):
         for _ in range(5):
             fn(*args)
