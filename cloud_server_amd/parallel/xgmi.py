@@ -126,6 +126,8 @@ class XgmiChannel:
         ``protocol``: "oneshot" (push everything to everyone), "twoshot" (reduce-scatter +
         all-gather), default the channel's pinned choice or the size crossover."""
         p = protocol or self.protocol
+        if self.world == 1:
+            p = "oneshot"             # nothing to scatter (and no room for two phases)
         if p is None:
             nbytes = sum(t.numel() * t.element_size() for t in tensors)
             p = "twoshot" if nbytes >= TWO_SHOT_MIN_BYTES and self.world > 2 else "oneshot"
@@ -196,7 +198,7 @@ def self_test(comm: XgmiComm) -> bool:
         y = x.clone()
         ch.all_reduce([y], protocol="oneshot")
         y2 = x.clone()
-        ch.all_reduce([y2], protocol="twoshot")
+        ch.all_reduce([y2], protocol="twoshot" if W > 2 else "oneshot")
         torch.cuda.synchronize(dev)
         want_sum = W * torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * sum(range(W))
         ok = (ch.error() == 0 and torch.equal(out, want) and torch.equal(y, want_sum)
