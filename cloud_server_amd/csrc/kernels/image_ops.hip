@@ -34,6 +34,26 @@ __device__ __forceinline__ uint8_t sat_rint(double v) {
   return (uint8_t)(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
 }
 
+// ------------------------------------------------------------------ counter RNG
+// Counter-based draws shared bit for bit with ops_ref.crng (NumPy): image i, draw j ->
+// splitmix64(splitmix64((i << 32) | j) ^ seed) >> 32.  No state: every pixel/thread
+// computes its own draw, so the random ops run entirely on the device.
+__device__ __forceinline__ uint64_t smix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t crng(uint64_t seed, uint64_t i, uint64_t j) {
+  return (uint32_t)(smix(smix((i << 32) | j) ^ seed) >> 32);
+}
+__device__ __forceinline__ double crng_uniform(uint64_t seed, uint64_t i, uint64_t j) {   // [0, 1), 24 bits
+  return (double)(crng(seed, i, j) >> 8) * (1.0 / 16777216.0);
+}
+__device__ __forceinline__ int crng_below(uint64_t seed, uint64_t i, uint64_t j, uint32_t n) {   // [0, n)
+  return (int)(((uint64_t)crng(seed, i, j) * n) >> 32);
+}
+
 // ------------------------------------------------------------------ flips (P0-P2)
 // mode 0: up-down, 1: left-right, 2: both (the reference "transpose" = cv2.flip(-1))
 __global__ __launch_bounds__(256) void flip_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
@@ -59,6 +79,25 @@ __global__ __launch_bounds__(256) void affine_kernel(const uint8_t* __restrict__
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long n = i / HW;
     const double v = (double)in[i] * alpha[n] + beta[n];
+    if (wrap) {
+      long t = (long)trunc(v) % 256;
+      out[i] = (uint8_t)(t < 0 ? t + 256 : t);
+    } else {
+      out[i] = sat_rint(v);
+    }
+  }
+}
+
+// random variant: alpha = U(0, max_alpha), beta = randint(-max_beta, max_beta) per image
+// from the counter RNG (draws 0 and 1 of image n), computed by every thread itself
+__global__ __launch_bounds__(256) void affine_rand_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                          long total, long HW, uint64_t seed, double max_alpha,
+                                                          int max_beta, int wrap) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / HW;
+    const double alpha = crng_uniform(seed, n, 0) * max_alpha;
+    const double beta = (double)(crng_below(seed, n, 1, (uint32_t)(2 * max_beta + 1)) - max_beta);
+    const double v = (double)in[i] * alpha + beta;
     if (wrap) {
       long t = (long)trunc(v) % 256;
       out[i] = (uint8_t)(t < 0 ? t + 256 : t);
@@ -231,6 +270,36 @@ __global__ __launch_bounds__(IMG_THREADS) void clahe_kernel(const uint8_t* __res
   }
 }
 
+// Median with a compile-time window: the k*k values live in registers (a runtime-sized
+// array went to scratch) and the rank selection is fully unrolled and branch-free.
+template <int K>
+__global__ __launch_bounds__(IMG_THREADS) void median_kernel(const uint8_t* __restrict__ in,
+                                                             uint8_t* __restrict__ out, int H, int W) {
+  extern __shared__ uint8_t s_img[];
+  constexpr int R = K / 2, N = K * K, M = N / 2;
+  const long base = (long)blockIdx.x * H * W;
+  const int HW = H * W;
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) s_img[p] = in[base + p];
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += IMG_THREADS) {
+    const int y = p / W, x = p - y * W;
+    int v[N];
+#pragma unroll
+    for (int dy = 0; dy < K; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) v[dy * K + dx] = s_img[clampi(y + dy - R, H) * W + clampi(x + dx - R, W)];
+    int med = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      int lt = 0, le = 0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) { lt += v[j] < v[i]; le += v[j] <= v[i]; }
+      med = (lt <= M && M < le) ? v[i] : med;
+    }
+    out[base + p] = (uint8_t)med;
+  }
+}
+
 // ------------------------------------------------------------------ non-local means (P8)
 // w(p,q) = exp(-max(0, d2)/h^2), d2 = mean squared 7x7 template difference (exact int
 // sum), 21x21 search window, REFLECT_101 padding staged once in LDS.
@@ -269,6 +338,71 @@ __global__ __launch_bounds__(IMG_THREADS) void nlmeans_kernel(const uint8_t* __r
   }
 }
 
+// Box-sum formulation (what the NumPy spec computes): for each of the 441 shifts the
+// squared differences of the (H+2tr) x (W+2tr) template area are summed with a vertical
+// then a horizontal running 7-window — ~13k integer ops per shift instead of 49 per
+// pixel per shift — and every pixel's weight / accumulator update follows.  Sums are
+// exact integers, the weight is the double exp of the spec.  LDS: padded image (uint8),
+// the difference plane and the vertical sums (int).
+__global__ __launch_bounds__(IMG_THREADS) void nlmeans_box_kernel(const uint8_t* __restrict__ in,
+                                                                  uint8_t* __restrict__ out, int H, int W,
+                                                                  double inv_h2, int tr, int sr) {
+  extern __shared__ int s_nl[];
+  const int pad = tr + sr, PW = W + 2 * pad, PH = H + 2 * pad;
+  const int T = 2 * tr + 1, AW = W + 2 * tr, AH = H + 2 * tr;      // template area
+  uint8_t* s_p = reinterpret_cast<uint8_t*>(s_nl);                  // [PH][PW]
+  int* s_d = s_nl + (PH * PW + 3) / 4;                              // [AH][AW] squared diffs
+  int* s_v = s_d + AH * AW;                                         // [H][AW] vertical sums
+  const long base = (long)blockIdx.x * H * W;
+  for (int p = threadIdx.x; p < PH * PW; p += IMG_THREADS) {
+    const int y = p / PW, x = p - y * PW;
+    s_p[p] = in[base + (long)reflect101(y - pad, H) * W + reflect101(x - pad, W)];
+  }
+  const double inv = inv_h2 / (double)(T * T);
+  constexpr int MAXP = 4;                      // pixels per thread (H*W <= 1024)
+  double acc[MAXP], wsum[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) acc[q] = wsum[q] = 0.0;
+  __syncthreads();
+  for (int dy = -sr; dy <= sr; ++dy) {
+    for (int dx = -sr; dx <= sr; ++dx) {
+      // 1) squared differences over the template area (area origin = padded (sr, sr))
+      for (int p = threadIdx.x; p < AH * AW; p += IMG_THREADS) {
+        const int y = p / AW + sr, x = p - (p / AW) * AW + sr;
+        const int d = (int)s_p[y * PW + x] - (int)s_p[(y + dy) * PW + x + dx];
+        s_d[p] = d * d;
+      }
+      __syncthreads();
+      // 2) vertical T-sums: rows y..y+T-1 of the area for output row y
+      for (int p = threadIdx.x; p < H * AW; p += IMG_THREADS) {
+        const int y = p / AW, x = p - y * AW;
+        int sum = 0;
+        for (int t = 0; t < T; ++t) sum += s_d[(y + t) * AW + x];
+        s_v[p] = sum;
+      }
+      __syncthreads();
+      // 3) horizontal T-sums -> weight -> accumulate this thread's pixels
+#pragma unroll
+      for (int q = 0; q < MAXP; ++q) {
+        const int p = threadIdx.x + q * IMG_THREADS;
+        if (p >= H * W) break;
+        const int y = p / W, x = p - y * W;
+        int d2 = 0;
+        for (int t = 0; t < T; ++t) d2 += s_v[y * AW + x + t];
+        const double w = exp(-(double)d2 * inv);
+        acc[q] += w * (double)s_p[(y + pad + dy) * PW + x + pad + dx];
+        wsum[q] += w;
+      }
+      __syncthreads();                         // s_d / s_v are rewritten by the next shift
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) {
+    const int p = threadIdx.x + q * IMG_THREADS;
+    if (p < H * W) out[base + p] = sat_rint(acc[q] / wsum[q]);
+  }
+}
+
 // ------------------------------------------------------------------ salt & pepper (P9)
 // Coordinates are drawn on the host with the reference RNG order; per image: all salt
 // (255) writes, barrier, then all pepper (0) writes.  Operates in place on ``img``.
@@ -279,6 +413,21 @@ __global__ __launch_bounds__(IMG_THREADS) void salt_pepper_kernel(uint8_t* __res
   for (int i = threadIdx.x; i < m; i += IMG_THREADS) img[base + (long)c[i] * W + c[m + i]] = 255;
   __syncthreads();
   for (int i = threadIdx.x; i < m; i += IMG_THREADS) img[base + (long)c[2 * m + i] * W + c[3 * m + i]] = 0;
+}
+
+// counter-RNG variant: copies the image, then salt draw j = (y: 2+4j, x: 3+4j) and pepper
+// draw j = (y: 4+4j, x: 5+4j) of image n (all salt, barrier, all pepper)
+__global__ __launch_bounds__(IMG_THREADS) void salt_pepper_rand_kernel(const uint8_t* __restrict__ in,
+                                                                       uint8_t* __restrict__ out, int H, int W,
+                                                                       uint64_t seed, int m) {
+  const long n = blockIdx.x, base = n * H * W;
+  for (int p = threadIdx.x; p < H * W; p += IMG_THREADS) out[base + p] = in[base + p];
+  __syncthreads();
+  for (int j = threadIdx.x; j < m; j += IMG_THREADS)
+    out[base + (long)crng_below(seed, n, 2 + 4 * (uint64_t)j, H) * W + crng_below(seed, n, 3 + 4 * (uint64_t)j, W)] = 255;
+  __syncthreads();
+  for (int j = threadIdx.x; j < m; j += IMG_THREADS)
+    out[base + (long)crng_below(seed, n, 4 + 4 * (uint64_t)j, H) * W + crng_below(seed, n, 5 + 4 * (uint64_t)j, W)] = 0;
 }
 
 // ------------------------------------------------------------------ bicubic resize (P14)
@@ -353,6 +502,22 @@ CSA_API int csa_img_affine(const uint8_t* in, uint8_t* out, int N, int H, int W,
   return (int)hipGetLastError();
 }
 
+CSA_API int csa_img_affine_rand(const uint8_t* in, uint8_t* out, int N, int H, int W, unsigned long long seed,
+                                double max_alpha, int max_beta, int wrap, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || max_beta < 0) return -1;
+  const long total = (long)N * H * W;
+  hipLaunchKernelGGL(affine_rand_kernel, dim3(grid_for(total)), dim3(256), 0, st, in, out, total, (long)H * W,
+                     (uint64_t)seed, max_alpha, max_beta, wrap);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_img_salt_pepper_rand(const uint8_t* in, uint8_t* out, int N, int H, int W, unsigned long long seed,
+                                     int m, hipStream_t st) {
+  if (N <= 0 || m < 0 || in == out) return -1;
+  hipLaunchKernelGGL(salt_pepper_rand_kernel, dim3(N), dim3(IMG_THREADS), 0, st, in, out, H, W, (uint64_t)seed, m);
+  return (int)hipGetLastError();
+}
+
 CSA_API int csa_img_sep_filter(const uint8_t* in, uint8_t* out, int N, int H, int W, const double* taps, int k,
                                hipStream_t st) {
   if (N <= 0 || H * W > MAX_IMG_PIX / 2 || k < 1 || k > 31 || in == out) return -1;
@@ -367,6 +532,13 @@ CSA_API int csa_img_rank_filter(const uint8_t* in, uint8_t* out, int N, int H, i
                                 hipStream_t st) {
   if (N <= 0 || H * W > MAX_IMG_PIX || k < 1 || op < 0 || op > 2 || in == out) return -1;
   if (op == 0 && (k > 7 || (k & 1) == 0)) return -1;
+  if (op == 0) {                         // median: register window, unrolled selection
+    if (k == 1) hipLaunchKernelGGL(median_kernel<1>, dim3(N), dim3(IMG_THREADS), H * W, st, in, out, H, W);
+    if (k == 3) hipLaunchKernelGGL(median_kernel<3>, dim3(N), dim3(IMG_THREADS), H * W, st, in, out, H, W);
+    if (k == 5) hipLaunchKernelGGL(median_kernel<5>, dim3(N), dim3(IMG_THREADS), H * W, st, in, out, H, W);
+    if (k == 7) hipLaunchKernelGGL(median_kernel<7>, dim3(N), dim3(IMG_THREADS), H * W, st, in, out, H, W);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(rank_filter_kernel, dim3(N), dim3(IMG_THREADS), H * W, st, in, out, H, W, k, op);
   return (int)hipGetLastError();
 }
@@ -395,6 +567,15 @@ CSA_API int csa_img_nlmeans(const uint8_t* in, uint8_t* out, int N, int H, int W
   const int tr = template_size / 2, sr = search_size / 2;
   if (N <= 0 || h <= 0.f || (H + 2 * (tr + sr)) * (W + 2 * (tr + sr)) > MAX_IMG_PIX || in == out) return -1;
   const int pad = tr + sr;
+  if (H * W <= 4 * IMG_THREADS) {       // box-sum kernel: <= 4 pixels per thread
+    const int AW = W + 2 * tr, AH = H + 2 * tr;
+    const size_t lds = ((size_t)((H + 2 * pad) * (W + 2 * pad) + 3) / 4 + (size_t)AH * AW + (size_t)H * AW) * 4;
+    if (lds <= 64 * 1024) {
+      hipLaunchKernelGGL(nlmeans_box_kernel, dim3(N), dim3(IMG_THREADS), lds, st, in, out, H, W,
+                         1.0 / ((double)h * (double)h), tr, sr);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL(nlmeans_kernel, dim3(N), dim3(IMG_THREADS), (H + 2 * pad) * (W + 2 * pad), st, in, out, H, W,
                      1.0 / ((double)h * (double)h), tr, sr);
   return (int)hipGetLastError();

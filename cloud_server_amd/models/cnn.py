@@ -139,6 +139,7 @@ class DigitNet(nn.Module):
         # squares, count} are all-reduced (autograd-aware, so the backward statistics are
         # global too) and every replica normalises with the GLOBAL batch statistics
         self.sync_bn = False
+        self.deterministic = False          # CSA_DETERMINISTIC: atomics-free op choices
         self.state = FlatState(plan.param_shapes(dense_last), device=device, pad_multiple=pad_multiple)
         init_params(plan, self.state, seed)
         self.flat = nn.Parameter(self.state.buffer)
@@ -184,6 +185,14 @@ class DigitNet(nn.Module):
             t = h.permute(0, 3, 1, 2)
             if any(lp.pads):
                 t = F.pad(t, (pl, pr, pt, pb), value=float("-inf"))
+            if self.deterministic:
+                # gather-form max pool: unfold + max (backward = one scatter per window +
+                # col2im, both free of atomics) instead of max_pool2d's atomic backward
+                Bn, Cn, Hn, Wn = t.shape
+                kh, kw = sp.kernel
+                oh, ow = (Hn - kh) // sp.stride[0] + 1, (Wn - kw) // sp.stride[1] + 1
+                cols = F.unfold(t, (kh, kw), stride=sp.stride).view(Bn, Cn, kh * kw, oh * ow)
+                return cols.max(dim=2).values.view(Bn, Cn, oh, ow).permute(0, 2, 3, 1)
             return F.max_pool2d(t, sp.kernel, sp.stride).permute(0, 2, 3, 1)
         if isinstance(sp, ActSpec):
             return act_fwd(h, sp)

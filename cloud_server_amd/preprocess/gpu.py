@@ -36,6 +36,8 @@ _SIGS = {
     "csa_img_resize": (C.c_int, [K.P, K.P, K.I, K.I, K.I, K.I, K.P, K.P, K.P, K.P, K.P]),
     "csa_img_infer_prep": (C.c_int, [K.P, K.P, K.I, K.P]),
     "csa_img_infer_prep_u8": (C.c_int, [K.P, K.P, K.I, K.P]),
+    "csa_img_affine_rand": (C.c_int, [K.P, K.P, K.I, K.I, K.I, C.c_ulonglong, C.c_double, K.I, K.I, K.P]),
+    "csa_img_salt_pepper_rand": (C.c_int, [K.P, K.P, K.I, K.I, K.I, C.c_ulonglong, K.I, K.P]),
 }
 _bound = False
 
@@ -108,7 +110,7 @@ def infer_prep(img20: Batch) -> torch.Tensor:
 
 
 def apply_op(name: str, batch: Batch, value1=None, value2=None, *, mode: str = "saturate",
-             rng: Optional[np.random.Generator] = None) -> Batch:
+             rng: Optional[np.random.Generator] = None, seed: Optional[int] = None) -> Batch:
     """``ops_ref.apply_op`` on the device.  Returns the same container type as ``batch``."""
     name = ops_ref.OP_MAP.get(name, name)
     lib = _lib()
@@ -120,20 +122,17 @@ def apply_op(name: str, batch: Batch, value1=None, value2=None, *, mode: str = "
     if name in ("flip_up_down", "flip_left_right", "transpose_image"):
         m = {"flip_up_down": 0, "flip_left_right": 1, "transpose_image": 2}[name]
         _check(lib.csa_img_flip(xp, op, n, H, W, m, st), name)
-    elif name in ("adjust_brightness_contrast", "random_brightness_contrast"):
-        if name == "adjust_brightness_contrast":
-            a = np.full(n, 1.0 if value1 is None else float(value1))
-            b = np.full(n, 0.0 if value2 is None else float(value2))
-        else:
-            rng = rng or np.random.default_rng()
-            max_alpha = 1.0 if value1 is None else float(value1)
-            max_beta = 0 if value2 is None else int(value2)
-            a, b = np.empty(n), np.empty(n)
-            for i in range(n):                       # same draw order as ops_ref
-                a[i] = rng.uniform(0, max_alpha)
-                b[i] = int(rng.integers(-max_beta, max_beta + 1))
+    elif name == "adjust_brightness_contrast":
+        a = np.full(n, 1.0 if value1 is None else float(value1))
+        b = np.full(n, 0.0 if value2 is None else float(value2))
         da, db = _d(a, torch.float64), _d(b, torch.float64)
         _check(lib.csa_img_affine(xp, op, n, H, W, da.data_ptr(), db.data_ptr(), int(mode == "wrap"), st), name)
+    elif name == "random_brightness_contrast":
+        # per-image draws from the counter RNG inside the kernel (ops_ref.crng)
+        s = ops_ref.seed_from(rng, seed)
+        max_alpha = 1.0 if value1 is None else float(value1)
+        max_beta = 0 if value2 is None else int(value2)
+        _check(lib.csa_img_affine_rand(xp, op, n, H, W, s, max_alpha, max_beta, int(mode == "wrap"), st), name)
     elif name in ("mean_filter", "gaussian_blur"):
         k = int(value1 or 3)
         if name == "gaussian_blur" and (k % 2 == 0 or k < 1):
@@ -156,15 +155,9 @@ def apply_op(name: str, batch: Batch, value1=None, value2=None, *, mode: str = "
     elif name == "nl_denoise_gray":
         _check(lib.csa_img_nlmeans(xp, op, n, H, W, float(value1 or 10), 7, 21, st), name)
     elif name == "add_salt_pepper_noise":
-        rng = rng or np.random.default_rng()
+        s = ops_ref.seed_from(rng, seed)
         m = int(H * W * float(value1 or 0))
-        coords = np.empty((n, 4, m), np.int32)
-        for i in range(n):                           # same draw order as ops_ref
-            coords[i, 0], coords[i, 1] = rng.integers(0, H, m), rng.integers(0, W, m)
-            coords[i, 2], coords[i, 3] = rng.integers(0, H, m), rng.integers(0, W, m)
-        out.copy_(x)
-        dc = _d(coords, torch.int32)
-        _check(lib.csa_img_salt_pepper(op, n, H, W, dc.data_ptr(), m, st), name)
+        _check(lib.csa_img_salt_pepper_rand(xp, op, n, H, W, s, m, st), name)
     else:
         raise ValueError(f"unknown preprocessing op {name!r}")
     return _finish(batch, out)

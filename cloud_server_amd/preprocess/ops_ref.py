@@ -126,18 +126,61 @@ def adjust_brightness_contrast(img, alpha=1.0, beta=0.0, mode: str = "saturate")
     return _sat(v)
 
 
+# ------------------------------------------------------------------------ counter RNG
+# Stateless draws shared bit for bit with the device kernels (image_ops.hip `crng`):
+# image i, draw j -> splitmix64(splitmix64((i << 32) | j) ^ seed) >> 32.  A batch's
+# random parameters are a pure function of (seed, image, draw), so the GPU computes them
+# in-kernel and this spec reproduces them exactly.
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _smix(z: np.ndarray) -> np.ndarray:
+    z = z + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def crng(seed: int, i, j) -> np.ndarray:
+    """uint32 draws for image indices ``i`` and draw indices ``j`` (broadcast)."""
+    i = np.asarray(i, np.uint64)
+    j = np.asarray(j, np.uint64)
+    with np.errstate(over="ignore"):
+        z = _smix((i << np.uint64(32)) | j) ^ np.uint64(int(seed) & 0xFFFFFFFFFFFFFFFF)
+        return (_smix(z) >> np.uint64(32)).astype(np.uint64)
+
+
+def crng_uniform(seed: int, i, j) -> np.ndarray:
+    return (crng(seed, i, j) >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
+
+
+def crng_below(seed: int, i, j, n: int) -> np.ndarray:
+    return ((crng(seed, i, j) * np.uint64(n)) >> np.uint64(32)).astype(np.int64)
+
+
+def seed_from(rng: Optional[np.random.Generator] = None, seed: Optional[int] = None) -> int:
+    """The counter-RNG seed of one op application: ``seed`` if given, else one draw of
+    ``rng`` (so a seeded pipeline is reproducible and CPU == GPU for the same rng)."""
+    if seed is not None:
+        return int(seed) & ((1 << 63) - 1)
+    return int((rng or np.random.default_rng()).integers(0, 1 << 62))
+
+
 def random_brightness_contrast(img, max_alpha=1.0, max_beta=0, mode: str = "saturate",
-                               rng: Optional[np.random.Generator] = None):
-    rng = rng or np.random.default_rng()
+                               rng: Optional[np.random.Generator] = None, seed: Optional[int] = None):
+    """alpha ~ U(0, max_alpha), beta ~ randint(-max_beta, max_beta), one draw per image
+    (preprocess.py:105-106), from the counter RNG (draws 0 and 1 of each image)."""
+    s = seed_from(rng, seed)
     b = _as_batch(img)
     max_alpha = 1.0 if max_alpha is None else float(max_alpha)
     max_beta = 0 if max_beta is None else int(max_beta)
-    out = np.empty_like(b)
-    for i in range(b.shape[0]):                     # one draw per image (preprocess.py:105-106)
-        a = rng.uniform(0, max_alpha)
-        be = int(rng.integers(-max_beta, max_beta + 1))
-        out[i] = adjust_brightness_contrast(b[i], a, be, mode)[0]
-    return out
+    idx = np.arange(b.shape[0])
+    a = crng_uniform(s, idx, 0) * max_alpha
+    be = (crng_below(s, idx, 1, 2 * max_beta + 1) - max_beta).astype(np.float64)
+    v = b.astype(np.float64) * a[:, None, None] + be[:, None, None]
+    if mode == "wrap":
+        return (np.trunc(v).astype(np.int64) % 256).astype(np.uint8)
+    return _sat(v)
 
 
 # ------------------------------------------------------------------------ linear filters
@@ -241,16 +284,22 @@ def nl_denoise_gray(img, h=10, *_, template: int = 7, search: int = 21):
 
 
 # ------------------------------------------------------------------------ noise
-def add_salt_pepper_noise(img, percent=0.05, *_, rng: Optional[np.random.Generator] = None):
-    rng = rng or np.random.default_rng()
+def add_salt_pepper_noise(img, percent=0.05, *_, rng: Optional[np.random.Generator] = None,
+                          seed: Optional[int] = None):
+    """m = H*W*percent salt pixels (255) then m pepper pixels (0) per image
+    (preprocess.py:155-170); coordinates from the counter RNG: salt j = draws (2+4j, 3+4j),
+    pepper j = draws (4+4j, 5+4j)."""
+    s = seed_from(rng, seed)
     b = _as_batch(img).copy()
     n, H, W = b.shape
     m = int(H * W * float(percent or 0))       # reference assumes 28x28 (preprocess.py:162)
-    for i in range(n):
-        ys, xs = rng.integers(0, H, m), rng.integers(0, W, m)
-        b[i, ys, xs] = 255
-        ys, xs = rng.integers(0, H, m), rng.integers(0, W, m)
-        b[i, ys, xs] = 0
+    if m == 0 or n == 0:
+        return b
+    i = np.arange(n)[:, None]
+    j = np.arange(m)[None, :]
+    rows = np.broadcast_to(i, (n, m))
+    b[rows, crng_below(s, i, 2 + 4 * j, H), crng_below(s, i, 3 + 4 * j, W)] = 255
+    b[rows, crng_below(s, i, 4 + 4 * j, H), crng_below(s, i, 5 + 4 * j, W)] = 0
     return b
 
 

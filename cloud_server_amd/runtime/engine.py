@@ -36,6 +36,19 @@ from ..utils.tracing import trace_range
 RING = 4096
 
 
+def deterministic_mode() -> bool:
+    import os
+    return os.environ.get("CSA_DETERMINISTIC", "0") == "1"
+
+
+def enable_deterministic_torch() -> None:
+    import os
+    os.environ.setdefault("CUBLAS_WORKSPACE_CONFIG", ":4096:8")
+    torch.use_deterministic_algorithms(True)
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+
+
 class StepProgram:
     """Interface: ``run()`` performs one full training step on device (capturable)."""
 
@@ -91,10 +104,20 @@ class TrainEngine:
         self.ring_correct = torch.zeros(RING, dtype=torch.int32, device=self.device)
         self.ring_loss = torch.zeros(RING, dtype=torch.float32, device=self.device)
         self.host_step = 0
+        # CSA_DETERMINISTIC=1: bitwise-reproducible steps for tests and
+        # debugging — the HIP program's split-K / statistics atomics make its fp32 sums
+        # order-dependent, so the step runs on the eager program with PyTorch's
+        # deterministic algorithms, atomics-free pooling and fixed-order collectives
+        # (RCCL ring / the xGMI kernels sum in rank order); still captured in a HIP graph
+        self.deterministic = deterministic_mode()
+        if self.deterministic:
+            backend = "torch"
+            enable_deterministic_torch()
+            self.model.deterministic = True
         if backend == "auto":
             backend = "hip" if self.device.type == "cuda" else "torch"
         self.backend = backend
-        self.fallback_reason = ""
+        self.fallback_reason = "deterministic mode" if self.deterministic else ""
         if backend == "hip":
             from .hip_program import HipProgram, Unsupported
             try:
