@@ -358,40 +358,62 @@ __global__ __launch_bounds__(IMG_THREADS) void nlmeans_box_kernel(const uint8_t*
     const int y = p / PW, x = p - y * PW;
     s_p[p] = in[base + (long)reflect101(y - pad, H) * W + reflect101(x - pad, W)];
   }
-  const double inv = inv_h2 / (double)(T * T);
-  constexpr int MAXP = 4;                      // pixels per thread (H*W <= 1024)
+  // every shift visits the same positions: their offsets are computed once (no integer
+  // division inside the 441-shift loop)
+  constexpr int MAXA = 8, MAXV = 8, MAXP = 4;  // area <= 2048, vertical <= 2048, pixels <= 1024
+  int oa[MAXA], ov[MAXV], op_[MAXP], opp[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXA; ++q) {
+    const int p = threadIdx.x + q * IMG_THREADS;
+    const int y = p / AW, x = p - (p / AW) * AW;
+    oa[q] = p < AH * AW ? (y + sr) * PW + x + sr : -1;            // area pixel in s_p
+  }
+#pragma unroll
+  for (int q = 0; q < MAXV; ++q) {
+    const int p = threadIdx.x + q * IMG_THREADS;
+    ov[q] = p < H * AW ? p : -1;                                     // s_v index; s_d row y = p / AW
+  }
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) {
+    const int p = threadIdx.x + q * IMG_THREADS;
+    const int y = p / W, x = p - (p / W) * W;
+    op_[q] = p < H * W ? y * AW + x : -1;                            // s_v start of the window
+    opp[q] = (y + pad) * PW + x + pad;                               // pixel in s_p
+  }
+  const float inv = (float)(inv_h2 / (double)(T * T));
   double acc[MAXP], wsum[MAXP];
 #pragma unroll
   for (int q = 0; q < MAXP; ++q) acc[q] = wsum[q] = 0.0;
   __syncthreads();
   for (int dy = -sr; dy <= sr; ++dy) {
     for (int dx = -sr; dx <= sr; ++dx) {
-      // 1) squared differences over the template area (area origin = padded (sr, sr))
-      for (int p = threadIdx.x; p < AH * AW; p += IMG_THREADS) {
-        const int y = p / AW + sr, x = p - (p / AW) * AW + sr;
-        const int d = (int)s_p[y * PW + x] - (int)s_p[(y + dy) * PW + x + dx];
-        s_d[p] = d * d;
+      const int sh = dy * PW + dx;
+      // 1) squared differences over the template area
+#pragma unroll
+      for (int q = 0; q < MAXA; ++q) {
+        if (oa[q] < 0) break;
+        const int d = (int)s_p[oa[q]] - (int)s_p[oa[q] + sh];
+        s_d[threadIdx.x + q * IMG_THREADS] = d * d;
       }
       __syncthreads();
-      // 2) vertical T-sums: rows y..y+T-1 of the area for output row y
-      for (int p = threadIdx.x; p < H * AW; p += IMG_THREADS) {
-        const int y = p / AW, x = p - y * AW;
+      // 2) vertical T-sums (s_d rows y..y+T-1 -> s_v[y]); same flat index p = y*AW + x
+#pragma unroll
+      for (int q = 0; q < MAXV; ++q) {
+        if (ov[q] < 0) break;
         int sum = 0;
-        for (int t = 0; t < T; ++t) sum += s_d[(y + t) * AW + x];
-        s_v[p] = sum;
+        for (int t = 0; t < T; ++t) sum += s_d[ov[q] + t * AW];
+        s_v[ov[q]] = sum;
       }
       __syncthreads();
-      // 3) horizontal T-sums -> weight -> accumulate this thread's pixels
+      // 3) horizontal T-sums -> weight -> this thread's pixels
 #pragma unroll
       for (int q = 0; q < MAXP; ++q) {
-        const int p = threadIdx.x + q * IMG_THREADS;
-        if (p >= H * W) break;
-        const int y = p / W, x = p - y * W;
+        if (op_[q] < 0) break;
         int d2 = 0;
-        for (int t = 0; t < T; ++t) d2 += s_v[y * AW + x + t];
-        const double w = exp(-(double)d2 * inv);
-        acc[q] += w * (double)s_p[(y + pad + dy) * PW + x + pad + dx];
-        wsum[q] += w;
+        for (int t = 0; t < T; ++t) d2 += s_v[op_[q] + t];
+        const float w = __expf(-(float)d2 * inv);
+        acc[q] += (double)(w * (float)s_p[opp[q] + sh]);
+        wsum[q] += (double)w;
       }
       __syncthreads();                         // s_d / s_v are rewritten by the next shift
     }
@@ -567,7 +589,8 @@ CSA_API int csa_img_nlmeans(const uint8_t* in, uint8_t* out, int N, int H, int W
   const int tr = template_size / 2, sr = search_size / 2;
   if (N <= 0 || h <= 0.f || (H + 2 * (tr + sr)) * (W + 2 * (tr + sr)) > MAX_IMG_PIX || in == out) return -1;
   const int pad = tr + sr;
-  if (H * W <= 4 * IMG_THREADS) {       // box-sum kernel: <= 4 pixels per thread
+  if (H * W <= 4 * IMG_THREADS && (H + 2 * tr) * (W + 2 * tr) <= 8 * IMG_THREADS &&
+      H * (W + 2 * tr) <= 8 * IMG_THREADS) {     // box-sum kernel's per-thread position tables
     const int AW = W + 2 * tr, AH = H + 2 * tr;
     const size_t lds = ((size_t)((H + 2 * pad) * (W + 2 * pad) + 3) / 4 + (size_t)AH * AW + (size_t)H * AW) * 4;
     if (lds <= 64 * 1024) {
