@@ -88,7 +88,8 @@ def bench_packed(args) -> int:
         import torch
         from cloud_server_amd.data.datasets import synthetic_mnist
         from cloud_server_amd.runtime.engine import TrainEngine
-        from cloud_server_amd.runtime.multijob import PackedJobs
+        from cloud_server_amd.runtime.multijob import PackedJobs, prefer_packed_kernels
+        prefer_packed_kernels()
         dev = "cuda:0" if torch.cuda.is_available() else "cpu"
         engs = []
         for r in range(K):

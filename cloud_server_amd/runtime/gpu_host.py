@@ -66,8 +66,9 @@ def _take_inbox(spool: str) -> List[dict]:
 
 
 def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0.0) -> int:
-    from .multijob import PackedJobs
+    from .multijob import PackedJobs, prefer_packed_kernels
     from .trainer import JobRun
+    prefer_packed_kernels()
 
     jobs: Dict[int, JobRun] = {}
     pack = None
