@@ -70,6 +70,7 @@ _SIGS = {
     "csa_dd_debug": (I, [P]),
     "csa_dd_fwd_splits": (I, [I, I, I]),
     "csa_dd_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
+    "csa_dd_fwd_bn": (I, [P, P, P, P, I, I, I, I, F, P, I, I, F, F, P, P, P, P]),
     "csa_dd_dgrad_splits": (I, [I, I, I]),
     "csa_dd_dgrad_slabs": (I, []),
     "csa_dd_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P]),

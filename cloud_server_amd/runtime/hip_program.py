@@ -871,6 +871,13 @@ class HipProgram:
                     e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
             else:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if u.direct and u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") == "1":
+                    # BN + act applied while the GEMM loads its input; N-tile 0 writes xt
+                    self._rc(lib.csa_dd_fwd_bn(
+                        K.ptr(u.x.view(B, -1)), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
+                        K.ptr(u.y), B, fout, fin, in_act, in_alpha, *self._bn_args_c(tf), K.ptr(u.xt), st),
+                        "dd_fwd_bn")
+                    continue
                 if u.xt is not None:
                     self._rc(lib.csa_bn_act_apply(
                         K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha, st),
