@@ -112,12 +112,120 @@ __device__ __forceinline__ void cp_stage_x(const CPGeom& g, const CPBand& t, con
 
 // Weights as a zero-padded [kpad][npad] LDS panel (the MFMA B operand), k = flattened
 // (i, j, cin) of the HWIO tensor.
+// Batches of 8 loads per thread from clamped addresses, pinned, then the stores: a load
+// inside the conditional that consumes it is sunk into it by hipcc and waited for there —
+// one serial memory round trip per loop iteration.
 __device__ __forceinline__ void cp_stage_panel(float* dst, const float* w, int K, int N, int kpad, int npad) {
   const FastDiv dn(npad);
-  for (int e = threadIdx.x; e < kpad * npad; e += CP_THREADS) {
+  const int total = kpad * npad;
+  constexpr int U = 8;
+  for (int base = 0; base < total; base += CP_THREADS * U) {
+    float v[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * CP_THREADS + (int)threadIdx.x;
+      int k, n;
+      dn.divmod(e < total ? e : 0, k, n);
+      ok[u] = e < total && k < K && n < N;
+      v[u] = w[ok[u] ? k * N + n : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) pin(v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * CP_THREADS + (int)threadIdx.x;
+      if (e < total) dst[e] = ok[u] ? v[u] : 0.f;
+    }
+  }
+}
+
+// Forward-kernel inputs in ONE batch of loads: panel A, panel B (the weights) and the x
+// tile.  The weight loads are issued first and stay in flight across the cursor -> row
+// index -> image chain (scalar loads), so the three round trips of separate staging
+// loops collapse into that chain alone.  Falls back to the loops when a thread would
+// hold more than the register batch.
+__device__ __forceinline__ void cp_stage_fwd_inputs(const CPGeom& g, const CPBand& t, const uint8_t* img,
+                                                    const int64_t* idx, const int64_t* cursor, int b,
+                                                    float* s_pA, const float* wA, int KA, int kpadA,
+                                                    float* s_pB, const float* wB, int KB, int kpadB, int pst,
+                                                    float* s_x);
+
+// dst[i] = i < n ? src[i] : 0 for i < total, same batching.
+__device__ __forceinline__ void cp_stage_flat(float* dst, const float* src, int n, int total) {
+  constexpr int U = 8;
+  for (int base = 0; base < total; base += CP_THREADS * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * CP_THREADS + (int)threadIdx.x;
+      v[u] = src[e < n ? e : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) pin(v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * CP_THREADS + (int)threadIdx.x;
+      if (e < total) dst[e] = e < n ? v[u] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void cp_stage_fwd_inputs(const CPGeom& g, const CPBand& t, const uint8_t* img,
+                                                    const int64_t* idx, const int64_t* cursor, int b,
+                                                    float* s_pA, const float* wA, int KA, int kpadA,
+                                                    float* s_pB, const float* wB, int KB, int kpadB, int pst,
+                                                    float* s_x) {
+  constexpr int UP = 8, UX = 2;
+  const int nA = kpadA * 16, nB = kpadB * pst, nP = nA + nB;
+  const int nX = t.TXH * t.TXW * g.C0;
+  if (nP > UP * CP_THREADS || nX > UX * CP_THREADS) {
+    cp_stage_x(g, t, cp_image(img, idx, cursor, b, g.B, (long)g.H * g.W * g.C0), s_x);
+    cp_stage_panel(s_pA, wA, KA, g.C1, kpadA, 16);
+    cp_stage_panel(s_pB, wB, KB, g.C2, kpadB, pst);
+    return;
+  }
+  const FastDiv d16(16), dpst(pst);
+  float pv[UP];
+  bool pok[UP];
+#pragma unroll
+  for (int u = 0; u < UP; ++u) {                 // weights: concatenated [panel A | panel B]
+    const int e = u * CP_THREADS + (int)threadIdx.x;
+    const bool inA = e < nA;
     int k, n;
-    dn.divmod(e, k, n);
-    dst[e] = (k < K && n < N) ? w[k * N + n] : 0.f;
+    if (inA) d16.divmod(e, k, n); else dpst.divmod(e < nP ? e - nA : 0, k, n);
+    const bool ok = e < nP && (inA ? (k < KA && n < g.C1) : (k < KB && n < g.C2));
+    pok[u] = ok;
+    pv[u] = ok ? (inA ? wA[k * g.C1 + n] : wB[k * g.C2 + n]) : 0.f;
+  }
+  // x tile: the row index chain (scalar loads) runs while the weights are in flight
+  const uint8_t* src = cp_image(img, idx, cursor, b, g.B, (long)g.H * g.W * g.C0);
+  const int y0 = t.c1y0 - g.PTA, x0 = -g.PLB - g.PLA;
+  const FastDiv dw(t.TXW * g.C0), dc(g.C0);
+  uint8_t xv[UX];
+  bool xok[UX];
+#pragma unroll
+  for (int u = 0; u < UX; ++u) {
+    const int e = u * CP_THREADS + (int)threadIdx.x;
+    int r, rem, xx, c;
+    dw.divmod(e < nX ? e : 0, r, rem);
+    dc.divmod(rem, xx, c);
+    const int y = y0 + r, x = x0 + xx;
+    xok[u] = e < nX && y >= 0 && y < g.H && x >= 0 && x < g.W;
+    xv[u] = src[xok[u] ? ((long)y * g.W + x) * g.C0 + c : 0];
+  }
+#pragma unroll
+  for (int u = 0; u < UP; ++u) pin(pv[u]);
+#pragma unroll
+  for (int u = 0; u < UP; ++u) {
+    const int e = u * CP_THREADS + (int)threadIdx.x;
+    if (e < nA) s_pA[e] = pok[u] ? pv[u] : 0.f;
+    else if (e < nP) s_pB[e - nA] = pok[u] ? pv[u] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < UX; ++u) {
+    const int e = u * CP_THREADS + (int)threadIdx.x;
+    if (e < nX) s_x[e] = xok[u] ? (float)xv[u] * (1.0f / 255.0f) : 0.f;
   }
 }
 
@@ -227,10 +335,9 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a) 
   float* s_x = reinterpret_cast<float*>(s_offPB + kpadB);
   float* s_c1 = s_x + ((t.TXH * t.TXW * g.C0 + 3) & ~3);
   CP_STAMP(0);
-  const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
-  cp_stage_x(g, t, src, s_x);
-  cp_stage_panel(s_pA, a.wA, KA, g.C1, kpadA, 16);
-  cp_stage_panel(s_pB, a.wB, KB, g.C2, kpadB, pst);
+  cp_stage_fwd_inputs(g, t, a.img, a.idx, a.cursor, b, s_pA, a.wA, KA, kpadA, s_pB, a.wB, KB, kpadB, pst, s_x);
+  CP_STAMP(5);
+  CP_STAMP(6);
   cp_tables_a(g, t, kpadA, s_offA, s_offPA);
   for (int k = threadIdx.x; k < kpadB; k += CP_THREADS) {     // c1 tile offset of tap (i, j, c1)
     int o = 0;
@@ -415,7 +522,7 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
   const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
   cp_stage_x(g, t, src, s_x);
   cp_stage_panel(s_pA, a.wA, L.KA, g.C1, L.kpadA, 16);
-  for (int i = threadIdx.x; i < L.kpadB * L.c16; i += CP_THREADS) s_wB[i] = i < L.KB * g.C2 ? a.wB[i] : 0.f;
+  cp_stage_flat(s_wB, a.wB, L.KB * g.C2, L.kpadB * L.c16);
   for (int i = threadIdx.x; i < L.D2H * L.D2W * g.C2; i += CP_THREADS) s_dc2[i] = 0.f;
   for (int i = threadIdx.x; i < g.C1; i += CP_THREADS) s_dc1[L.npix1 * g.C1 + i] = 0.f;
   cp_tables_a(g, t, L.kpadA, s_offA, s_offPA);

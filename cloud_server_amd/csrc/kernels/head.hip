@@ -515,9 +515,6 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
   float* s_lg = s_w + K * NCLS;            // [PRG_MAX][10] logits
   float* s_dl = s_lg + PRG_MAX * NCLS;     // [PRG_MAX][10] dlogits
   if (g == 0 && tid == 0) *a.step += 1;
-  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
-  int label = 0;
-  if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
   {
     const int K4 = K >> 2, nh4 = rows * K4, nw4 = (K * NCLS) >> 2, tot = nh4 + nw4;
     const float4* h4 = reinterpret_cast<const float4*>(a.h + (long)m0 * K);
@@ -547,6 +544,11 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
       }
     }
   }
+  // the label chain (cursor -> row index -> label) is only needed after the logits: it is
+  // issued after the staging loads so its two dependent round trips overlap them
+  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
+  int label = 0;
+  if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
   __syncthreads();
   // logits: wave w takes rows w, w+4, ...; lanes split K, then a wave reduction per class
   for (int r = wave; r < rows; r += 4) {

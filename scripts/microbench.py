@@ -108,7 +108,8 @@ def main() -> int:
                     eng.program.lib.csa_cp_debug(None)
                 t = dbg.tolist()
                 if name.endswith("fwd"):
-                    print(f"{i:2d} {name}: stage {t[1]-t[0]} convA {t[2]-t[1]} convB+pool {t[3]-t[2]} stats {t[4]-t[3]}")
+                    print(f"{i:2d} {name}: stage {t[1]-t[0]} (image {t[5]-t[0]} panels {t[6]-t[5]} tables {t[1]-t[6]}) "
+                          f"convA {t[2]-t[1]} convB+pool {t[3]-t[2]} stats {t[4]-t[3]}")
                 else:
                     print(f"{i:2d} {name}: stage+bn {t[9]-t[8]} route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} "
                           f"dc1 {t[13]-t[12]} dwA {t[14]-t[13]} atomics {t[15]-t[14]}")
