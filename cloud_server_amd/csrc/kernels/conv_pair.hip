@@ -24,6 +24,7 @@
 // (uint8 dataset rows gathered through the batch index stream).  Everything else uses the
 // per-layer kernels (conv.hip).
 #include "common.h"
+#include <cstdlib>
 #include <algorithm>
 
 namespace csa {
@@ -739,7 +740,10 @@ static bool cp_geom(const int* v, CPGeom& g) {
   if (g.W1 < 1 || g.H2 < 1 || g.W2 < 1) return false;
   if (((g.KAh * g.KAw * g.C0 + 3) & ~3) > 32) return false;   // static conv-A offset tables
   const int rows = g.pool ? g.PH : g.H2;
-  g.PR = g.pool ? 2 : 4;
+  static const int pr_env = [] { const char* e = getenv("CSA_CP_PR"); return e ? atoi(e) : 0; }();
+  // unit rows per workgroup: PR = 1 (pooled) measured 120.0 vs 124.8 (PR 2) vs 130.5 us (PR 3)
+  // per graph step — more workgroups (700 for B = 50) beat the per-band staging overhead
+  g.PR = pr_env > 0 ? pr_env : (g.pool ? 1 : 2);
   g.nbands = (rows + g.PR - 1) / g.PR;
   return true;
 }
