@@ -17,6 +17,7 @@
 //   * advance the batch-stream cursor (mod its wrap).
 #include "common.h"
 #include "optim_common.h"
+#include <cstdlib>
 
 namespace csa {
 
@@ -220,8 +221,12 @@ CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, lo
   long zmax = 0;
   for (int i = 0; i < nzero; ++i) zmax = zero_ns[i] > zmax ? zero_ns[i] : zmax;
   const long work = n4 > zmax ? n4 : zmax;
+  // block cap: swept on MI355X for the 2.28 M-parameter sample (graph step, µs): 512 ->
+  // 122.8, 1024 -> 121.0, 1536 -> 120.2, 2048 -> 120.3, 8192 (one float4 per thread) ->
+  // 121.6 — more blocks cost more than the grid-stride second iteration saves
+  static const int cap = [] { const char* e = getenv("CSA_OPT_MAX_BLOCKS"); return e ? atoi(e) : 2048; }();
   int blocks = (int)((work + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(optim_kernel, dim3(blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
