@@ -25,6 +25,7 @@
 // workgroup's K range; their partials meet in LDS in fixed wave order.
 #include "common.h"
 #include "optim_common.h"
+#include <cstdlib>
 
 namespace csa {
 
@@ -484,7 +485,9 @@ __global__ __launch_bounds__(DD_THREADS) void dd_wgrad_kernel(DDWgrad a) {
 
 // K slices: enough workgroups for ~1 wave per SIMD (1024), each wave >= 16 k.
 static int dd_splits(int tiles, int K) {
-  int ks = (1024 / DD_WAVES + tiles - 1) / tiles;
+  // waves per launch: swept 512 / 1024 / 2048 / 4096 -> graph step 125.4 / 120.3 / 119.5 / 122.5 us
+  static const int target = [] { const char* e = getenv("CSA_DD_WAVES"); return e ? atoi(e) : 2048; }();
+  int ks = (target / DD_WAVES + tiles - 1) / tiles;
   const int maxks = (K + 8 * DD_WAVES * 2 - 1) / (8 * DD_WAVES * 2);   // >= 16 k per wave
   ks = ks < 1 ? 1 : ks;
   ks = ks > maxks ? maxks : ks;

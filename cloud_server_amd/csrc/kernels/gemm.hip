@@ -17,6 +17,7 @@
 //   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
 //   D: reg r of lane l is D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31]
 #include "common.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace csa {
@@ -436,9 +437,10 @@ static Plan plan_gemm(int M, int N, int K, bool allow_split) {
   const int wg = ((tm + p.wm - 1) / p.wm) * ((tn + p.wn - 1) / p.wn);
   // split K across workgroups until each wave owns <= one KC chunk (one memory round
   // trip per wave), keeping the launch under ~4096 waves and 512 slices
+  static const int maxw = [] { const char* e = getenv("CSA_GEMM_MAX_WAVES"); return e ? atoi(e) : 4096; }();
   int splits = 1;
   if (allow_split)
-    while ((K + splits * p.wk - 1) / (splits * p.wk) > KC && wg * 4 * splits * 2 <= 4096 && splits < 512)
+    while ((K + splits * p.wk - 1) / (splits * p.wk) > KC && wg * 4 * splits * 2 <= maxw && splits < 512)
       splits *= 2;
   p.splits = splits;
   const int kps = (K + splits - 1) / splits;
