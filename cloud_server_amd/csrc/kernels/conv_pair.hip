@@ -80,6 +80,7 @@ __device__ __forceinline__ CPBand cp_band(const CPGeom& g, int r2a, int r2b) {
 
 __device__ __forceinline__ const uint8_t* cp_image(const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                                                    int b, int B, long imsz) {
+  if (!idx) return img + (long)b * imsz;        // staged batch: image b at a fixed address
   const int64_t* id = cursor ? idx + cursor[0] * B : idx;
   return img + id[b] * imsz;
 }

@@ -495,6 +495,8 @@ struct HeadPartArgs {
   float* mpart; int* mcorr;  // [G]
   float* logits_out;         // optional [M][10]
   int64_t* step;
+  int64_t* adv_cursor;       // batch staging: block 0 advances the stream cursor (mod wrap)
+  long wrap;
 };
 
 __host__ __device__ inline size_t head_part_lds(int RG, int K) {
@@ -514,7 +516,13 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
   float* s_w = s_h + RG * K;               // [K][10]
   float* s_lg = s_w + K * NCLS;            // [PRG_MAX][10] logits
   float* s_dl = s_lg + PRG_MAX * NCLS;     // [PRG_MAX][10] dlogits
-  if (g == 0 && tid == 0) *a.step += 1;
+  if (g == 0 && tid == 0) {
+    *a.step += 1;
+    if (a.adv_cursor) {          // the step's batch is staged: its kernels no longer read the cursor
+      const int64_t c = *a.adv_cursor + 1;
+      *a.adv_cursor = (a.wrap > 0 && c >= a.wrap) ? 0 : c;
+    }
+  }
   {
     const int K4 = K >> 2, nh4 = rows * K4, nw4 = (K * NCLS) >> 2, tot = nh4 + nw4;
     const float4* h4 = reinterpret_cast<const float4*>(a.h + (long)m0 * K);
@@ -546,9 +554,13 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
   }
   // the label chain (cursor -> row index -> label) is only needed after the logits: it is
   // issued after the staging loads so its two dependent round trips overlap them
-  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
   int label = 0;
-  if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
+  if (!a.idx) {                    // staged labels
+    if (tid < rows) label = (int)a.labels[m0 + tid];
+  } else {
+    const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
+    if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
+  }
   __syncthreads();
   // logits: wave w takes rows w, w+4, ...; lanes split K, then a wave reduction per class
   for (int r = wave; r < rows; r += 4) {
@@ -705,14 +717,29 @@ CSA_API int csa_head_part_rows(int M, int K) {
   return rg;
 }
 
+CSA_API int csa_head_part2(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
+                           const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,
+                           int loss, float grad_scale, float* dh, float* part, float* mpart, int* mcorr,
+                           float* logits_out, int64_t* step, int64_t* adv_cursor, long wrap, hipStream_t st);
+
 CSA_API int csa_head_part(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
                           const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,
                           int loss, float grad_scale, float* dh, float* part, float* mpart, int* mcorr,
                           float* logits_out, int64_t* step, hipStream_t st) {
+  return csa_head_part2(h, M, K, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, part, mpart,
+                        mcorr, logits_out, step, nullptr, 0, st);
+}
+
+// idx == null: labels are the staged [M] labels of the step; adv_cursor != null: block 0
+// advances the batch-stream cursor after the step counter.
+CSA_API int csa_head_part2(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
+                           const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,
+                           int loss, float grad_scale, float* dh, float* part, float* mpart, int* mcorr,
+                           float* logits_out, int64_t* step, int64_t* adv_cursor, long wrap, hipStream_t st) {
   const int rg = csa_head_part_rows(M, K);
   if (!rg) return -1;
   HeadPartArgs a{h, M, K, rg, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, part,
-                 mpart, mcorr, logits_out, step};
+                 mpart, mcorr, logits_out, step, adv_cursor, wrap};
   const size_t shm = head_part_lds(rg, K);
   if (shm > 64 * 1024) {
     static bool attr = hipFuncSetAttribute((const void*)head_part_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -44,6 +44,29 @@ struct MetricFold {        // head partials -> ring[(step - 1) % ring]
   float* ring_loss; int* ring_correct; int ring;
 };
 
+// The NEXT step's batch (rows[*cursor]) copied into fixed staging buffers, so the step's
+// kernels read their images / labels at fixed addresses instead of walking the cursor ->
+// row index -> image chain (two dependent round trips at the start of each kernel).  The
+// cursor was already advanced by this step's head kernel.
+struct BatchStage {
+  const uint32_t* img; const int64_t* labels; const int64_t* rows; const int64_t* cursor;
+  int B; long words;               // 32-bit words per image
+  uint32_t* out_img; int64_t* out_lbl;
+  int blocks;                      // trailing workgroups doing the copy (0: off)
+};
+
+__device__ __forceinline__ void stage_gather(const BatchStage& s, int blk) {
+  const long i = (long)blk * 256 + threadIdx.x;
+  const long total = (long)s.B * s.words;
+  const int64_t c = *s.cursor;
+  if (i < s.B) s.out_lbl[i] = s.labels[s.rows[c * s.B + i]];
+  if (i >= total) return;
+  const long b = i / s.words, off = i - b * s.words;
+  s.out_img[i] = s.img[s.rows[c * s.B + b] * s.words + off];
+}
+
+__global__ __launch_bounds__(256) void gather_batch_kernel(BatchStage s) { stage_gather(s, blockIdx.x); }
+
 struct OptArgs {
   int opt; float* w; const float* g; float* s0; float* s1;
   SegList seg;                     // flat segments to update
@@ -53,6 +76,7 @@ struct OptArgs {
   ZeroList z; FoldList fold; MetricFold met;
   int64_t* cursor;                 // batch-stream cursor: += 1 (mod cursor_wrap) per step
   long cursor_wrap;
+  BatchStage stage;                // next step's batch gathered by the trailing blocks
 };
 
 constexpr int MAXS = 16;   // stripes / partial rows per folded gradient
@@ -98,8 +122,13 @@ __device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g
 }
 
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
+  const int nmain = (int)gridDim.x - a.stage.blocks;
+  if ((int)blockIdx.x >= nmain) {
+    stage_gather(a.stage, (int)blockIdx.x - nmain);
+    return;
+  }
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long nth = (long)gridDim.x * blockDim.x;
+  const long nth = (long)nmain * blockDim.x;
   const float lr = opt_step_lr(a.opt, a.lr, a.step);
   const long n4 = a.seg.start4[a.seg.count];
   float4* w4 = (float4*)a.w;
@@ -177,6 +206,39 @@ using namespace csa;
 // zero_grad != 0: the update clears g[i] after reading it (g is then an accumulator that
 // must start the next step at zero); zero_ptrs must NOT overlap g or the fold stripes.
 // met_parts > 0: write the metric ring from the head's partial loss / #correct.
+static BatchStage make_stage(const uint8_t* img, const int64_t* labels, const int64_t* rows, const int64_t* cursor,
+                             int B, long imsz, uint8_t* out_img, int64_t* out_lbl) {
+  BatchStage s{};
+  if (!out_img) return s;
+  s.img = reinterpret_cast<const uint32_t*>(img);
+  s.labels = labels; s.rows = rows; s.cursor = cursor; s.B = B; s.words = imsz / 4;
+  s.out_img = reinterpret_cast<uint32_t*>(out_img); s.out_lbl = out_lbl;
+  const long total = (long)B * s.words > B ? (long)B * s.words : B;
+  s.blocks = (int)((total + 255) / 256);
+  return s;
+}
+
+// Prime the staging buffers for the current cursor (before the first step, after the
+// host moved the cursor).  imsz % 4 == 0.
+CSA_API int csa_gather_batch(const uint8_t* img, const int64_t* labels, const int64_t* rows, const int64_t* cursor,
+                             int B, long imsz, uint8_t* out_img, int64_t* out_lbl, hipStream_t st) {
+  if (B <= 0 || imsz <= 0 || imsz % 4 || !out_img || !out_lbl) return -1;
+  const BatchStage s = make_stage(img, labels, rows, cursor, B, imsz, out_img, out_lbl);
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(s.blocks), dim3(256), 0, st, s);
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, long n, const long* seg_lo,
+                            const long* seg_hi, int nseg, int zero_grad, float lr, const int64_t* step,
+                            float* const* zero_ptrs, const long* zero_ns, int nzero, const long* fold_off,
+                            const long* fold_n, float* const* fold_src, const int* fold_S, const long* fold_ld,
+                            const int* fold_zero, int nfold, const long* keep_lo, const long* keep_hi, int nkeep,
+                            const float* met_loss, const int* met_corr, int met_parts, float met_div,
+                            float* ring_loss, int* ring_correct, int ring, int64_t* cursor, long cursor_wrap,
+                            const uint8_t* st_img, const int64_t* st_labels, const int64_t* st_rows,
+                            const int64_t* st_cursor, int st_B, long st_imsz, uint8_t* st_out_img,
+                            int64_t* st_out_lbl, hipStream_t st);
+
 CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, long n, const long* seg_lo,
                            const long* seg_hi, int nseg, int zero_grad, float lr, const int64_t* step,
                            float* const* zero_ptrs, const long* zero_ns, int nzero, const long* fold_off,
@@ -185,6 +247,25 @@ CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, lo
                            const float* met_loss, const int* met_corr, int met_parts, float met_div,
                            float* ring_loss, int* ring_correct, int ring, int64_t* cursor, long cursor_wrap,
                            hipStream_t st) {
+  return csa_optimizer2s(opt, w, g, s0, s1, n, seg_lo, seg_hi, nseg, zero_grad, lr, step, zero_ptrs, zero_ns, nzero,
+                         fold_off, fold_n, fold_src, fold_S, fold_ld, fold_zero, nfold, keep_lo, keep_hi, nkeep,
+                         met_loss, met_corr, met_parts, met_div, ring_loss, ring_correct, ring, cursor, cursor_wrap,
+                         nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, st);
+}
+
+// ... plus the next step's batch staging (st_out_img != null; the head advanced the
+// cursor, so pass cursor = null here).
+CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, long n, const long* seg_lo,
+                            const long* seg_hi, int nseg, int zero_grad, float lr, const int64_t* step,
+                            float* const* zero_ptrs, const long* zero_ns, int nzero, const long* fold_off,
+                            const long* fold_n, float* const* fold_src, const int* fold_S, const long* fold_ld,
+                            const int* fold_zero, int nfold, const long* keep_lo, const long* keep_hi, int nkeep,
+                            const float* met_loss, const int* met_corr, int met_parts, float met_div,
+                            float* ring_loss, int* ring_correct, int ring, int64_t* cursor, long cursor_wrap,
+                            const uint8_t* st_img, const int64_t* st_labels, const int64_t* st_rows,
+                            const int64_t* st_cursor, int st_B, long st_imsz, uint8_t* st_out_img,
+                            int64_t* st_out_lbl, hipStream_t st) {
+  if (st_out_img && (st_imsz % 4 || st_B <= 0)) return -1;
   if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG || met_parts > MAXS) return -1;
   OptArgs a{};
   a.keep.count = nkeep;
@@ -228,7 +309,8 @@ CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, lo
   int blocks = (int)((work + 255) / 256);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(optim_kernel, dim3(blocks), dim3(256), 0, st, a);
+  a.stage = make_stage(st_img, st_labels, st_rows, st_cursor, st_B, st_imsz, st_out_img, st_out_lbl);
+  hipLaunchKernelGGL(optim_kernel, dim3(blocks + a.stage.blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ class BatchStream:
         self._done_ev: List[Optional[torch.cuda.Event]] = [None, None]   # device finished half h
         self._filled = [False, False]
         self.refills = 0
+        self.on_reset = None
         self.seek(0)
 
     def _next_indices(self, count: int) -> np.ndarray:
@@ -93,6 +94,8 @@ class BatchStream:
         self._fill(1)
         self.cursor.zero_()
         self.half, self.used = 0, 0
+        if self.on_reset is not None:
+            self.on_reset()              # device-side consumers of the cursor (batch staging)
 
     def _fill(self, h: int) -> None:
         idx = self._next_indices(self.chunk * self.batch).reshape(self.chunk, self.batch)
@@ -122,7 +125,10 @@ class BatchStream:
         other = 1 - self.half
         if not self._filled[other]:
             ev = self._done_ev[other]
-            if ev is None or ev.query():
+            # the last step of a half already reads the next half's first row (the HIP
+            # program stages the NEXT step's batch at the end of each step): that half
+            # must be filled before this step is enqueued
+            if ev is None or ev.query() or self.used == self.chunk - 1:
                 self._refill_now(other)
         self.used += 1
 

@@ -50,6 +50,9 @@ _SIGS = {
     "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P, I, P, L, P]),
     "csa_optimizer2": (I, [I, P, P, P, P, L, P, P, I, I, F, P, P, P, I, P, P, P, P, P, P, I, P, P, I,
                            P, P, I, F, P, P, I, P, L, P]),
+    "csa_optimizer2s": (I, [I, P, P, P, P, L, P, P, I, I, F, P, P, P, I, P, P, P, P, P, P, I, P, P, I,
+                           P, P, I, F, P, P, I, P, L,
+                                P, P, P, P, I, L, P, P, P]),
     "csa_dense_bwd_update_ok": (I, [I, I, I, I]),
     "csa_dense_bwd_update_slabs": (I, [I]),
     "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
@@ -62,6 +65,8 @@ _SIGS = {
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
                               P, P, P, P, I, P]),
     "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),
+    "csa_head_part2": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P, L, P]),
+    "csa_gather_batch": (I, [P, P, P, P, I, L, P, P, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),

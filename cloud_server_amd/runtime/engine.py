@@ -128,6 +128,8 @@ class TrainEngine:
                 self.program = TorchProgram(self)
         else:
             self.program = TorchProgram(self)
+        # the program re-stages its batch whenever the host moves the cursor (seek/resume)
+        self.stream.on_reset = (lambda: self.program.prime()) if hasattr(self.program, "prime") else None
         if use_graph is None:
             use_graph = self.device.type == "cuda"
         self.use_graph = use_graph and self.device.type == "cuda"

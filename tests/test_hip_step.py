@@ -254,3 +254,25 @@ def test_conv_pair_fused_active(name):
     ds = synthetic_mnist(200, seed=3)
     eng = TrainEngine(_cfg(CASES[name]), ds, device="cuda", backend="hip", use_graph=False)
     assert eng.program.pair is not None
+
+
+def test_staged_batch_matches_cursor_path(monkeypatch):
+    """CSA_STAGE_BATCH=1: the next step's batch is staged by the optimizer and the cursor is
+    advanced by the head — identical training to the cursor-walking kernels, also across
+    a seek (checkpoint resume) and graph capture."""
+    ds = synthetic_mnist(700, seed=17)
+    cfg = _cfg(CASES["sample"], optimizer="AdagradOptimizer", lr=0.01)
+    outs = []
+    for staged in ("0", "1"):
+        monkeypatch.setenv("CSA_STAGE_BATCH", staged)
+        eng = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True, stream_chunk=4)
+        assert eng.program.staged == (staged == "1")
+        for _ in range(13):            # crosses several half boundaries of the row table
+            eng.step()
+        eng.stream.seek(5)             # resume-style cursor move: the program re-stages
+        for _ in range(6):
+            eng.step()
+        torch.cuda.synchronize()
+        outs.append((eng.flat.clone(), eng.metrics_since(0)))
+    assert (outs[0][0] - outs[1][0]).abs().max().item() < 3e-3
+    assert outs[0][1]["accuracy"] == outs[1][1]["accuracy"]
