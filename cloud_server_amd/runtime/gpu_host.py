@@ -65,7 +65,8 @@ def _take_inbox(spool: str) -> List[dict]:
     return out
 
 
-def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0.0) -> int:
+def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0.0,
+          parent_pid: int = 0) -> int:
     from .multijob import PackedJobs, prefer_packed_kernels
     from .trainer import JobRun
     prefer_packed_kernels()
@@ -73,6 +74,7 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
     jobs: Dict[int, JobRun] = {}
     pack = None
     idle_since = time.time()
+    parent = parent_pid or os.getppid()     # the manager's launcher; if it dies we are orphaned
 
     def retire(jid: int, rc: int) -> None:
         jobs.pop(jid, None)
@@ -97,6 +99,13 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
                 rc = _finish(job)
                 retire(jid, rc)
                 changed = True
+        if os.getppid() != parent:
+            # the manager is gone (killed without a clean shutdown): checkpoint and stop
+            # every hosted job rather than keep a GPU context nobody can control
+            for jid, job in list(jobs.items()):
+                job.state = "stopped"
+                retire(jid, _finish(job))
+            return 0
         if not jobs:
             pack = None
             if idle_exit_s and time.time() - idle_since > idle_exit_s:
@@ -147,10 +156,12 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--idle-exit", type=float, default=0.0,
                     help="exit after this many seconds without jobs (0: never)")
+    ap.add_argument("--parent-pid", type=int, default=0,
+                    help="the launcher's pid: the host stops its jobs and exits when it is gone")
     a = ap.parse_args(argv)
     os.makedirs(os.path.join(a.spool, "inbox"), exist_ok=True)
     os.makedirs(os.path.join(a.spool, "done"), exist_ok=True)
-    return serve(a.spool, a.device, a.backend, a.idle_exit)
+    return serve(a.spool, a.device, a.backend, a.idle_exit, a.parent_pid)
 
 
 if __name__ == "__main__":

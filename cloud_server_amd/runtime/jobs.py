@@ -351,7 +351,7 @@ class JobManager:
                 env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
                 argv = [sys.executable, "-m", "cloud_server_amd.runtime.gpu_host", "--spool", spool,
                         "--device", "cpu" if self.use_cpu else "cuda:0",
-                        "--backend", self.settings.train_backend]
+                        "--backend", self.settings.train_backend, "--parent-pid", str(self._launcher.pid)]
                 self._req.put(("launch", self._host_id(gpu), argv, env, spool, os.path.join(spool, "host.log")))
             h["jobs"].add(jid)
             info["host"] = gpu

@@ -115,3 +115,29 @@ def test_bench_jobs_flag_prints_aggregate_line():
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["metric"] == "train_samples_per_s" and d["config"]["jobs"] == 2
     assert d["config"]["global_batch"] == 16 and d["value"] > 0
+
+
+def test_gpu_host_exits_when_orphaned(tmp_path):
+    """A host whose parent (the manager's launcher) died stops its jobs and exits."""
+    spool = tmp_path / "spool"
+    code = ("import os, sys, subprocess, time\n"
+            f"p = subprocess.Popen([sys.executable, '-m', 'cloud_server_amd.runtime.gpu_host', '--spool', r'{spool}',"
+            " '--device', 'cpu', '--backend', 'torch', '--parent-pid', str(os.getpid())], cwd=r'" + ROOT + "',"
+            " stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL)\n"
+            "print(p.pid, flush=True)\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=ROOT)
+    pid = int(out.stdout.strip().splitlines()[-1])
+    t0 = time.time()
+    def alive():
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                return f.read().split(")")[-1].split()[0] != "Z"    # a zombie has exited
+        except OSError:
+            return False
+    while time.time() - t0 < 60:
+        if not alive():
+            break
+        time.sleep(0.2)
+    else:
+        os.kill(pid, 9)
+        raise AssertionError("orphaned gpu_host kept running")
