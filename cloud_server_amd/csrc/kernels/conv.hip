@@ -23,7 +23,7 @@ namespace csa {
 
 constexpr int CONV_THREADS = 256;
 
-__device__ long long* g_conv_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
+__constant__ long long* g_conv_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
 #define CONV_STAMP(i)                                                                       \
   do {                                                                                      \
     if (g_conv_dbg && threadIdx.x == 0 && blockIdx.x == 0)                                  \

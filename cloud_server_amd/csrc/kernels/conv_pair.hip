@@ -34,7 +34,7 @@ constexpr int CP_MAXC2 = 64;
 constexpr int CP_MAXC1 = 32;
 constexpr size_t CP_LDS_MAX = 150 * 1024;
 
-__device__ long long* g_cp_dbg = nullptr;   // diagnostics: s_memtime stamps of block 0
+__constant__ long long* g_cp_dbg = nullptr;   // diagnostics: s_memtime stamps of block 0
 #define CP_STAMP(i)                                                                           \
   do {                                                                                        \
     if (g_cp_dbg && threadIdx.x == 0 && blockIdx.x == 0) g_cp_dbg[i] = (long long)__builtin_amdgcn_s_memtime(); \
@@ -490,6 +490,11 @@ __host__ __device__ inline CPBwdLayout cp_bwd_layout(const CPGeom& g, int band, 
   return L;
 }
 
+// Prologue register batch of the backward (ONE = true): weights (panel A + dense wB),
+// x tile and BN slab rows per thread.  The host picks ONE when every band fits.
+constexpr int CPB_UP = 8, CPB_UX = 2, CPB_US = 8;
+
+template <bool ONE>
 __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float s_bn[4 * CP_MAXC2];
@@ -521,10 +526,61 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
   int* s_pix1d = s_pix1x + L.kp1;                            //      pixel -> dc1 offset
   int* s_tapB = s_pix1d + L.kp1;                             // dwB: tap -> c1 tile offset
   CP_STAMP(8);
-  const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
-  cp_stage_x(g, t, src, s_x);
-  cp_stage_panel(s_pA, a.wA, L.KA, g.C1, L.kpadA, 16);
-  cp_stage_flat(s_wB, a.wB, L.KB * g.C2, L.kpadB * L.c16);
+  // Prologue.  ONE: every global load of the prologue — the two weight blocks, the x tile,
+  // both BN slabs and the BN affine vectors — is issued first, the index tables below are
+  // computed while they travel (VALU work that otherwise sat between dependent round
+  // trips), then the LDS stores and the slab reduction.
+  const int nA = L.kpadA * 16, nWB = L.KB * g.C2, nP = nA + L.kpadB * L.c16;
+  const int nX = t.TXH * t.TXW * g.C0;
+  const int C2x2 = 2 * g.C2, sper = CP_THREADS / C2x2;
+  const int scol = (int)threadIdx.x % C2x2, srow = (int)threadIdx.x / C2x2;
+  const bool sact = srow < sper;
+  float pv[CPB_UP], vf[CPB_US], vb[CPB_US], sc = 0.f, of = 0.f;
+  bool pok[CPB_UP], xok[CPB_UX];
+  uint8_t xv[CPB_UX];
+  if (ONE) {
+    if (a.bn_on) for (int i = threadIdx.x; i < C2x2; i += CP_THREADS) { s_red[i] = 0.f; s_ss[i] = 0.f; }
+#pragma unroll
+    for (int u = 0; u < CPB_UP; ++u) {             // [panel A (padded to 16 cols) | wB dense]
+      const int e = u * CP_THREADS + (int)threadIdx.x;
+      const bool inA = e < nA;
+      const int k = e >> 4, n = e & 15, f = e - nA;
+      const bool ok = inA ? (k < L.KA && n < g.C1) : (e < nP && f < nWB);
+      pok[u] = ok;
+      const float* p = !ok ? a.wA : (inA ? a.wA + k * g.C1 + n : a.wB + f);
+      pv[u] = *p;
+    }
+    if (a.bn_on) {
+      const int cc = (int)threadIdx.x < g.C2 ? (int)threadIdx.x : g.C2 - 1;
+#pragma unroll
+      for (int u = 0; u < CPB_US; ++u) {
+        const int r = srow + u * sper;
+        vf[u] = a.bn.slab[(size_t)(sact && r < a.bn.nslab ? r : 0) * C2x2 + scol];
+        vb[u] = a.bwd_slab[(size_t)(sact && r < a.bwd_nslab ? r : 0) * C2x2 + scol];
+      }
+      sc = a.bn.scale[cc];
+      of = a.bn.offset[cc];
+    }
+    const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
+    const int y0 = t.c1y0 - g.PTA, x0 = -g.PLB - g.PLA;
+    const FastDiv dw(t.TXW * g.C0), dc(g.C0);
+#pragma unroll
+    for (int u = 0; u < CPB_UX; ++u) {
+      const int e = u * CP_THREADS + (int)threadIdx.x;
+      int r, rem, xx, c;
+      dw.divmod(e < nX ? e : 0, r, rem);
+      dc.divmod(rem, xx, c);
+      const int y = y0 + r, x = x0 + xx;
+      xok[u] = e < nX && y >= 0 && y < g.H && x >= 0 && x < g.W;
+      xv[u] = src[xok[u] ? ((long)y * g.W + x) * g.C0 + c : 0];
+    }
+  } else {
+    const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
+    cp_stage_x(g, t, src, s_x);
+    cp_stage_panel(s_pA, a.wA, L.KA, g.C1, L.kpadA, 16);
+    cp_stage_flat(s_wB, a.wB, L.KB * g.C2, L.kpadB * L.c16);
+  }
+  CP_STAMP(16);
   for (int i = threadIdx.x; i < L.D2H * L.D2W * g.C2; i += CP_THREADS) s_dc2[i] = 0.f;
   for (int i = threadIdx.x; i < g.C1; i += CP_THREADS) s_dc1[L.npix1 * g.C1 + i] = 0.f;
   cp_tables_a(g, t, L.kpadA, s_offA, s_offPA);
@@ -565,12 +621,60 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
       s_tapB[k] = o;
     }
   }
+  CP_STAMP(17);
+  if (ONE) {
+#pragma unroll
+    for (int u = 0; u < CPB_UP; ++u) pin(pv[u]);
+#pragma unroll
+    for (int u = 0; u < CPB_UP; ++u) {
+      const int e = u * CP_THREADS + (int)threadIdx.x;
+      if (e < nA) s_pA[e] = pok[u] ? pv[u] : 0.f;
+      else if (e < nP) s_wB[e - nA] = pok[u] ? pv[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < CPB_UX; ++u) {
+      const int e = u * CP_THREADS + (int)threadIdx.x;
+      if (e < nX) s_x[e] = xok[u] ? (float)xv[u] * (1.0f / 255.0f) : 0.f;
+    }
+  }
+  CP_STAMP(18);
   // BatchNorm tables of the unit output and the backward sums (every block reduces the
   // small slabs; block 0 writes the BN parameter gradients and running statistics)
+  CP_STAMP(19);
   if (a.bn_on) {
-    bn_reduce_to_lds(a.bn, s_bn, s_bn + CP_MAXC2, s_bn + 2 * CP_MAXC2, s_bn + 3 * CP_MAXC2, s_ss);
-    __syncthreads();
-    slab_sum_to_lds(a.bwd_slab, a.bwd_nslab, 2 * g.C2, s_ss);
+    if (ONE) {
+#pragma unroll
+      for (int u = 0; u < CPB_US; ++u) { pin(vf[u]); pin(vb[u]); }
+      float af = 0.f, ab = 0.f;
+#pragma unroll
+      for (int u = 0; u < CPB_US; ++u) {
+        const int r = srow + u * sper;
+        af += r < a.bn.nslab ? vf[u] : 0.f;
+        ab += r < a.bwd_nslab ? vb[u] : 0.f;
+      }
+      __syncthreads();                             // the zeroing of s_red / s_ss
+      if (sact) {
+        atomicAdd(&s_red[scol], af);
+        atomicAdd(&s_ss[scol], ab);
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < g.C2) {
+        const int c = threadIdx.x;
+        const float mean = s_red[c] / a.bn.count;
+        const float var = fmaxf(s_red[g.C2 + c] / a.bn.count - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + a.bn.eps);
+        const float aa = sc * rstd;
+        s_bn[c] = mean;
+        s_bn[CP_MAXC2 + c] = rstd;
+        s_bn[2 * CP_MAXC2 + c] = aa;
+        s_bn[3 * CP_MAXC2 + c] = of - mean * aa;
+      }
+      __syncthreads();
+    } else {
+      bn_reduce_to_lds(a.bn, s_bn, s_bn + CP_MAXC2, s_bn + 2 * CP_MAXC2, s_bn + 3 * CP_MAXC2, s_ss);
+      __syncthreads();
+      slab_sum_to_lds(a.bwd_slab, a.bwd_nslab, 2 * g.C2, s_ss);
+    }
     if (blockIdx.x == 0)
       for (int c = threadIdx.x; c < g.C2; c += CP_THREADS) {
         a.doffset[c] = s_ss[c];
@@ -749,6 +853,26 @@ static bool cp_geom(const int* v, CPGeom& g) {
   return true;
 }
 
+// Does every band's backward prologue fit the one-batch register budget?
+static bool cp_bwd_one_batch(const CPBwdArgs& a) {
+  if (getenv("CSA_CP_BWD_STAGED")) return false;
+  const CPGeom& g = a.g;
+  const int C2x2 = 2 * g.C2, per = CP_THREADS / C2x2;
+  if (a.bn_on && (per == 0 || a.bn.nslab > CPB_US * per || a.bwd_nslab > CPB_US * per)) return false;
+  for (int band = 0; band < g.nbands; ++band) {
+    const int pr0 = band * g.PR, pr1 = std::min(g.PH, pr0 + g.PR);
+    const bool last = band == g.nbands - 1;
+    const int r2a = g.pool ? 2 * pr0 : pr0, r2b = g.pool ? (last ? g.H2 : 2 * pr1) : pr1;
+    const int T1H = (r2b - r2a) + g.KBh - 1, T1W = g.W2 + g.KBw - 1;
+    const int TXH = T1H + g.KAh - 1, TXW = T1W + g.KAw - 1;
+    const CPBwdLayout L = cp_bwd_layout(g, band, TXH, TXW, T1H, T1W);
+    if (L.kpadA * 16 + L.kpadB * L.c16 > CPB_UP * CP_THREADS || TXH * TXW * g.C0 > CPB_UX * CP_THREADS ||
+        g.C1 > 16)
+      return false;
+  }
+  return true;
+}
+
 static size_t cp_lds(const CPGeom& g, bool bwd) {
   size_t mx = 0;
   for (int band = 0; band < g.nbands; ++band) {
@@ -821,10 +945,15 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
   a.bn_on = bn_slab != nullptr; a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab;
   a.dscale = dscale; a.doffset = doffset; a.run_mean = run_mean; a.run_var = run_var; a.momentum = momentum;
   a.dwA = dwA; a.dbA = dbA; a.dwB = dwB; a.dbB = dbB; a.stripes = stripes < 1 ? 1 : stripes;
-  static bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)CP_LDS_MAX) == hipSuccess;
+  static bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_kernel<true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess &&
+                     hipFuncSetAttribute((const void*)conv_pair_bwd_kernel<false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
-  hipLaunchKernelGGL(conv_pair_bwd_kernel, dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CP_THREADS),
-                     cp_lds(a.g, true), st, a);
+  const dim3 grid((unsigned)(a.g.B * a.g.nbands));
+  if (cp_bwd_one_batch(a))
+    hipLaunchKernelGGL(conv_pair_bwd_kernel<true>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
+  else
+    hipLaunchKernelGGL(conv_pair_bwd_kernel<false>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
   return (int)hipGetLastError();
 }

@@ -39,7 +39,7 @@ constexpr int DD_U = 4;               // 8-k blocks whose loads are in flight to
 
 // diagnostics: block-0 phase stamps [0..3] + the earliest block start [4] and the latest
 // block end [5] of a launch (s_memtime ticks); null disables
-__device__ long long* g_dd_dbg = nullptr;
+__constant__ long long* g_dd_dbg = nullptr;
 #define DD_STAMP(i)                                                                           \
   do {                                                                                        \
     if (g_dd_dbg && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) \

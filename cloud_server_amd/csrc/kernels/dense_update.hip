@@ -62,7 +62,7 @@ struct DUArgs {
   int dbg;                  // diagnostics (CSA_DU_DBG bits): 1 no wgrad, 2 no dgrad, 4 no update, 8 no loads
 };
 
-__device__ long long* g_du_dbg = nullptr;   // diagnostics: s_memtime stamps of block 0
+__constant__ long long* g_du_dbg = nullptr;   // diagnostics: s_memtime stamps of block 0
 #define DU_STAMP(i)                                                                          \
   do {                                                                                       \
     if (g_du_dbg && threadIdx.x == 0 && blockIdx.x == 0) g_du_dbg[i] = (long long)__builtin_amdgcn_s_memtime(); \

@@ -237,7 +237,7 @@ struct Stage {
 // The kernel.  Grid: x = N tiles, y = M tiles, z = split-K slices.
 // WG tile = (32*WM) x (32*WN); its K slice is split WK ways across the waves.
 // ----------------------------------------------------------------------------------
-__device__ long long* g_gemm_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
+__constant__ long long* g_gemm_dbg = nullptr;   // diagnostics: s_memtime stamps of WG 0
 #define GEMM_STAMP(i)                                                                       \
   do {                                                                                      \
     if (g_gemm_dbg && threadIdx.x == 0 && tid.x == 0 && tid.y == 0 && tid.z == 0)              \

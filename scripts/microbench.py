@@ -97,7 +97,7 @@ def main() -> int:
                 print(f"{i:2d} {name:18s} stamps (s_memtime ticks): prologue {t[1]-t[0]} chunks {t[2]-t[1]} "
                       f"dgrad-epilogue {t[3]-t[2]}")
     if os.environ.get("MB_CP"):
-        dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+        dbg = torch.zeros(24, dtype=torch.int64, device="cuda")
         for i, (name, fn, args) in enumerate(rec.calls):
             if name.startswith("csa_conv_pair_"):
                 for _ in range(3):
@@ -111,7 +111,8 @@ def main() -> int:
                     print(f"{i:2d} {name}: stage {t[1]-t[0]} (image {t[5]-t[0]} panels {t[6]-t[5]} tables {t[1]-t[6]}) "
                           f"convA {t[2]-t[1]} convB+pool {t[3]-t[2]} stats {t[4]-t[3]}")
                 else:
-                    print(f"{i:2d} {name}: stage+bn {t[9]-t[8]} route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} "
+                    print(f"{i:2d} {name}: stage+bn {t[9]-t[8]} (loads {t[16]-t[8]} tables {t[17]-t[16]} "
+                          f"stores {t[18]-t[17]} bn {t[9]-t[19]}) route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} "
                           f"dc1 {t[13]-t[12]} dwA {t[14]-t[13]} atomics {t[15]-t[14]}")
     if os.environ.get("MB_DD"):
         dbg = torch.zeros(16, dtype=torch.int64, device="cuda")

@@ -261,7 +261,10 @@ def test_staged_batch_matches_cursor_path(monkeypatch):
     advanced by the head — identical training to the cursor-walking kernels, also across
     a seek (checkpoint resume) and graph capture."""
     ds = synthetic_mnist(700, seed=17)
-    cfg = _cfg(CASES["sample"], optimizer="AdagradOptimizer", lr=0.01)
+    # plain GD: parameter differences stay proportional to the gradients' atomic-order
+    # noise (Adagrad's first steps move every weight by ~lr whatever its gradient's size,
+    # so a near-zero gradient's rounding can flip a whole step)
+    cfg = _cfg(CASES["sample"], optimizer="GradientDescentOptimizer", lr=0.001)
     outs = []
     for staged in ("0", "1"):
         monkeypatch.setenv("CSA_STAGE_BATCH", staged)
@@ -274,5 +277,6 @@ def test_staged_batch_matches_cursor_path(monkeypatch):
             eng.step()
         torch.cuda.synchronize()
         outs.append((eng.flat.clone(), eng.metrics_since(0)))
-    assert (outs[0][0] - outs[1][0]).abs().max().item() < 3e-3
+    assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-3
     assert outs[0][1]["accuracy"] == outs[1][1]["accuracy"]
+    assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) < 1e-4 * max(1.0, abs(outs[0][1]["loss"]))
