@@ -179,15 +179,17 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) dd_pin(bw[u][s]);
     }
+    // the group's transform first (all table reads of the group issued together, then
+    // the activation), the MFMA chain after it: a table read -> MFMA pairing left every
+    // MFMA waiting on its own LDS round trip
+    float ta_[DD_U][4], tb_[DD_U][4];
 #pragma unroll
     for (int u = 0; u < DD_U; ++u) {
       const int kk0 = k + 8 * u + 4 * h;
       int q_, c = 0;
       if (BN) dC.divmod(min(kk0, a.K - 1), q_, c);
-      float ta[4], tb[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int kk = kk0 + s;
         float xa_s = dd_c(pa[u], s), xb_s = dd_c(pb[u], s);
         if (BN) {
           const float sa = s_bn[2 * DD_MAXC + c], sb = s_bn[3 * DD_MAXC + c];
@@ -195,12 +197,30 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
           xb_s = xb_s * sa + sb;
           c = c + 1 == a.bn.C ? 0 : c + 1;
         }
-        if (a.act != ACT_NONE) { xa_s = act_fwd(xa_s, a.act, a.alpha); xb_s = act_fwd(xb_s, a.act, a.alpha); }
-        ta[s] = xa_s;
-        tb[s] = xb_s;
+        ta_[u][s] = xa_s;
+        tb_[u][s] = xb_s;
+      }
+    }
+    if (a.act != ACT_NONE) {
+#pragma unroll
+      for (int u = 0; u < DD_U; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          ta_[u][s] = act_fwd(ta_[u][s], a.act, a.alpha);
+          tb_[u][s] = act_fwd(tb_[u][s], a.act, a.alpha);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < DD_U; ++u) {
+      const int kk0 = k + 8 * u + 4 * h;
+      float* ta = ta_[u];
+      float* tb = tb_[u];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int kk = kk0 + s;
         const float b = kk < kb ? bw[u][s] : 0.f;     // outside this wave's range: no term
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa_s * vA, b, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xb_s * vB, b, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[s] * vA, b, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(tb[s] * vB, b, acc1, 0, 0, 0);
       }
       // xt: 8-k block j is written by the N-tile j % ntiles (writes spread over the
       // workgroups that loaded it anyway); kept in registers and stored after the K loop,
