@@ -482,6 +482,13 @@ __global__ __launch_bounds__(RT) void head_cols_kernel(HeadArgs a) {
 // The row-group kernel above spent most of its 14.5 µs in ~20k same-line dWh atomics and
 // a last-arriver hand-off.
 // ---------------------------------------------------------------------------------
+// diagnostics: s_memtime stamps of workgroup 0 (null disables; csa_head_debug)
+__constant__ long long* g_head_dbg = nullptr;
+#define HEAD_STAMP(i)                                                                         \
+  do {                                                                                        \
+    if (g_head_dbg && threadIdx.x == 0 && blockIdx.x == 0) g_head_dbg[i] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
 constexpr int PRG_MAX = 16;        // rows per workgroup
 constexpr size_t PHEAD_LDS_MAX = 150 * 1024;
 
@@ -516,6 +523,10 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
   float* s_w = s_h + RG * K;               // [K][10]
   float* s_lg = s_w + K * NCLS;            // [PRG_MAX][10] logits
   float* s_dl = s_lg + PRG_MAX * NCLS;     // [PRG_MAX][10] dlogits
+  HEAD_STAMP(0);
+  float bias[NCLS];                // read first: consumed after the logits
+#pragma unroll
+  for (int j = 0; j < NCLS; ++j) bias[j] = a.b[j];
   if (g == 0 && tid == 0) {
     *a.step += 1;
     if (a.adv_cursor) {          // the step's batch is staged: its kernels no longer read the cursor
@@ -552,6 +563,7 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
       }
     }
   }
+  HEAD_STAMP(1);
   // the label chain (cursor -> row index -> label) is only needed after the logits: it is
   // issued after the staging loads so its two dependent round trips overlap them
   int label = 0;
@@ -562,29 +574,42 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
     if (tid < rows) label = (int)a.labels[idx[m0 + tid]];
   }
   __syncthreads();
-  // logits: wave w takes rows w, w+4, ...; lanes split K, then a wave reduction per class
+  HEAD_STAMP(2);
+  // logits: wave w takes rows w, w+4, ...; lane l owns k = 4l + 256i (one float4 of h and
+  // the 40 contiguous weights of those 4 k as ten float4 LDS reads), then a DPP wave
+  // reduction per class
   for (int r = wave; r < rows; r += 4) {
     float acc[NCLS];
 #pragma unroll
     for (int j = 0; j < NCLS; ++j) acc[j] = 0.f;
-    for (int k = lane; k < K; k += 64) {
-      const float hv = s_h[r * K + k];
-      const float* wr = s_w + k * NCLS;
+    for (int k4 = lane * 4; k4 < K; k4 += 256) {
+      const float4 hv = *reinterpret_cast<const float4*>(s_h + r * K + k4);
+      const float4* wr = reinterpret_cast<const float4*>(s_w + k4 * NCLS);
+      float wv[4 * NCLS];
 #pragma unroll
-      for (int j = 0; j < NCLS; ++j) acc[j] = fmaf(hv, wr[j], acc[j]);
+      for (int q = 0; q < NCLS; ++q) {
+        const float4 t = wr[q];
+        wv[4 * q] = t.x; wv[4 * q + 1] = t.y; wv[4 * q + 2] = t.z; wv[4 * q + 3] = t.w;
+      }
+      const float hs[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int j = 0; j < NCLS; ++j) acc[j] = fmaf(hs[s2], wv[s2 * NCLS + j], acc[j]);
     }
 #pragma unroll
     for (int j = 0; j < NCLS; ++j) {
-      const float t = wave_sum(acc[j]);
+      const float t = wave_sum_dpp(acc[j]);
       if (lane == 0) s_lg[r * NCLS + j] = t;
     }
   }
   __syncthreads();
+  HEAD_STAMP(3);
   // loss / dlogits / correct: one thread per row
   if (tid < rows) {
     float row[NCLS];
 #pragma unroll
-    for (int j = 0; j < NCLS; ++j) row[j] = s_lg[tid * NCLS + j] + a.b[j];
+    for (int j = 0; j < NCLS; ++j) row[j] = s_lg[tid * NCLS + j] + bias[j];
     float mx = row[0];
     int am = 0;
 #pragma unroll
@@ -624,6 +649,7 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
     a.mpart[g] = ls;
     a.mcorr[g] = nc;
   }
+  HEAD_STAMP(4);
   float* prow = a.part + (long)g * (K * NCLS + NCLS);
   if (tid < NCLS) {            // dbh partial
     float acc = 0.f;
@@ -649,9 +675,11 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
         a.dh[(long)(m0 + r) * K + k] = gv;
       }
     }
+    float2* p2 = reinterpret_cast<float2*>(prow + k * NCLS);    // part rows: 8 B aligned
 #pragma unroll
-    for (int j = 0; j < NCLS; ++j) prow[k * NCLS + j] = dw[j];
+    for (int j = 0; j < NCLS / 2; ++j) p2[j] = make_float2(dw[2 * j], dw[2 * j + 1]);
   }
+  HEAD_STAMP(5);
 }
 
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.
@@ -709,6 +737,10 @@ using namespace csa;
 
 // Rows per workgroup of the partial-output head (0: shape outside its family: more than
 // 16 groups of <= 16 rows, K % 4, or the LDS budget).
+CSA_API int csa_head_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_head_dbg), &p, sizeof(p));
+}
+
 CSA_API int csa_head_part_rows(int M, int K) {
   if (M < 1 || K < 4 || K % 4) return 0;
   int rg = 4;

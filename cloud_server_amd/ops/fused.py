@@ -61,6 +61,7 @@ _SIGS = {
     "csa_du_debug": (I, [P]),
     "csa_conv_pair_ok": (I, [P]),
     "csa_cp_debug": (I, [P]),
+    "csa_head_debug": (I, [P]),
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P]),
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
                               P, P, P, P, I, P]),

@@ -625,14 +625,15 @@ class HipProgram:
         cursor -> row index -> image chain.  ``prime()`` fills them for the current cursor
         whenever the host moved it (construction, warm-up restore, seek).
 
-        Opt-in (``CSA_STAGE_BATCH=1``): measured 119.3 vs 119.5 µs per graph step — the
-        conv pair's start-up phase is bound by 700 workgroups reading the same weight
-        panel at once (L2 channel hot spot, ~2.6 µs), not by the row-index chain."""
+        Default on (``CSA_STAGE_BATCH=0`` turns it off): 3 alternating bench pairs on
+        MI355X, 0.1169 vs 0.1175 ms/step (scripts/ab_env.sh) — small, because the conv
+        pair's start-up phase is mostly bound by 700 workgroups reading the same weights
+        at once, but consistent."""
         e = self.e
         img = e.data.images
         imsz = img[0].numel() if img.dim() > 1 else 0
         self.staged = (self.pair is not None and bool(self.head_rg) and img.dtype == torch.uint8
-                       and imsz % 4 == 0 and os.environ.get("CSA_STAGE_BATCH", "0") == "1")
+                       and imsz % 4 == 0 and os.environ.get("CSA_STAGE_BATCH", "1") == "1")
         self.stage_img = self.stage_lbl = None
         if self.staged:
             self.stage_img = torch.zeros(self.B, imsz, dtype=torch.uint8, device=e.device)

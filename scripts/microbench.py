@@ -128,6 +128,19 @@ def main() -> int:
                 t = dbg.tolist()
                 print(f"{i:2d} {name}: block0 loop {t[1]-t[0]} reduce {t[2]-t[1]} epilogue {t[3]-t[2]} "
                       f"| block0 total {t[3]-t[0]} | all blocks span {t[5]-t[4]}  first start->b0 start {t[0]-t[4]}")
+    if os.environ.get("MB_HEAD"):
+        dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name.startswith("csa_head_part"):
+                for _ in range(3):
+                    dbg.zero_()
+                    eng.program.lib.csa_head_debug(dbg.data_ptr())
+                    fn(*args)
+                    torch.cuda.synchronize()
+                    eng.program.lib.csa_head_debug(None)
+                t = dbg.tolist()
+                print(f"{i:2d} {name}: stage {t[1]-t[0]} labels+sync {t[2]-t[1]} logits {t[3]-t[2]} "
+                      f"loss {t[4]-t[3]} dW/dh {t[5]-t[4]} | total {t[5]-t[0]}")
     for i, (name, fn, args) in enumerate(rec.calls):
         for _ in range(5):
             fn(*args)
