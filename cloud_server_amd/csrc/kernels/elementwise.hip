@@ -12,6 +12,7 @@ namespace csa {
 
 struct ApplyArgs {
   const float* x; float* y; long n; int C; BNRef bn; int act; float alpha;
+  float* tab;   // optional [4][C] mean | rstd | a | b for later consumers (block 0 writes)
 };
 
 __global__ __launch_bounds__(256) void bn_act_apply_kernel(ApplyArgs a) {
@@ -23,6 +24,8 @@ __global__ __launch_bounds__(256) void bn_act_apply_kernel(ApplyArgs a) {
   if (i4 < n4) v = reinterpret_cast<const float4*>(a.x)[i4];
   bn_reduce_to_lds(a.bn, s_bn, s_bn + 128, s_bn + 256, s_bn + 384, s_bn + 512);
   __syncthreads();
+  if (a.tab && blockIdx.x == 0)
+    for (int c = threadIdx.x; c < 4 * a.C; c += blockDim.x) a.tab[c] = s_bn[(c / a.C) * 128 + c % a.C];
   if (i4 >= n4) return;
   const FastDiv dc(a.C);
   int q, c0;
@@ -44,9 +47,9 @@ using namespace csa;
 // n % 4 == 0; channel of element e is e % C (NHWC flattened).
 CSA_API int csa_bn_act_apply(const float* x, float* y, long n, int C, const float* bn_slab,
                              int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                             const float* bn_offset, int act, float alpha, hipStream_t st) {
+                             const float* bn_offset, int act, float alpha, float* tab, hipStream_t st) {
   if (n % 4 || C > 128 || C <= 0) return -1;
-  ApplyArgs a{x, y, n, C, BNRef{bn_slab, bn_nslab, C, bn_count, bn_eps, bn_scale, bn_offset}, act, alpha};
+  ApplyArgs a{x, y, n, C, BNRef{bn_slab, bn_nslab, C, bn_count, bn_eps, bn_scale, bn_offset}, act, alpha, tab};
   const long n4 = n / 4;
   hipLaunchKernelGGL(bn_act_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
   return (int)hipGetLastError();

@@ -56,7 +56,7 @@ _SIGS = {
     "csa_dense_bwd_update_ok": (I, [I, I, I, I]),
     "csa_dense_bwd_update_slabs": (I, [I]),
     "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
-                                 P, P, P, P, F, P]),
+                                 P, P, P, P, F, P, P]),
     "csa_head_part_rows": (I, [I, I]),
     "csa_du_debug": (I, [P]),
     "csa_conv_pair_ok": (I, [P]),
@@ -71,7 +71,7 @@ _SIGS = {
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),
-    "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P]),
+    "csa_bn_act_apply": (I, [P, P, L, I, P, I, F, F, P, P, I, F, P, P]),
     # register-direct MFMA dense kernels (dense_direct.hip)
     "csa_dd_debug": (I, [P]),
     "csa_dd_fwd_splits": (I, [I, I, I]),

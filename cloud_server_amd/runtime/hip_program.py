@@ -273,10 +273,11 @@ class HipProgram:
         must be all-reduced before any update."""
         e, B = self.e, self.B
         self.fused = (not e.ctx.enabled) and os.environ.get("CSA_FUSED_UPDATE", "1") == "1"
-        # measured on MI355X (profiles/r2_dense_fused.md): at one workgroup per CU the fused
-        # dense kernel's serial chunk chain (18 / 23 us for fc2 / fc1) loses to the
-        # split-K backward pair + flat optimizer, so the dense half is opt-in for now
-        fuse_dense = self.fused and os.environ.get("CSA_FUSED_DENSE", "0") == "1"
+        # measured on MI355X (profiles/r2_dense_fused.md): the row-group kernel (one
+        # 1024-thread workgroup per 16 input features) replaces fc1's split-K pair + its
+        # share of the flat optimizer (bench 0.1166 -> 0.1107 ms/step); CSA_FUSED_DENSE=0
+        # restores the separate kernels
+        fuse_dense = self.fused and os.environ.get("CSA_FUSED_DENSE", "1") == "1"
         for u in self.units:
             u.fused = False
             if not fuse_dense or u.kind != "dense":
@@ -288,7 +289,12 @@ class HipProgram:
             if tf.act is not None and not tf.has_bn:
                 continue                         # weight-gradient operand would need the act
             C = tf.norm.in_shape.c if tf.has_bn else 0
-            u.fused = bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C))
+            # one workgroup per 16 input features: a narrow layer (fc2: 32 workgroups)
+            # leaves the chip idle and is faster on the split-K pair + flat optimizer
+            # (profiles/r2_dense_fused.md)
+            groups = (fin + 15) // 16
+            u.fused = (bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C))
+                       and groups >= int(os.environ.get("CSA_FUSED_DENSE_MIN_GROUPS", "128")))
         self.head_rg = 0
         if self.fused and self.head_tf.norm is None:
             last = self.units[-1]
@@ -307,12 +313,14 @@ class HipProgram:
         direct = mode in ("1", "fwd") and not (e.ctx.enabled and e.sync.strategy == "lowrank")
         for u in self.units:
             u.direct = u.direct_bwd = u.direct_update = False
-            if u.kind != "dense" or u.fused or not direct:
+            if u.kind != "dense" or not direct:
                 continue
             fin = u.layer.in_shape.numel
             if u.in_tf.has_bn and fin % 4:
                 continue                         # BN'd input not materialised: LDS-staged GEMM
             u.direct = True
+            if u.fused:
+                continue                         # backward + update: csa_dense_bwd_update
             u.direct_bwd = mode == "1"
             u.direct_update = bool(u.direct_bwd and self.fused and self.head_rg)
 
@@ -512,6 +520,12 @@ class HipProgram:
             u.xt = None
             if u.kind == "dense" and u.in_tf.has_bn and u.layer.in_shape.numel % 4 == 0:
                 u.xt = torch.zeros(B, u.layer.in_shape.numel, **f32)
+            # BatchNorm tables [mean | rstd | a | b][C] written once per step by the
+            # bn_act_apply that materialises xt (the fused dense backward's epilogue reads
+            # them instead of reducing the statistic slab again)
+            u.in_tf.bn_tab = (torch.zeros(4, u.in_tf.slab.shape[2], **f32)
+                              if u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") != "1"
+                              else None)
         self.dlast = self.units[-1].dy     # head input grad
         self.idx = None
         if self.head_rg:
@@ -927,7 +941,8 @@ class HipProgram:
                     continue
                 if u.xt is not None:
                     self._rc(lib.csa_bn_act_apply(
-                        K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha, st),
+                        K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha,
+                        K.ptr(getattr(tf, "bn_tab", None)), st),
                         "bn_act_apply")
                 if u.direct:
                     xin = u.xt if u.xt is not None else u.x.view(B, -1)
@@ -1203,7 +1218,7 @@ class HipProgram:
             K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
             K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
             K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
-            1.0, st), "dense_bwd_update")
+            1.0, K.ptr(getattr(tf, "bn_tab", None)), st), "dense_bwd_update")
 
     def _opt_segments(self):
         """Flat [lo, hi) spans the optimizer launch updates: everything except the

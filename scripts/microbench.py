@@ -31,7 +31,7 @@ class Recorder:
 
     def __getattr__(self, name):
         fn = getattr(self.lib, name)
-        if not name.startswith("csa_") or name.endswith(("_splits", "_slabs", "_nslab")):
+        if not name.startswith("csa_") or name.endswith(("_splits", "_slabs", "_nslab", "_ws", "_ok", "_rows")):
             return fn
 
         def wrapped(*args):
@@ -84,18 +84,30 @@ def main() -> int:
                 t = dbg.tolist()
                 print(f"{i:2d} {name:18s} conv stamps:", [t[j + 1] - t[j] for j in range(7)])
     if os.environ.get("MB_DU"):
-        dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+        # per-block stamps (100 MHz realtime): start, loads landed, ticket drawn, finisher end
         for i, (name, fn, args) in enumerate(rec.calls):
             if name == "csa_dense_bwd_update":
+                grid = 4096
+                dbg = torch.zeros(grid * 8, dtype=torch.int64, device="cuda")
                 for _ in range(3):
                     dbg.zero_()
                     eng.program.lib.csa_du_debug(dbg.data_ptr())
                     fn(*args)
                     torch.cuda.synchronize()
                     eng.program.lib.csa_du_debug(None)
-                t = dbg.tolist()
-                print(f"{i:2d} {name:18s} stamps (s_memtime ticks): prologue {t[1]-t[0]} chunks {t[2]-t[1]} "
-                      f"dgrad-epilogue {t[3]-t[2]}")
+                t = dbg.view(-1, 8)
+                t = t[t[:, 0] > 0].double()
+                t0 = t[:, 0].min()
+                names = ["stage", "W landed", "mfma+update", "fold", "epilogue", "slab atomics"]
+                parts = []
+                for k in range(6):
+                    ok = (t[:, k + 1] > 0) & (t[:, k] > 0)
+                    d = (t[ok, k + 1] - t[ok, k]) / 100
+                    if len(d):
+                        parts.append(f"{names[k]} {d.mean():.2f}/{d.max():.2f}")
+                end = (t.max() - t0) / 100
+                print(f"{i:2d} {name}: blocks {len(t)} span {end:.2f} us | start spread "
+                      f"{(t[:, 0].max() - t0) / 100:.2f} | " + " | ".join(parts) + " (mean/max us)")
     if os.environ.get("MB_CP"):
         dbg = torch.zeros(24, dtype=torch.int64, device="cuda")
         for i, (name, fn, args) in enumerate(rec.calls):

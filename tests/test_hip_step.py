@@ -230,6 +230,7 @@ def test_fused_update_path_active_and_matches_unfused(monkeypatch):
         cfg = _cfg(CASES["sample"], optimizer=opt, lr=1e-3)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "1")
         monkeypatch.setenv("CSA_FUSED_DENSE", "1")
+        monkeypatch.setenv("CSA_FUSED_DENSE_MIN_GROUPS", "1")     # fc2 (32 row groups) too
         a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "0")
         b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
@@ -278,5 +279,6 @@ def test_staged_batch_matches_cursor_path(monkeypatch):
         torch.cuda.synchronize()
         outs.append((eng.flat.clone(), eng.metrics_since(0)))
     assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-3
-    assert outs[0][1]["accuracy"] == outs[1][1]["accuracy"]
+    # the statistic atomics' order may flip a borderline sample or two of the 19 x 50
+    assert abs(outs[0][1]["accuracy"] - outs[1][1]["accuracy"]) <= 3 / (19 * 50) + 1e-9
     assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) < 1e-4 * max(1.0, abs(outs[0][1]["loss"]))
