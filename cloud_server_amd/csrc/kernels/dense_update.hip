@@ -85,7 +85,7 @@ __constant__ long long* g_du_dbg = nullptr;
 __host__ __device__ inline int du_sn(int N) { return N + 4; }            // dY LDS row stride
 __host__ __device__ inline int du_tiles(int M) { return (M + 15) / 16; } // batch tiles of 16
 __host__ __device__ inline size_t du_lds_floats(int M, int N) {
-  const size_t a = (size_t)M * du_sn(N), b = (size_t)DU_WAVES * du_tiles(M) * 16 * DU_FT;
+  const size_t a = (size_t)M * du_sn(N), b = (size_t)DU_WAVES * 4 * 16 * DU_FT;   // dY | the fold
   return (a > b ? a : b) + DU_MAXM * DU_FT + 6 * MAXC_DU;
 }
 
@@ -116,8 +116,8 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
   const int M = a.M, K = a.K, N = a.N, SN = du_sn(N);
   float* sdy = smem;                                       // [M][SN] dY, later the fold
   float* s_bn = smem + du_lds_floats(M, N) - 6 * MAXC_DU;  // [mean | rstd | a | b] x MAXC_DU
-  float* sxw = s_bn - DU_MAXM * DU_FT;                     // [64 m][16 f] Xw slice (rows >= M zero)
-  float* s_st = s_bn + 4 * MAXC_DU;                        // [2][MAXC_DU] BN-backward sums
+  float* sxw = s_bn - DU_MAXM * DU_FT;                     // [64 m][16 f] Xw slice, later BN partials
+  float* s_st = s_bn + 4 * MAXC_DU;                        // [2][MAXC_DU] slab-reduction scratch
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, q = lane >> 4;
@@ -127,24 +127,32 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
   constexpr int nslot = NSLOT;
   DU_STAMP(0);
 
-  // ---- one batch of loads
-  // (1) dY -> registers for the LDS stage: float4 e = tid + 1024 u, row e / (N/4)
-  const int n4 = N >> 2, tot4 = M * n4;
-  constexpr int DYV = DU_MAXM * 512 / 4 / DU_THREADS;     // 8 float4 per thread at most
-  float4 dyv[DYV];
+  // ---- every load, issued in the order it is consumed (vmcnt retires in order).  Two
+  // column halves: half j = columns [256 j, 256 j + 256) = every wave's sub-tile j, so the
+  // MFMAs of half 0 run while half 1's dY and W are still in flight.
+  // (0) the weight-gradient operand slice Xw[m][f0 .. f0+15], one element per thread
+  float xw1 = a.Xw[(long)min(tid >> 4, M - 1) * K + f0 + min(tid & 15, nf - 1)];
+  const int n4 = N >> 2;
+  int h4[DU_SUB];
 #pragma unroll
-  for (int u = 0; u < DYV; ++u) {
-    const int e = min(u * DU_THREADS + tid, tot4 - 1);
-    dyv[u] = reinterpret_cast<const float4*>(a.dY)[e];
-  }
-  // (2) W and slot float4s of this lane's sub-tiles
-  const int frow = f0 + min(i, nf - 1);
+  for (int j = 0; j < DU_SUB; ++j) h4[j] = max(min(N - 256 * j, 256), 0) >> 2;
   const float* b0 = nslot >= 1 ? a.s0w : a.W;              // address select: loads stay unconditional
   const float* b1 = nslot >= 2 ? a.s1w : a.W;
-  float4 wv[DU_SUB], s0v[DU_SUB], s1v[DU_SUB];
+  const int frow = f0 + min(i, nf - 1);
+  float4 dyv[DU_SUB][4], wv[DU_SUB], s0v[DU_SUB], s1v[DU_SUB];
   long wofs[DU_SUB];
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
+    // (1) dY half j: float4 e = u * 1024 + tid -> row e / h4, column 256 j + 4 (e % h4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = u * DU_THREADS + tid;
+      int row = 0, c4 = 0;
+      if (h4[j] == 64) { row = e >> 6; c4 = e & 63; }
+      else if (h4[j] > 0) { row = e / h4[j]; c4 = e - row * h4[j]; }
+      dyv[j][u] = reinterpret_cast<const float4*>(a.dY)[min(row, M - 1) * n4 + (h4[j] > 0 ? 64 * j + c4 : 0)];
+    }
+    // (2) W and slot float4s of sub-tile j
     const int col = min(16 * (wave + DU_WAVES * j), N - 16) + 4 * q;
     wofs[j] = (long)frow * N + col;
     wv[j] = *reinterpret_cast<const float4*>(a.W + wofs[j]);
@@ -152,10 +160,7 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
     if (nslot >= 1) s0v[j] = *reinterpret_cast<const float4*>(b0 + wofs[j]);
     if (nslot >= 2) s1v[j] = *reinterpret_cast<const float4*>(b1 + wofs[j]);
   }
-  // (3) the weight-gradient operand slice Xw[m][f0 .. f0+15], one element per thread
-  //     (staged in LDS: every wave needs all of it)
-  float xw1 = a.Xw[(long)min(tid >> 4, M - 1) * K + f0 + min(tid & 15, nf - 1)];
-  // (3b) bias: wave w owns column grp * bias_per + w (+16 r); its first operands prefetched
+  // (3) bias: wave w owns column grp * bias_per + w (+16 r); its first operands prefetched
   //     (unconditional loads from selected addresses: a load inside a branch is waited
   //     for right there, and vmcnt is in order — it would wait for W too)
   const int bn0 = grp * a.bias_per + wave;
@@ -175,39 +180,44 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
   const float* tsrc = tabs ? a.bn_tab : a.Xw;
   const int tc = tabs ? ch : 0, tC = tabs ? C : 0;
   float tmean = tsrc[tc], trstd = tsrc[tC + tc], ta = tsrc[2 * tC + tc], tb = tsrc[3 * tC + tc];
-#pragma unroll
-  for (int u = 0; u < DYV; ++u) pin(dyv[u]);
-  // stage dY (rows < M only: dgrad rows >= M are clamped reads whose outputs are dropped,
-  // wgrad rows >= M meet Xw = 0)
-#pragma unroll
-  for (int u = 0; u < DYV; ++u) {
-    const int e = u * DU_THREADS + tid;
-    if (e < tot4) {
-      const int m = e / n4, c4 = e - m * n4;
-      *reinterpret_cast<float4*>(sdy + m * SN + 4 * c4) = dyv[u];
-    }
-  }
-  pin(xw1);
-  sxw[tid] = ((tid >> 4) < M && (tid & 15) < nf) ? xw1 : 0.f;
-  if (a.bn_on && dgrad && !tabs)                          // no precomputed tables: reduce here
-    bn_reduce_to_lds(a.bn, s_bn, s_bn + MAXC_DU, s_bn + 2 * MAXC_DU, s_bn + 3 * MAXC_DU, s_st);
-  __syncthreads();
-  DU_STAMP(1);
-#pragma unroll
-  for (int j = 0; j < DU_SUB; ++j) { pin(wv[j]); pin(s0v[j]); pin(s1v[j]); }
-  DU_STAMP(2);
-  float xb[DU_KS];                                         // weight-gradient B: Xw[4s + q][f0 + i]
-#pragma unroll
-  for (int s = 0; s < DU_KS; ++s) xb[s] = sxw[(4 * s + q) * DU_FT + i];
 
   const float lr = opt_step_lr(a.opt, a.lr, a.step);
   du_f32x4 dacc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dacc[t] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  float xb[DU_KS];                                         // weight-gradient B: Xw[4s + q][f0 + i]
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
+    if (j == 0) {
+      pin(xw1);
+      sxw[tid] = ((tid >> 4) < M && (tid & 15) < nf) ? xw1 : 0.f;
+    }
+    // stage dY half j (rows < M only: dgrad rows >= M are clamped reads whose outputs are
+    // dropped, wgrad rows >= M meet Xw = 0); its columns are disjoint from half 0's, which
+    // other waves may still be reading
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pin(dyv[j][u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = u * DU_THREADS + tid;
+      if (h4[j] > 0 && e < M * h4[j]) {
+        const int row = h4[j] == 64 ? e >> 6 : e / h4[j];
+        const int c4 = e - row * h4[j];
+        *reinterpret_cast<float4*>(sdy + row * SN + 256 * j + 4 * c4) = dyv[j][u];
+      }
+    }
+    if (j == 0 && a.bn_on && dgrad && !tabs)              // no precomputed tables: reduce here
+      bn_reduce_to_lds(a.bn, s_bn, s_bn + MAXC_DU, s_bn + 2 * MAXC_DU, s_bn + 3 * MAXC_DU, s_st);
+    __syncthreads();
+    if (j == 0) {
+      DU_STAMP(1);
+#pragma unroll
+      for (int s = 0; s < DU_KS; ++s) xb[s] = sxw[(4 * s + q) * DU_FT + i];
+    }
+    pin(wv[j]); pin(s0v[j]); pin(s1v[j]);
+    if (j == 0) DU_STAMP(2);
     const int n0 = 16 * (wave + DU_WAVES * j);
-    if (n0 >= N) break;                                    // wave-uniform
+    if (n0 >= N) continue;                                 // wave-uniform
     // input-gradient partial (OLD weights): 4 batch tiles x 4 k-steps
     const float wk[4] = {wv[j].x, wv[j].y, wv[j].z, wv[j].w};
     if (dgrad) {
@@ -231,14 +241,14 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
       g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, xb[s], g0, 0, 0, 0);
       g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, xb[s + 1], g1, 0, 0, 0);
     }
-    // optimizer update of the lane's 4 weights (D lane (i, q) = dW[f0 + i][n0 + 4q + r])
+    // optimizer update of the lane's 4 weights (D lane (i, q) = dW[f0 + i][n0 + 4q + r]);
+    // written back after the fold: a store in flight would hold the fold's barrier (the
+    // compiler drains vmcnt before it) for the whole 16 MB write-back
     float w[4] = {wv[j].x, wv[j].y, wv[j].z, wv[j].w};
     float s0[4] = {s0v[j].x, s0v[j].y, s0v[j].z, s0v[j].w};
     float s1[4] = {s1v[j].x, s1v[j].y, s1v[j].z, s1v[j].w};
 #pragma unroll
     for (int r = 0; r < 4; ++r) opt_update(a.opt, lr, w[r], (g0[r] + g1[r]) * a.scale, s0[r], s1[r]);
-    // stored after the fold: a store in flight here would hold the fold's barrier
-    // (the compiler drains vmcnt before it) for the whole 16 MB write-back
     wv[j] = make_float4(w[0], w[1], w[2], w[3]);
     s0v[j] = make_float4(s0[0], s0[1], s0[2], s0[3]);
     s1v[j] = make_float4(s1[0], s1[1], s1[2], s1[3]);
@@ -272,24 +282,28 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
     return;
   }
 
-  // ---- fold the 16 waves' partials (D_t lane (i, q) holds rows 16t + 4q + r, feature i)
+  // ---- fold the 16 waves' partials.  Layout [wave][t][q][i][r]: lane (i, q) of tile t
+  // holds rows 16t + 4q + r of feature i, written as one conflict-free float4; a reading
+  // wave (4 rows x 16 features) reads 64 consecutive floats
   __syncthreads();                                         // every dY read is done
-  const int TM = du_tiles(M) * 16;
-  float* fold = sdy;                                       // [16 waves][TM][16]
+  float* fold = sdy;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     if (16 * t >= M) break;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) fold[(wave * TM + 16 * t + 4 * q + r) * DU_FT + i] = dacc[t][r];
+    *reinterpret_cast<du_f32x4*>(fold + ((wave * 4 + t) * 4 + q) * 64 + 4 * i) = dacc[t];
   }
-  if (a.bn_on) for (int c = tid; c < 2 * MAXC_DU; c += DU_THREADS) s_st[c] = 0.f;
   __syncthreads();
   DU_STAMP(4);
   du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, wave, i, nf, N, bown, bn0, bw, bs0, bs1);
-  if (eok) {
-    float g = 0.f;
+  float g = 0.f;
+  {
+    const int t = em >> 4, qq = (em >> 2) & 3, r = em & 3;
+    const float* src = fold + (t * 4 + qq) * 64 + 4 * ef + r;
 #pragma unroll
-    for (int w = 0; w < DU_WAVES; ++w) g += fold[(w * TM + em) * DU_FT + ef];
+    for (int w = 0; w < DU_WAVES; ++w) g += em < M ? src[w * 4 * 4 * 64] : 0.f;
+  }
+  float v1 = 0.f, v2 = 0.f;
+  if (eok) {
     if (tf) {
       float mean = tmean, rstd = trstd, sa = ta, sb = tb;
       if (a.bn_on && !tabs) {
@@ -298,20 +312,28 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
       const float z = a.bn_on ? xf * sa + sb : xf;
       const float y = act_fwd(z, a.act, a.alpha);
       g = act_bwd(g, z, y, a.act, a.alpha);
-      if (a.bn_on) {
-        atomicAdd(&s_st[ch], g);
-        atomicAdd(&s_st[MAXC_DU + ch], g * (xf - mean) * rstd);
-      }
+      v1 = g;
+      v2 = g * (xf - mean) * rstd;
     }
     a.dX[(long)em * K + f0 + ef] = g;
   }
   DU_STAMP(5);
   if (a.bn_on && a.bwd_slab) {
+    // BN-backward statistics per feature in fixed order: the wave's 4 rows by shuffles,
+    // the 16 waves through LDS (sxw is free), then one atomic per (feature, statistic)
+    // into one of DU_SLAB rows (zeroed every step by the optimizer launch)
+    v1 += __shfl_xor(v1, 16, 64); v1 += __shfl_xor(v1, 32, 64);
+    v2 += __shfl_xor(v2, 16, 64); v2 += __shfl_xor(v2, 32, 64);
+    float* sred = sxw;                                     // [16 waves][2][16]
+    if (lane < 16) { sred[wave * 32 + lane] = v1; sred[wave * 32 + 16 + lane] = v2; }
     __syncthreads();
-    // fold into one of DU_SLAB rows (atomics; zeroed every step by the optimizer launch)
-    const int C = a.bn.C > 0 ? a.bn.C : 1;
-    float* row = a.bwd_slab + (size_t)(grp % DU_SLAB) * 2 * C;
-    for (int c = tid; c < 2 * C; c += DU_THREADS) atomicAdd(&row[c], c < C ? s_st[c] : s_st[MAXC_DU + c - C]);
+    if (tid < 32 && (tid & 15) < nf) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < DU_WAVES; ++w) acc += sred[w * 32 + tid];
+      const int st = tid >> 4, c = (f0 + (tid & 15)) % C;
+      atomicAdd(a.bwd_slab + (size_t)(grp % DU_SLAB) * 2 * C + st * C + c, acc);
+    }
   }
   DU_STAMP(6);
 }
