@@ -43,15 +43,15 @@
 namespace csa {
 
 typedef float du_f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int du_u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DU_FT = 16;            // W rows per workgroup
-constexpr int DU_WAVES = 16;
-constexpr int DU_THREADS = 64 * DU_WAVES;
-constexpr int DU_SUB = 2;            // 16-column sub-tiles per wave (N <= 16 * 16 * 2 = 512)
+constexpr int DU_FT = 16;            // W rows per row group
+constexpr int DU_SUB = 2;            // 16-column sub-tiles per wave (= the two column halves)
 constexpr int DU_MAXM = 64;          // batch rows (4 tiles of 16)
 constexpr int DU_KS = DU_MAXM / 4;   // wgrad MFMA k-steps (4 batch rows each)
 constexpr int MAXC_DU = 128;         // BatchNorm channels handled in LDS
 constexpr int DU_SLAB = 16;          // BN-backward slab rows (atomically folded)
+constexpr int DU_PART = DU_MAXM * DU_FT;   // floats of one block's input-gradient partial
 constexpr size_t DU_LDS_MAX = 150 * 1024;
 
 struct DUArgs {
@@ -70,7 +70,9 @@ struct DUArgs {
   float* s0w; float* s1w;   // optimizer slots of W (same [K][N] layout) ...
   float* s0b; float* s1b;   // ... and of the bias
   float scale;
-  int bias_per;             // bias columns per workgroup
+  int cs;                   // column blocks per row group (> 1: partial hand-off)
+  float* part;              // [groups * cs][DU_PART] input-gradient partials (write-through)
+  unsigned* cnt;            // [groups] arrival tickets (zero between launches)
 };
 
 // diagnostics: s_memrealtime stamps (100 MHz, one clock for all XCDs) of EVERY block,
@@ -82,26 +84,30 @@ __constant__ long long* g_du_dbg = nullptr;
     if (g_du_dbg && threadIdx.x == 0) g_du_dbg[blockIdx.x * 8 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-__host__ __device__ inline int du_sn(int N) { return N + 4; }            // dY LDS row stride
-__host__ __device__ inline int du_tiles(int M) { return (M + 15) / 16; } // batch tiles of 16
-__host__ __device__ inline size_t du_lds_floats(int M, int N) {
-  const size_t a = (size_t)M * du_sn(N), b = (size_t)DU_WAVES * 4 * 16 * DU_FT;   // dY | the fold
-  return (a > b ? a : b) + DU_MAXM * DU_FT + 6 * MAXC_DU;
+__host__ __device__ constexpr int du_nb(int waves) { return 32 * waves; }      // columns per block
+__host__ __device__ inline size_t du_lds_floats(int M, int waves) {
+  const size_t a = (size_t)M * (du_nb(waves) + 4), b = (size_t)waves * 4 * 16 * DU_FT;   // dY | the fold
+  return (a > b ? a : b) + DU_MAXM * DU_FT + 6 * MAXC_DU + 4;
 }
 
-// Write back the updated W / slot float4s of a lane's sub-tiles (rows < nf, columns < N).
+__device__ __forceinline__ du_u32x4 du_bits(float4 v) { du_u32x4 u; __builtin_memcpy(&u, &v, 16); return u; }
+__device__ __forceinline__ float4 du_f4(du_u32x4 u) { float4 v; __builtin_memcpy(&v, &u, 16); return v; }
+
+// Write back the updated W / slot float4s of a lane's sub-tiles (rows < nf, columns < N)
+// and the wave's first bias column.
 template <int NSLOT>
 __device__ __forceinline__ void du_store_w(const DUArgs& a, const float4 (&wv)[DU_SUB], const float4 (&s0v)[DU_SUB],
-                                           const float4 (&s1v)[DU_SUB], const long (&wofs)[DU_SUB], int wave, int i,
-                                           int nf, int N, bool bown, int bn0, float bw, float bs0, float bs1) {
-  if (bown && (threadIdx.x & 63) == 0) {     // the wave's first bias column
+                                           const float4 (&s1v)[DU_SUB], const long (&wofs)[DU_SUB],
+                                           const bool (&sok)[DU_SUB], int i, int nf, bool bown, int bn0, float bw,
+                                           float bs0, float bs1) {
+  if (bown && (threadIdx.x & 63) == 0) {
     a.bias[bn0] = bw;
     if (NSLOT >= 1) a.s0b[bn0] = bs0;
     if (NSLOT >= 2) a.s1b[bn0] = bs1;
   }
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
-    if (16 * (wave + DU_WAVES * j) >= N || i >= nf) continue;
+    if (!sok[j] || i >= nf) continue;
     *reinterpret_cast<float4*>(a.W + wofs[j]) = wv[j];
     if (NSLOT >= 1) *reinterpret_cast<float4*>(a.s0w + wofs[j]) = s0v[j];
     if (NSLOT >= 2) *reinterpret_cast<float4*>(a.s1w + wofs[j]) = s1v[j];
@@ -109,77 +115,96 @@ __device__ __forceinline__ void du_store_w(const DUArgs& a, const float4 (&wv)[D
 }
 
 // NSLOT = optimizer slots (0 SGD, 1 Adagrad, 2 Adam / Adadelta): unused slot registers
-// are not allocated (the 1024-thread workgroup has 128 VGPRs per lane)
-template <int NSLOT>
-__global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) {
+// are not allocated.  WAVES = 16 (one block per row group, all N <= 512 columns) or 4
+// (128 columns per block, cs blocks per row group: narrow layers use more CUs).
+template <int NSLOT, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) {
+  constexpr int THREADS = 64 * WAVES, NB = du_nb(WAVES), SN = NB + 4, HW = 16 * WAVES;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int M = a.M, K = a.K, N = a.N, SN = du_sn(N);
-  float* sdy = smem;                                       // [M][SN] dY, later the fold
-  float* s_bn = smem + du_lds_floats(M, N) - 6 * MAXC_DU;  // [mean | rstd | a | b] x MAXC_DU
+  const int M = a.M, K = a.K, N = a.N, cs = a.cs;
+  float* sdy = smem;                                       // [M][SN] dY columns of the block, later the fold
+  float* s_bn = smem + du_lds_floats(M, WAVES) - 6 * MAXC_DU - 4;   // [mean | rstd | a | b] x MAXC_DU
   float* sxw = s_bn - DU_MAXM * DU_FT;                     // [64 m][16 f] Xw slice, later BN partials
   float* s_st = s_bn + 4 * MAXC_DU;                        // [2][MAXC_DU] slab-reduction scratch
+  int* s_flag = reinterpret_cast<int*>(s_st + 2 * MAXC_DU);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, q = lane >> 4;
-  const int grp = blockIdx.x, f0 = grp * DU_FT, nf = min(DU_FT, K - f0);
+  const int grp = blockIdx.x / cs, cblk = blockIdx.x - grp * cs;
+  const int f0 = grp * DU_FT, nf = min(DU_FT, K - f0);
+  const int cb = cblk * NB, nb = min(NB, N - cb);          // the block's columns [cb, cb + nb)
+  const int groups = gridDim.x / cs;
   const bool dgrad = a.dX != nullptr;
   const bool tf = dgrad && (a.act != ACT_NONE || a.bn_on);
+  const bool tabs = a.bn_on && a.bn_tab;
+  const int C = a.bn.C > 0 ? a.bn.C : 1;
   constexpr int nslot = NSLOT;
   DU_STAMP(0);
 
   // ---- every load, issued in the order it is consumed (vmcnt retires in order).  Two
-  // column halves: half j = columns [256 j, 256 j + 256) = every wave's sub-tile j, so the
-  // MFMAs of half 0 run while half 1's dY and W are still in flight.
-  // (0) the weight-gradient operand slice Xw[m][f0 .. f0+15], one element per thread
-  float xw1 = a.Xw[(long)min(tid >> 4, M - 1) * K + f0 + min(tid & 15, nf - 1)];
+  // column halves: half j = block columns [HW j, HW (j + 1)) = every wave's sub-tile j, so
+  // the MFMAs of half 0 run while half 1's dY and W are still in flight.
+  // (0) the weight-gradient operand slice Xw[m][f0 .. f0+15], 16 m-rows per 256 threads
+  float xw1[1024 / THREADS];
+#pragma unroll
+  for (int u = 0; u < 1024 / THREADS; ++u) {
+    const int e = u * THREADS + tid;
+    xw1[u] = a.Xw[(long)min(e >> 4, M - 1) * K + f0 + min(e & 15, nf - 1)];
+  }
+  // (0b) BN tables -> LDS (4C <= 512 values)
+  const float* tsrc = tabs ? a.bn_tab : a.Xw;               // address select: unconditional loads
+  float tv[512 / THREADS > 0 ? 512 / THREADS : 1];
+  constexpr int NTV = 512 / THREADS > 0 ? 512 / THREADS : 1;
+#pragma unroll
+  for (int u = 0; u < NTV; ++u) {
+    const int e = u * THREADS + tid;
+    tv[u] = tsrc[tabs && e < 4 * C ? e : 0];
+  }
   const int n4 = N >> 2;
   int h4[DU_SUB];
 #pragma unroll
-  for (int j = 0; j < DU_SUB; ++j) h4[j] = max(min(N - 256 * j, 256), 0) >> 2;
-  const float* b0 = nslot >= 1 ? a.s0w : a.W;              // address select: loads stay unconditional
+  for (int j = 0; j < DU_SUB; ++j) h4[j] = max(min(nb - HW * j, HW), 0) >> 2;
+  const float* b0 = nslot >= 1 ? a.s0w : a.W;
   const float* b1 = nslot >= 2 ? a.s1w : a.W;
   const int frow = f0 + min(i, nf - 1);
   float4 dyv[DU_SUB][4], wv[DU_SUB], s0v[DU_SUB], s1v[DU_SUB];
   long wofs[DU_SUB];
+  bool sok[DU_SUB];
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
-    // (1) dY half j: float4 e = u * 1024 + tid -> row e / h4, column 256 j + 4 (e % h4)
+    // (1) dY half j: float4 e = u * THREADS + tid -> row e / h4, block column HW j + 4 (e % h4)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = u * DU_THREADS + tid;
+      const int e = u * THREADS + tid;
       int row = 0, c4 = 0;
-      if (h4[j] == 64) { row = e >> 6; c4 = e & 63; }
+      if (h4[j] == HW / 4) { row = e / (HW / 4); c4 = e % (HW / 4); }
       else if (h4[j] > 0) { row = e / h4[j]; c4 = e - row * h4[j]; }
-      dyv[j][u] = reinterpret_cast<const float4*>(a.dY)[min(row, M - 1) * n4 + (h4[j] > 0 ? 64 * j + c4 : 0)];
+      dyv[j][u] = reinterpret_cast<const float4*>(a.dY)[min(row, M - 1) * n4 + (h4[j] > 0 ? (cb + HW * j) / 4 + c4 : 0)];
     }
     // (2) W and slot float4s of sub-tile j
-    const int col = min(16 * (wave + DU_WAVES * j), N - 16) + 4 * q;
-    wofs[j] = (long)frow * N + col;
+    const int lc = 16 * (wave + WAVES * j);                 // block-local first column
+    sok[j] = lc < nb;
+    wofs[j] = (long)frow * N + cb + min(lc, nb - 16) + 4 * q;
     wv[j] = *reinterpret_cast<const float4*>(a.W + wofs[j]);
     s0v[j] = s1v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (nslot >= 1) s0v[j] = *reinterpret_cast<const float4*>(b0 + wofs[j]);
     if (nslot >= 2) s1v[j] = *reinterpret_cast<const float4*>(b1 + wofs[j]);
   }
-  // (3) bias: wave w owns column grp * bias_per + w (+16 r); its first operands prefetched
-  //     (unconditional loads from selected addresses: a load inside a branch is waited
-  //     for right there, and vmcnt is in order — it would wait for W too)
-  const int bn0 = grp * a.bias_per + wave;
-  const bool bown = a.bias && wave < a.bias_per && bn0 < N;
+  // (3) bias: the block's columns are spread over the row groups, one per wave (+WAVES r);
+  //     the first column's operands prefetched (unconditional loads from selected
+  //     addresses: a load inside a branch is waited for right there, and vmcnt is in order)
+  const int bper = (nb + groups - 1) / groups;
+  const int bn0 = cb + grp * bper + wave;
+  const bool bown = a.bias && wave < bper && grp * bper + wave < nb;
   const int bnc = bown ? bn0 : 0;
   float bw = (a.bias ? a.bias : a.dY)[bnc];
   float bs0 = (nslot >= 1 && a.bias ? a.s0b : a.dY)[bnc];
   float bs1 = (nslot >= 2 && a.bias ? a.s1b : a.dY)[bnc];
-  // (4) epilogue operands: thread -> (batch row em = tid / 16, feature ef = tid % 16)
-  const int em = tid >> 4, ef = tid & 15;
-  const bool eok = dgrad && em < M && ef < nf;
-  const bool tabs = a.bn_on && a.bn_tab;
-  const int C = a.bn.C > 0 ? a.bn.C : 1;
-  const int ch = (f0 + ef) % C;
-  const float* xsrc = tf && a.x_fwd ? a.x_fwd : a.Xw;     // address select (same [M][K] shape)
-  float xf = xsrc[(long)min(em, M - 1) * K + f0 + min(ef, nf - 1)];
-  const float* tsrc = tabs ? a.bn_tab : a.Xw;
-  const int tc = tabs ? ch : 0, tC = tabs ? C : 0;
-  float tmean = tsrc[tc], trstd = tsrc[tC + tc], ta = tsrc[2 * tC + tc], tb = tsrc[3 * tC + tc];
+  // (4) epilogue operands: item it = tid < 256 -> batch row em = it / 4, features 4 (it % 4) ..
+  const int em = tid >> 2, fq = 4 * (tid & 3);
+  const bool eitem = tid < 256;
+  const float* xsrc = tf && a.x_fwd ? a.x_fwd : a.Xw;      // address select (same [M][K] shape)
+  float4 xf = *reinterpret_cast<const float4*>(xsrc + (long)min(em, M - 1) * K + f0 + min(fq, nf - 4));
 
   const float lr = opt_step_lr(a.opt, a.lr, a.step);
   du_f32x4 dacc[4];
@@ -189,8 +214,18 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
     if (j == 0) {
-      pin(xw1);
-      sxw[tid] = ((tid >> 4) < M && (tid & 15) < nf) ? xw1 : 0.f;
+#pragma unroll
+      for (int u = 0; u < 1024 / THREADS; ++u) {
+        const int e = u * THREADS + tid;
+        pin(xw1[u]);
+        sxw[e] = ((e >> 4) < M && (e & 15) < nf) ? xw1[u] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < NTV; ++u) {
+        const int e = u * THREADS + tid;
+        pin(tv[u]);
+        if (tabs && e < 4 * C) s_bn[(e / C) * MAXC_DU + e % C] = tv[u];
+      }
     }
     // stage dY half j (rows < M only: dgrad rows >= M are clamped reads whose outputs are
     // dropped, wgrad rows >= M meet Xw = 0); its columns are disjoint from half 0's, which
@@ -199,11 +234,11 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
     for (int u = 0; u < 4; ++u) pin(dyv[j][u]);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = u * DU_THREADS + tid;
+      const int e = u * THREADS + tid;
       if (h4[j] > 0 && e < M * h4[j]) {
-        const int row = h4[j] == 64 ? e >> 6 : e / h4[j];
+        const int row = h4[j] == HW / 4 ? e / (HW / 4) : e / h4[j];
         const int c4 = e - row * h4[j];
-        *reinterpret_cast<float4*>(sdy + row * SN + 256 * j + 4 * c4) = dyv[j][u];
+        *reinterpret_cast<float4*>(sdy + row * SN + HW * j + 4 * c4) = dyv[j][u];
       }
     }
     if (j == 0 && a.bn_on && dgrad && !tabs)              // no precomputed tables: reduce here
@@ -216,8 +251,8 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
     }
     pin(wv[j]); pin(s0v[j]); pin(s1v[j]);
     if (j == 0) DU_STAMP(2);
-    const int n0 = 16 * (wave + DU_WAVES * j);
-    if (n0 >= N) continue;                                 // wave-uniform
+    if (!sok[j]) continue;                                 // wave-uniform
+    const int n0 = 16 * (wave + WAVES * j);                // block-local
     // input-gradient partial (OLD weights): 4 batch tiles x 4 k-steps
     const float wk[4] = {wv[j].x, wv[j].y, wv[j].z, wv[j].w};
     if (dgrad) {
@@ -242,8 +277,8 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
       g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, xb[s + 1], g1, 0, 0, 0);
     }
     // optimizer update of the lane's 4 weights (D lane (i, q) = dW[f0 + i][n0 + 4q + r]);
-    // written back after the fold: a store in flight would hold the fold's barrier (the
-    // compiler drains vmcnt before it) for the whole 16 MB write-back
+    // written back late: a store in flight would hold the next barrier (the compiler drains
+    // vmcnt before it) for the whole write-back
     float w[4] = {wv[j].x, wv[j].y, wv[j].z, wv[j].w};
     float s0[4] = {s0v[j].x, s0v[j].y, s0v[j].z, s0v[j].w};
     float s1[4] = {s1v[j].x, s1v[j].y, s1v[j].z, s1v[j].w};
@@ -253,13 +288,14 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
     s0v[j] = make_float4(s0[0], s0[1], s0[2], s0[3]);
     s1v[j] = make_float4(s1[0], s1[1], s1[2], s1[3]);
   }
-  pin(bw); pin(bs0); pin(bs1); pin(xf); pin(tmean); pin(trstd); pin(ta); pin(tb);
+  pin(bw); pin(bs0); pin(bs1); pin(xf);
   // bias: column sums of dY over the batch, one column per wave (prefetched operands)
   if (bown) {
-    for (int u = wave; u < a.bias_per; u += DU_WAVES) {
-      const int n = grp * a.bias_per + u;
-      if (n >= N) break;
-      float v = lane < M ? sdy[lane * SN + n] : 0.f;
+    for (int u = wave; u < bper; u += WAVES) {
+      const int lcol = grp * bper + u;
+      if (lcol >= nb) break;
+      const int n = cb + lcol;
+      float v = lane < M ? sdy[lane * SN + lcol] : 0.f;
       v = wave_sum(v);
       if (lane == 0) {
         if (u != wave) {
@@ -278,13 +314,12 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
   }
   DU_STAMP(3);
   if (!dgrad) {                                            // uniform: first layer
-    du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, wave, i, nf, N, bown, bn0, bw, bs0, bs1);
+    du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
     return;
   }
 
-  // ---- fold the 16 waves' partials.  Layout [wave][t][q][i][r]: lane (i, q) of tile t
-  // holds rows 16t + 4q + r of feature i, written as one conflict-free float4; a reading
-  // wave (4 rows x 16 features) reads 64 consecutive floats
+  // ---- fold the waves' partials.  Layout [wave][t][q][i][r]: lane (i, q) of tile t holds
+  // rows 16t + 4q + r of feature i, written as one conflict-free float4
   __syncthreads();                                         // every dY read is done
   float* fold = sdy;
 #pragma unroll
@@ -294,43 +329,95 @@ __global__ __launch_bounds__(DU_THREADS) void dense_bwd_update_kernel(DUArgs a) 
   }
   __syncthreads();
   DU_STAMP(4);
-  du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, wave, i, nf, N, bown, bn0, bw, bs0, bs1);
-  float g = 0.f;
-  {
+  // item (em, fq): the block's partial of dX[em][f0 + fq .. +3], waves summed in order
+  float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (eitem && em < M) {
     const int t = em >> 4, qq = (em >> 2) & 3, r = em & 3;
-    const float* src = fold + (t * 4 + qq) * 64 + 4 * ef + r;
+    const float* src = fold + (t * 4 + qq) * 64 + 4 * fq + r;
 #pragma unroll
-    for (int w = 0; w < DU_WAVES; ++w) g += em < M ? src[w * 4 * 4 * 64] : 0.f;
-  }
-  float v1 = 0.f, v2 = 0.f;
-  if (eok) {
-    if (tf) {
-      float mean = tmean, rstd = trstd, sa = ta, sb = tb;
-      if (a.bn_on && !tabs) {
-        mean = s_bn[ch]; rstd = s_bn[MAXC_DU + ch]; sa = s_bn[2 * MAXC_DU + ch]; sb = s_bn[3 * MAXC_DU + ch];
-      }
-      const float z = a.bn_on ? xf * sa + sb : xf;
-      const float y = act_fwd(z, a.act, a.alpha);
-      g = act_bwd(g, z, y, a.act, a.alpha);
-      v1 = g;
-      v2 = g * (xf - mean) * rstd;
+    for (int w = 0; w < WAVES; ++w) {
+      const float* p = src + w * 4 * 4 * 64;
+      g4.x += p[0]; g4.y += p[4]; g4.z += p[8]; g4.w += p[12];
     }
-    a.dX[(long)em * K + f0 + ef] = g;
+  }
+  if (cs > 1) {
+    // publish write-through (sc1), drain, one agent-scope ticket per block; the row
+    // group's last arriving block sums the cs partials in column-block order
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        a.part, 0, (int)((size_t)gridDim.x * DU_PART * sizeof(float)), 0x00020000);
+    if (eitem && em < M)
+      __builtin_amdgcn_raw_buffer_store_b128(du_bits(g4), prs, (int)(((size_t)blockIdx.x * DU_PART + em * DU_FT + fq) * 4), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every storing wave drains
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(a.cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(cs - 1);
+      if (last) __hip_atomic_store(a.cnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+      *s_flag = last;
+    }
+    __syncthreads();
+    du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
+    if (!*s_flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: loads stay below
+    g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (eitem && em < M) {
+      float4 v[8];
+      for (int c0 = 0; c0 < cs; c0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = du_f4(__builtin_amdgcn_raw_buffer_load_b128(
+              prs, (int)((((size_t)grp * cs + min(c0 + u, cs - 1)) * DU_PART + em * DU_FT + fq) * 4), 0, 16));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (c0 + u < cs) { g4.x += v[u].x; g4.y += v[u].y; g4.z += v[u].z; g4.w += v[u].w; }
+      }
+    }
+  } else {
+    du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
+  }
+  // ---- transform backward (activation; BN statistics), dX
+  float v1[4] = {0.f, 0.f, 0.f, 0.f}, v2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (eitem && em < M && fq < nf) {
+    float g[4] = {g4.x, g4.y, g4.z, g4.w};
+    const float x[4] = {xf.x, xf.y, xf.z, xf.w};
+    if (tf) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ch = (f0 + fq + r) % C;
+        const float z = a.bn_on ? x[r] * s_bn[2 * MAXC_DU + ch] + s_bn[3 * MAXC_DU + ch] : x[r];
+        const float y = act_fwd(z, a.act, a.alpha);
+        g[r] = act_bwd(g[r], z, y, a.act, a.alpha);
+        v1[r] = g[r];
+        v2[r] = a.bn_on ? g[r] * (x[r] - s_bn[ch]) * s_bn[MAXC_DU + ch] : 0.f;
+      }
+    }
+    *reinterpret_cast<float4*>(a.dX + (long)em * K + f0 + fq) = make_float4(g[0], g[1], g[2], g[3]);
   }
   DU_STAMP(5);
   if (a.bn_on && a.bwd_slab) {
-    // BN-backward statistics per feature in fixed order: the wave's 4 rows by shuffles,
-    // the 16 waves through LDS (sxw is free), then one atomic per (feature, statistic)
-    // into one of DU_SLAB rows (zeroed every step by the optimizer launch)
-    v1 += __shfl_xor(v1, 16, 64); v1 += __shfl_xor(v1, 32, 64);
-    v2 += __shfl_xor(v2, 16, 64); v2 += __shfl_xor(v2, 32, 64);
-    float* sred = sxw;                                     // [16 waves][2][16]
-    if (lane < 16) { sred[wave * 32 + lane] = v1; sred[wave * 32 + 16 + lane] = v2; }
+    // BN-backward statistics per feature in fixed order: the wave's 16 rows by shuffles
+    // (lanes l, l ^ 4, .. share a feature quad), the 4 item waves through LDS, then one
+    // atomic per (feature, statistic) into one of DU_SLAB rows (zeroed every step by the
+    // optimizer launch)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) {
+        v1[r] += __shfl_xor(v1[r], o, 64);
+        v2[r] += __shfl_xor(v2[r], o, 64);
+      }
+    }
+    float* sred = sxw;                                     // [4 item waves][2][16]
+    if (eitem && lane < 4) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sred[wave * 32 + 4 * lane + r] = v1[r];
+        sred[wave * 32 + 16 + 4 * lane + r] = v2[r];
+      }
+    }
     __syncthreads();
     if (tid < 32 && (tid & 15) < nf) {
-      float acc = 0.f;
-#pragma unroll
-      for (int w = 0; w < DU_WAVES; ++w) acc += sred[w * 32 + tid];
+      const float acc = sred[tid] + sred[32 + tid] + sred[64 + tid] + sred[96 + tid];
       const int st = tid >> 4, c = (f0 + (tid & 15)) % C;
       atomicAdd(a.bwd_slab + (size_t)(grp % DU_SLAB) * 2 * C + st * C + c, acc);
     }
@@ -347,22 +434,50 @@ CSA_API int csa_du_debug(long long* p) {
 }
 
 // Shape family of the fused kernel (0 = outside: the caller uses the separate backward
-// kernels + the flat optimizer).  Needs M <= 64, N % 16 == 0, N <= 512, dY in LDS.
+// kernels + the flat optimizer).  M <= 64, K % 4 == 0, N % 16 == 0; N <= 512 (one block
+// per row group) or N % 128 == 0 (column blocks of 128).
 CSA_API int csa_dense_bwd_update_ok(int M, int K, int N, int bn_C) {
-  if (M < 1 || M > DU_MAXM || K < 1 || N < 16 || N % 16 || N > 16 * DU_WAVES * DU_SUB) return 0;
+  if (M < 1 || M > DU_MAXM || K < 4 || K % 4 || N < 16 || N % 16) return 0;
   if (bn_C > MAXC_DU) return 0;
-  return du_lds_floats(M, N) * sizeof(float) <= DU_LDS_MAX ? 1 : 0;
+  if (N > 512 && N % 128) return 0;
+  return du_lds_floats(M, 16) * sizeof(float) <= DU_LDS_MAX ? 1 : 0;
 }
 
 // BN-backward slab rows the kernel accumulates into (atomically; the caller zeroes them).
 CSA_API int csa_dense_bwd_update_slabs(int K) { return (K + DU_FT - 1) / DU_FT < DU_SLAB ? (K + DU_FT - 1) / DU_FT : DU_SLAB; }
+
+// Column blocks per row group the launcher picks: one 1024-thread block when the row groups
+// fill the chip (fc1: 245) and N <= 512, else 128-column blocks of 256 threads.
+static int du_cs(int K, int N) {
+  const int groups = (K + DU_FT - 1) / DU_FT;
+  static const int minb = [] { const char* e = getenv("CSA_DU_WIDE_MIN_GROUPS"); return e ? atoi(e) : 128; }();
+  if (N <= 512 && groups >= minb) return 1;
+  return (N + 127) / 128;
+}
+
+// Workspace of the partial hand-off: floats of the slabs (ws[0]), arrival counters (ws[1]).
+CSA_API int csa_dense_bwd_update_ws(int K, int N, long long* ws) {
+  const long long groups = (K + DU_FT - 1) / DU_FT, cs = du_cs(K, N);
+  ws[0] = cs > 1 ? groups * cs * DU_PART : 0;
+  ws[1] = cs > 1 ? groups : 0;
+  return (int)cs;
+}
+
+template <int NSLOT, int WAVES>
+static void du_launch(const DUArgs& a, int blocks, hipStream_t st) {
+  static const bool attr = hipFuncSetAttribute((const void*)dense_bwd_update_kernel<NSLOT, WAVES>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)DU_LDS_MAX) == hipSuccess;
+  (void)attr;
+  hipLaunchKernelGGL((dense_bwd_update_kernel<NSLOT, WAVES>), dim3((unsigned)blocks), dim3(64 * WAVES),
+                     du_lds_floats(a.M, WAVES) * sizeof(float), st, a);
+}
 
 CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
                                  const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
                                  int bn_C, float bn_count, float bn_eps, const float* bn_scale,
                                  const float* bn_offset, float* bwd_slab, const float* Xw, int opt, float lr,
                                  const int64_t* step, float* s0w, float* s1w, float* s0b, float* s1b,
-                                 float scale, const float* bn_tab, hipStream_t st) {
+                                 float scale, const float* bn_tab, float* part, unsigned* cnt, hipStream_t st) {
   if (!csa_dense_bwd_update_ok(M, K, N, bn_slab ? bn_C : 0)) return -1;
   if (!Xw || !W || !dY) return -2;
   DUArgs a{};
@@ -373,16 +488,19 @@ CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* 
   a.bwd_slab = bwd_slab; a.Xw = Xw;
   a.opt = opt; a.lr = lr; a.step = step; a.s0w = s0w; a.s1w = s1w; a.s0b = s0b; a.s1b = s1b; a.scale = scale;
   const int groups = (K + DU_FT - 1) / DU_FT;
-  a.bias_per = (N + groups - 1) / groups;
-  const size_t shm = du_lds_floats(M, N) * sizeof(float);
-  static const bool attr =
-      hipFuncSetAttribute((const void*)dense_bwd_update_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DU_LDS_MAX) == hipSuccess &&
-      hipFuncSetAttribute((const void*)dense_bwd_update_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DU_LDS_MAX) == hipSuccess &&
-      hipFuncSetAttribute((const void*)dense_bwd_update_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DU_LDS_MAX) == hipSuccess;
-  if (!attr) return -3;
+  a.cs = du_cs(K, N);
+  a.part = part; a.cnt = cnt;
+  if (a.cs > 1 && dX && (!part || !cnt)) return -2;
+  const int blocks = groups * a.cs;
   const int ns = opt_nslots(opt);
-  if (ns == 0) hipLaunchKernelGGL(dense_bwd_update_kernel<0>, dim3((unsigned)groups), dim3(DU_THREADS), shm, st, a);
-  else if (ns == 1) hipLaunchKernelGGL(dense_bwd_update_kernel<1>, dim3((unsigned)groups), dim3(DU_THREADS), shm, st, a);
-  else hipLaunchKernelGGL(dense_bwd_update_kernel<2>, dim3((unsigned)groups), dim3(DU_THREADS), shm, st, a);
+  if (a.cs == 1) {
+    if (ns == 0) du_launch<0, 16>(a, blocks, st);
+    else if (ns == 1) du_launch<1, 16>(a, blocks, st);
+    else du_launch<2, 16>(a, blocks, st);
+  } else {
+    if (ns == 0) du_launch<0, 4>(a, blocks, st);
+    else if (ns == 1) du_launch<1, 4>(a, blocks, st);
+    else du_launch<2, 4>(a, blocks, st);
+  }
   return (int)hipGetLastError();
 }

@@ -56,7 +56,8 @@ _SIGS = {
     "csa_dense_bwd_update_ok": (I, [I, I, I, I]),
     "csa_dense_bwd_update_slabs": (I, [I]),
     "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
-                                 P, P, P, P, F, P, P]),
+                                 P, P, P, P, F, P, P, P, P]),
+    "csa_dense_bwd_update_ws": (I, [I, I, P]),
     "csa_head_part_rows": (I, [I, I]),
     "csa_du_debug": (I, [P]),
     "csa_conv_pair_ok": (I, [P]),

@@ -28,6 +28,7 @@ reference accepts (construct_distribute.py:155-165, 208-265) lowers to HIP kerne
 from __future__ import annotations
 
 import ctypes as C
+import ctypes as _ctypes   # (C is shadowed by channel counts in _alloc)
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -289,12 +290,11 @@ class HipProgram:
             if tf.act is not None and not tf.has_bn:
                 continue                         # weight-gradient operand would need the act
             C = tf.norm.in_shape.c if tf.has_bn else 0
-            # one workgroup per 16 input features: a narrow layer (fc2: 32 workgroups)
-            # leaves the chip idle and is faster on the split-K pair + flat optimizer
-            # (profiles/r2_dense_fused.md)
+            # (a narrow layer's row groups are split over 128-column blocks with a partial
+            # hand-off, so fc2's 32 row groups still use 128 CUs: profiles/r2_dense_fused.md)
             groups = (fin + 15) // 16
             u.fused = (bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C))
-                       and groups >= int(os.environ.get("CSA_FUSED_DENSE_MIN_GROUPS", "128")))
+                       and groups >= int(os.environ.get("CSA_FUSED_DENSE_MIN_GROUPS", "1")))
         self.head_rg = 0
         if self.fused and self.head_tf.norm is None:
             last = self.units[-1]
@@ -523,6 +523,14 @@ class HipProgram:
             # BatchNorm tables [mean | rstd | a | b][C] written once per step by the
             # bn_act_apply that materialises xt (the fused dense backward's epilogue reads
             # them instead of reducing the statistic slab again)
+            if u.kind == "dense" and u.fused:
+                # partial input-gradient slabs + per-row-group arrival tickets when the
+                # kernel splits a row group over column blocks (the last arriver resets
+                # its ticket; zero-initialised here)
+                ws = (_ctypes.c_longlong * 2)()
+                self.lib.csa_dense_bwd_update_ws(u.layer.in_shape.numel, u.layer.spec.hidden, ws)
+                u.du_part = torch.zeros(max(int(ws[0]), 1), **f32)
+                u.du_cnt = torch.zeros(max(int(ws[1]), 1), dtype=torch.int32, device=dev)
             u.in_tf.bn_tab = (torch.zeros(4, u.in_tf.slab.shape[2], **f32)
                               if u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") != "1"
                               else None)
@@ -1218,7 +1226,7 @@ class HipProgram:
             K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
             K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
             K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
-            1.0, K.ptr(getattr(tf, "bn_tab", None)), st), "dense_bwd_update")
+            1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), st), "dense_bwd_update")
 
     def _opt_segments(self):
         """Flat [lo, hi) spans the optimizer launch updates: everything except the
