@@ -498,7 +498,7 @@ struct HeadPartArgs {
   const int64_t* labels; const int64_t* idx; const int64_t* cursor;
   int loss; float grad_scale;
   float* dh;                 // [M][K] or null
-  float* part;               // [G][K*10 + 10]
+  float* part;               // [G][K*10 + 10, padded to a multiple of 4]
   float* mpart; int* mcorr;  // [G]
   float* logits_out;         // optional [M][10]
   int64_t* step;
@@ -650,7 +650,8 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
     a.mcorr[g] = nc;
   }
   HEAD_STAMP(4);
-  float* prow = a.part + (long)g * (K * NCLS + NCLS);
+  // rows padded to a float4 multiple: the optimizer folds the G rows with float4 loads
+  float* prow = a.part + (long)g * ((K * NCLS + NCLS + 3) & ~3);
   if (tid < NCLS) {            // dbh partial
     float acc = 0.f;
     for (int r = 0; r < rows; ++r) acc += s_dl[r * NCLS + tid];

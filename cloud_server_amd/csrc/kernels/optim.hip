@@ -121,10 +121,20 @@ __device__ __forceinline__ float4 fold_grad(const FoldList& fl, long e, float4 g
   return make_float4(gs[0], gs[1], gs[2], gs[3]);
 }
 
+// diagnostics: s_memrealtime stamps (100 MHz) of every block, [block][4] = start, main
+// loop done, zero lists done, end (scripts/microbench.py MB_OPT)
+__constant__ long long* g_opt_dbg = nullptr;
+#define OPT_STAMP(i)                                                                         \
+  do {                                                                                       \
+    if (g_opt_dbg && threadIdx.x == 0) g_opt_dbg[blockIdx.x * 4 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
+  OPT_STAMP(0);
   const int nmain = (int)gridDim.x - a.stage.blocks;
   if ((int)blockIdx.x >= nmain) {
     stage_gather(a.stage, (int)blockIdx.x - nmain);
+    OPT_STAMP(3);
     return;
   }
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -163,12 +173,14 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     if (nslot >= 1) s04[i] = s0;
     if (nslot >= 2) s14[i] = s1;
   }
+  OPT_STAMP(1);
   // zero accumulators for the next step
   for (int z = 0; z < a.z.count; ++z) {
     float* p = a.z.p[z];
     const long n = a.z.n[z];
     for (long i = tid; i < n; i += nth) p[i] = 0.f;
   }
+  OPT_STAMP(2);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (a.met.parts > 0) {
       // all partials' loads in flight together (a serial load -> add loop is one memory
@@ -195,11 +207,16 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       *a.cursor = (a.cursor_wrap > 0 && c >= a.cursor_wrap) ? 0 : c;
     }
   }
+  OPT_STAMP(3);
 }
 
 }  // namespace csa
 
 using namespace csa;
+
+CSA_API int csa_opt_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_opt_dbg), &p, sizeof(p));
+}
 
 // Segments seg_lo/seg_hi (count <= 16, float4-aligned; nseg == 0: the whole [0, n)).
 // zero_ptrs/zero_ns: count <= 16 regions; fold_*: count <= 8 striped/partial descriptors.

@@ -60,6 +60,7 @@ _SIGS = {
     "csa_dense_bwd_update_ws": (I, [I, I, P]),
     "csa_head_part_rows": (I, [I, I]),
     "csa_du_debug": (I, [P]),
+    "csa_opt_debug": (I, [P]),
     "csa_conv_pair_ok": (I, [P]),
     "csa_cp_debug": (I, [P]),
     "csa_head_debug": (I, [P]),

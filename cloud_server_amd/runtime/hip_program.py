@@ -539,7 +539,11 @@ class HipProgram:
         if self.head_rg:
             K = self.dlast[0].numel()
             G = -(-B // self.head_rg)
-            self.head_part = torch.zeros(G, K * 10 + 10, **f32)     # per-group dWh | dbh
+            # per-group dWh | dbh, rows padded to float4 (the optimizer's fold then reads
+            # whole float4s: an odd row stride sent every head float4 down the per-element
+            # path, 4 dependent round trips, 7 us of the 8.6 us launch)
+            self.head_part = torch.zeros(G, (K * 10 + 10 + 3) // 4 * 4, **f32)
+            self.head_kw = K * 10
             self.head_mloss = torch.zeros(G, **f32)
             self.head_mcorr = torch.zeros(G, dtype=torch.int32, device=dev)
 
@@ -1276,9 +1280,13 @@ class HipProgram:
                     folds.append((offs[f"{lp.name}.bias"], u.db_acc.shape[1], u.db_acc, u.wg_stripes, u.db_acc.shape[1], 1))
         if self.head_rg:
             hp = self.head_part
-            kw = hp.shape[1] - 10
+            kw = self.head_kw
             folds.append((offs["head.weight"], kw, hp, hp.shape[0], hp.shape[1], 0))
-            folds.append((offs["head.bias"], 10, hp[:, kw:], hp.shape[0], hp.shape[1], 0))
+            # the bias span rounded up to a float4: the partial rows' padding and the flat
+            # layout's padding are zero, so the extra lanes update zero parameters by zero
+            # (no per-element edge path: one round trip instead of four)
+            nb = 12 if hp.shape[1] >= kw + 12 and self.e.flat.numel() >= offs["head.bias"] + 12 else 10
+            folds.append((offs["head.bias"], nb, hp[:, kw:], hp.shape[0], hp.shape[1], 0))
         if len(folds) > 8:
             raise Unsupported("more than 8 striped gradients")
         fo = (C.c_long * 8)(*[f[0] for f in folds])

@@ -108,6 +108,33 @@ def main() -> int:
                 end = (t.max() - t0) / 100
                 print(f"{i:2d} {name}: blocks {len(t)} span {end:.2f} us | start spread "
                       f"{(t[:, 0].max() - t0) / 100:.2f} | " + " | ".join(parts) + " (mean/max us)")
+    if os.environ.get("MB_OPT"):
+        # per-block stamps (100 MHz realtime): start, main loop done, zero lists done, end
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name.startswith("csa_optimizer"):
+                dbg = torch.zeros(4096 * 4, dtype=torch.int64, device="cuda")
+                for _ in range(3):
+                    dbg.zero_()
+                    eng.program.lib.csa_opt_debug(dbg.data_ptr())
+                    fn(*args)
+                    torch.cuda.synchronize()
+                    eng.program.lib.csa_opt_debug(None)
+                t = dbg.view(-1, 4)
+                nz = t[:, 0] > 0
+                idx = torch.nonzero(nz).flatten()
+                t = t[nz].double()
+                t0 = t[:, 0].min()
+                main = t[:, 2] > 0
+                st = ~main
+                def q(x):
+                    return f"{x.mean():.2f}/{x.max():.2f}" if len(x) else "-"
+                print(f"{i:2d} {name}: blocks {len(t)} (staging {int(st.sum())}) span {(t[:, 3].max() - t0) / 100:.2f} us | "
+                      f"start spread {(t[:, 0].max() - t0) / 100:.2f} | main {q((t[main, 1] - t[main, 0]) / 100)} | "
+                      f"zero {q((t[main, 2] - t[main, 1]) / 100)} | meta {q((t[main, 3] - t[main, 2]) / 100)} | "
+                      f"staging {q((t[st, 3] - t[st, 0]) / 100)} (mean/max us); block0 end {(t[0, 3] - t0) / 100:.2f}")
+                mt = (t[:, 1] - t[:, 0]) / 100
+                top = torch.argsort(mt, descending=True)[:6]
+                print("     slowest main loops (block: us):", [(int(idx[j]), round(float(mt[j]), 2)) for j in top])
     if os.environ.get("MB_CP"):
         dbg = torch.zeros(24, dtype=torch.int64, device="cuda")
         for i, (name, fn, args) in enumerate(rec.calls):

@@ -281,4 +281,4 @@ def test_staged_batch_matches_cursor_path(monkeypatch):
     assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-3
     # the statistic atomics' order may flip a borderline sample or two of the 19 x 50
     assert abs(outs[0][1]["accuracy"] - outs[1][1]["accuracy"]) <= 3 / (19 * 50) + 1e-9
-    assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) < 1e-4 * max(1.0, abs(outs[0][1]["loss"]))
+    assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) < 1e-3 * max(1.0, abs(outs[0][1]["loss"]))
