@@ -356,10 +356,8 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
       *s_flag = last;
     }
     __syncthreads();
-    if (!*s_flag) {
-      du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
-      return;
-    }
+    du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
+    if (!*s_flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: loads stay below
     g4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (eitem && em < M) {
@@ -374,13 +372,13 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
           if (c0 + u < cs) { g4.x += v[u].x; g4.y += v[u].y; g4.z += v[u].z; g4.w += v[u].w; }
       }
     }
+  } else {
+    du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
   }
-  // ---- transform backward (activation; BN statistics), dX.  Every global store of the
-  // block (dX, W, slots) waits until after the last barrier: the compiler drains vmcnt in
-  // front of a barrier, and the W / slot write-back is the launch's 16 MB
+  // ---- transform backward (activation; BN statistics), dX
   float v1[4] = {0.f, 0.f, 0.f, 0.f}, v2[4] = {0.f, 0.f, 0.f, 0.f};
-  float g[4] = {g4.x, g4.y, g4.z, g4.w};
   if (eitem && em < M && fq < nf) {
+    float g[4] = {g4.x, g4.y, g4.z, g4.w};
     const float x[4] = {xf.x, xf.y, xf.z, xf.w};
     if (tf) {
 #pragma unroll
@@ -393,6 +391,7 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
         v2[r] = a.bn_on ? g[r] * (x[r] - s_bn[ch]) * s_bn[MAXC_DU + ch] : 0.f;
       }
     }
+    *reinterpret_cast<float4*>(a.dX + (long)em * K + f0 + fq) = make_float4(g[0], g[1], g[2], g[3]);
   }
   DU_STAMP(5);
   if (a.bn_on && a.bwd_slab) {
@@ -423,9 +422,6 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
       atomicAdd(a.bwd_slab + (size_t)(grp % DU_SLAB) * 2 * C + st * C + c, acc);
     }
   }
-  if (eitem && em < M && fq < nf)
-    *reinterpret_cast<float4*>(a.dX + (long)em * K + f0 + fq) = make_float4(g[0], g[1], g[2], g[3]);
-  du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
   DU_STAMP(6);
 }
 
