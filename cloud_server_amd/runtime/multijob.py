@@ -38,6 +38,10 @@ def prefer_packed_kernels() -> None:
     """Kernel choices for engines that will run packed (unless the user chose)."""
     import os
     os.environ.setdefault("CSA_DENSE_DIRECT", "1")
+    # wide dense backward as 128-column blocks (256 threads, 33 KB LDS: four per CU beside
+    # other jobs' kernels) instead of one 1024-thread, 106 KB row-group block per CU:
+    # K = 4 805.5k vs 743.0k, K = 8 917.8k vs 861.0k samples/s (profiles/r2_multitenant.md)
+    os.environ.setdefault("CSA_DU_WIDE_MIN_GROUPS", "100000")
 
 
 class PackedJobs:
