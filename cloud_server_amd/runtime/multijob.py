@@ -42,6 +42,9 @@ def prefer_packed_kernels() -> None:
     # other jobs' kernels) instead of one 1024-thread, 106 KB row-group block per CU:
     # K = 4 805.5k vs 743.0k, K = 8 917.8k vs 861.0k samples/s (profiles/r2_multitenant.md)
     os.environ.setdefault("CSA_DU_WIDE_MIN_GROUPS", "100000")
+    # conv pair: two pooled rows per workgroup (350 instead of 700 for B = 50) — less
+    # per-band staging CU-time: K = 8 995.4k vs 930.5k samples/s (scripts/gpu_pack4.sh)
+    os.environ.setdefault("CSA_CP_PR", "2")
 
 
 class PackedJobs:
