@@ -194,6 +194,10 @@ def main() -> int:
     m = eng.metrics_since(eng.host_step - min(args.steps, 100))
 
     total = args.batch * ctx.world * args.steps / dt
+    pg = "none"
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        pg = torch.distributed.get_backend()
+        pg = "rccl" if pg == "nccl" else pg          # the "nccl" backend IS RCCL on ROCm
     if ctx.rank == 0:
         out = {
             "metric": "train_samples_per_s",
@@ -219,8 +223,8 @@ def main() -> int:
                 "hip_graph": eng.use_graph,
                 # per call site: xGMI peer-buffer kernel or RCCL, and (CSA_XGMI=auto) the
                 # start-up timings that decided it
-                "collectives": {t: ("xgmi" if c is not None else "rccl") for t, c in eng.sync._choice.items()}
-                               or ("rccl" if ctx.world > 1 else "none"),
+                "collectives": {t: ("xgmi" if c is not None else pg) for t, c in eng.sync._choice.items()}
+                               or (pg if ctx.world > 1 else "none"),
                 "xgmi": eng.sync.xgmi_reason,
                 "collective_tuning_us": eng.sync.xgmi_tuning,
                 "strategy_tuning_ms_per_step": tuning,
