@@ -176,14 +176,16 @@ def main() -> int:
     eng = TrainEngine(cfg, ds, device=ctx.device, ctx=ctx, backend=args.backend,
                       use_graph=not args.no_graph, strategy=args.strategy)
 
-    for _ in range(args.warmup):
-        eng.step()
+    # run_steps: exactly K steps; on one GPU groups of CSA_GRAPH_STEPS steps replay one
+    # multi-step graph (runtime/engine.py)
+    eng.step()                          # capture + first step
+    eng.prepare_group_graph()
+    eng.run_steps(max(args.warmup - 1, 0))
     eng.sync_device()
     barrier(ctx)
     eng.sync_device()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
+    eng.run_steps(args.steps)
     eng.sync_device()
     barrier(ctx)
     eng.sync_device()

@@ -108,6 +108,13 @@ class BatchStream:
         self._filled[h] = True
         self.refills += 1
 
+    def can_group(self, k: int) -> bool:
+        """Can the next ``k`` steps be enqueued as ONE launch (a multi-step graph)?  Yes
+        when they stay inside one half of the row table, so every before_step() call the
+        group makes up front marks and refills exactly what per-step calls would."""
+        pos = 0 if self.used >= self.chunk else self.used
+        return 1 <= k <= self.chunk and pos + k <= self.chunk
+
     def before_step(self) -> None:
         """Host-side bookkeeping; call once per step before launching/replaying it."""
         if self.used >= self.chunk:

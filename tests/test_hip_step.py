@@ -282,3 +282,27 @@ def test_staged_batch_matches_cursor_path(monkeypatch):
     # the statistic atomics' order may flip a borderline sample or two of the 19 x 50
     assert abs(outs[0][1]["accuracy"] - outs[1][1]["accuracy"]) <= 3 / (19 * 50) + 1e-9
     assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) < 1e-3 * max(1.0, abs(outs[0][1]["loss"]))
+
+
+def test_run_steps_groups_equal_single_steps(monkeypatch):
+    """run_steps(n) replays CSA_GRAPH_STEPS-step graphs where a group fits in a half of the
+    batch row table and single steps elsewhere: exactly n steps run, with the same batches
+    (cursor, step counter) and numerics as n step() calls — across half boundaries."""
+    ds = synthetic_mnist(700, seed=29)
+    cfg = _cfg(CASES["sample"], optimizer="GradientDescentOptimizer", lr=0.001)
+    monkeypatch.setenv("CSA_GRAPH_STEPS", "4")
+    a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True, stream_chunk=6)
+    b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True, stream_chunk=6)
+    a.step()
+    a.prepare_group_graph()
+    assert a.graph_k is not None
+    a.run_steps(17)
+    for _ in range(18):
+        b.step()
+    torch.cuda.synchronize()
+    assert a.host_step == b.host_step == 18
+    assert int(a.dstep.item()) == int(b.dstep.item()) == 18
+    assert int(a.stream.cursor.item()) == int(b.stream.cursor.item())
+    assert (a.flat - b.flat).abs().max().item() < 1e-3
+    ma, mb = a.metrics_since(0), b.metrics_since(0)
+    assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
