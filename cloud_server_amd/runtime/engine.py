@@ -223,7 +223,7 @@ class TrainEngine:
     def group_steps(self) -> int:
         """Steps per multi-step graph (1: grouping off — eager, data parallel, or
         CSA_GRAPH_STEPS=1)."""
-        k = int(os.environ.get("CSA_GRAPH_STEPS", "4"))
+        k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
         return k if (self.use_graph and k > 1 and not self.ctx.enabled) else 1
 
     def prepare_group_graph(self) -> None:
@@ -239,9 +239,9 @@ class TrainEngine:
 
     def run_steps(self, n: int) -> None:
         """``n`` training steps.  With a captured single-GPU program, groups of
-        ``CSA_GRAPH_STEPS`` (default 4) steps replay ONE graph holding that many steps:
-        one launch instead of k, measured 108.8 -> 104.8 µs/step at k = 4 on MI355X
-        (scripts/graph_unroll_probe.py).  Groups never straddle a half of the batch row
+        ``CSA_GRAPH_STEPS`` (default 8) steps replay ONE graph holding that many steps:
+        one launch instead of k.  Bench on MI355X (scripts/gpu_sweep.sh): 0.108 ms/step
+        ungrouped, 0.1045 at k = 4, 0.1035 at k = 8, 0.1034 at k = 16.  Groups never straddle a half of the batch row
         table (BatchStream.can_group); the remainder runs step by step, so exactly ``n``
         steps execute."""
         k = self.group_steps()

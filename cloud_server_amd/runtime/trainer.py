@@ -246,6 +246,15 @@ class JobRun:
         step = eng.host_step
         if ctx.enabled and eng.device.type == "cuda" and step % (self.ctl_every * self.log_every) == 1:
             eng.probe_comm()            # per-rank collective time for metrics.jsonl
+            return
+        # k steps as one multi-step graph launch (TrainEngine.run_steps) when no per-step
+        # hook falls inside them: the group's LAST step may be a log point (after_step
+        # handles it), earlier ones may not; fault / hang injection steps run alone
+        k = eng.group_steps() if eng.graph is not None else 1
+        if (k > 1 and step + k <= self.cfg.iter
+                and all((s % self.log_every) != 0 for s in range(step, step + k - 1))
+                and not (step <= self.fault_at < step + k) and not (step <= self.hang_at < step + k)):
+            eng.run_steps(k)
         else:
             eng.step()
 
