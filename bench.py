@@ -98,12 +98,11 @@ def bench_packed(args) -> int:
             engs.append(TrainEngine(cfg, synthetic_mnist(60000, seed=r), device=dev,
                                     backend=args.backend, use_graph=not args.no_graph))
         pack = PackedJobs(engs)
-        for _ in range(args.warmup):
-            pack.step()
+        pack.step()                       # capture + first step
+        pack.run_steps(max(args.warmup - 1, 0))   # (captures the multi-step graph)
         pack.sync_device()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            pack.step()
+        pack.run_steps(args.steps)
         pack.sync_device()
         dt = time.perf_counter() - t0
         backend = engs[0].backend

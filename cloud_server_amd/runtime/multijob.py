@@ -60,7 +60,48 @@ class PackedJobs:
         if any(e.ctx.enabled for e in engines):
             raise ValueError("packed jobs are single-GPU jobs (no data-parallel group)")
         self.graph = None
+        self.graph_k = None
         self.host_step = 0
+
+    def _capture_group(self, k: int) -> None:
+        """k steps of every job as ONE graph: each job's branch runs its k steps back to
+        back (the jobs drift within the graph instead of joining after every step)."""
+        streams = self._streams
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            cap = torch.cuda.current_stream(self.device)
+            for e, s in zip(self.engines, streams):
+                s.wait_stream(cap)
+                with torch.cuda.stream(s):
+                    for _ in range(k):
+                        e.program.run()
+            for s in streams:
+                cap.wait_stream(s)
+        self.graph_k = g
+
+    def run_steps(self, n: int) -> None:
+        """``n`` steps of every job: groups of CSA_GRAPH_STEPS steps as one multi-step
+        graph where every job's group stays inside one half of its row table (see
+        TrainEngine.run_steps), single packed steps otherwise."""
+        import os
+        k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        while n > 0:
+            if (self.cuda and k > 1 and n >= k and self.graph is not None
+                    and all(e.stream.can_group(k) for e in self.engines)):
+                if self.graph_k is None:
+                    self._capture_group(k)
+                for _ in range(k):
+                    for e in self.engines:
+                        e.stream.before_step()
+                with trace_range("csa.packed_steps"):
+                    self.graph_k.replay()
+                for e in self.engines:
+                    e.host_step += k
+                self.host_step += k
+                n -= k
+            else:
+                self.step()
+                n -= 1
 
     def _capture(self) -> None:
         for e in self.engines:
