@@ -51,7 +51,7 @@ from ..models.dsl import ConfigError, parse_train_config, spec_to_dict
 from ..models.options import CATALOG, get_options
 from ..preprocess import ops_ref, pipeline
 from ..runtime.devices import node_status
-from ..runtime.jobs import JobManager
+from ..runtime.jobs import JobConflict, JobManager
 from ..runtime.trainer import METRICS, RESULT, STATUS, read_train_results
 from ..serve.inference import FAIL_NO_MODEL, InferenceService
 from ..store.db import FILE_TYPES, Database, check_password
@@ -558,6 +558,8 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
             ngpus = int(f["options"].get("gpus", 1))
         try:
             jid = jobs.submit(u["id"], model, datatype, f, ngpus=ngpus)
+        except JobConflict as exc:
+            return J({"message": "error", "detail": str(exc)}, 409)
         except ValueError as exc:
             return J({"message": "error", "detail": str(exc)}, 400)
         return J({"message": "success", "job": jid, "params": cfg.plan().num_params()})
@@ -714,6 +716,8 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
             return J({"detail": "Not found."}, 404)
         try:
             return J(jobs.control(jid, "resume"))
+        except JobConflict as exc:
+            return J({"message": "error", "detail": str(exc)}, 409)
         except ValueError as exc:
             return J({"message": "error", "detail": str(exc)}, 400)
 

@@ -40,11 +40,17 @@ import traceback
 from typing import Any, Dict, List, Optional
 
 from ..store.db import Database
+from ..utils.locks import SUBMIT_LOCK, locked
 from . import checkpoint as ckpt
 from .scheduler import make_scheduler
 from .trainer import CONTROL, STATUS, run_job, write_status
 
-TERMINAL = ("done", "stopped", "failed", "paused")
+TERMINAL = ("done", "stopped", "failed", "paused", "resumed")
+ACTIVE = ("queued", "running")
+
+
+class JobConflict(ValueError):
+    """A job for this (user, model) is already queued or running (HTTP 409)."""
 
 
 def _launcher_main(req: "mp.Queue", resp: "mp.Queue") -> None:   # pragma: no cover - subprocess
@@ -144,17 +150,34 @@ class JobManager:
 
     # ------------------------------------------------------------------ public API
     def submit(self, owner: int, model: str, datatype: str, config: Dict[str, Any],
-               ngpus: int = 1) -> int:
+               ngpus: int = 1, resume_of: Optional[int] = None) -> int:
+        """Queue a job for (owner, model).  One job per model dir at a time: a queued or
+        running job makes this raise ``JobConflict`` (the reference instead ``pkill``ed
+        whatever ran, apps/construction/views.py:128-129); a paused one is superseded
+        (marked ``stopped``) unless this call resumes it (``resume_of``: then it is marked
+        ``resumed``).  The check and the insert run under the model dir's submit lock, so
+        concurrent API workers cannot both admit a job."""
         mdir = self.settings.model_dir(owner, model)
         os.makedirs(mdir, exist_ok=True)
-        with open(os.path.join(mdir, "model.json"), "w", encoding="utf-8") as f:
-            json.dump(config, f, ensure_ascii=False)
-        try:
-            os.remove(os.path.join(mdir, CONTROL))
-        except OSError:
-            pass
-        jid = self.db.add_job(owner, model, datatype, config)
-        write_status(mdir, state="queued", job=jid)
+        with locked(os.path.join(mdir, SUBMIT_LOCK)):
+            prior = [j for j in self.db.jobs_for(owner, model) if j["state"] in ACTIVE + ("paused",)]
+            busy = [j["id"] for j in prior if j["state"] in ACTIVE]
+            if busy:
+                raise JobConflict(f"model {model!r} already has job {busy[-1]} "
+                                  f"({self.db.get_job(busy[-1])['state']}): stop it first")
+            with open(os.path.join(mdir, "model.json"), "w", encoding="utf-8") as f:
+                json.dump(config, f, ensure_ascii=False)
+            try:
+                os.remove(os.path.join(mdir, CONTROL))
+            except OSError:
+                pass
+            jid = self.db.add_job(owner, model, datatype, config)
+            for j in prior:                              # paused jobs of this model
+                if j["id"] == resume_of:
+                    self.db.update_job(j["id"], state="resumed", error=f"resumed as job {jid}")
+                else:
+                    self.db.update_job(j["id"], state="stopped", error=f"superseded by job {jid}")
+            write_status(mdir, state="queued", job=jid)
         ngpus = max(1, min(int(ngpus), max(self.ngpu, 1)))
         if not self.sched.submit(jid, 1 if self.use_cpu else ngpus):
             self.db.update_job(jid, state="failed", error="cannot place job")
@@ -186,7 +209,8 @@ class JobManager:
             if job["state"] not in ("paused", "stopped", "failed"):
                 raise ValueError(f"job {jid} is {job['state']}")
             cfg = json.loads(job["config"])
-            return {"job": self.submit(job["owner_id"], job["model"], job["datatype"], cfg), "action": "resume"}
+            return {"job": self.submit(job["owner_id"], job["model"], job["datatype"], cfg, resume_of=jid),
+                    "action": "resume"}
         raise ValueError(f"unknown action {action!r}")
 
     def status(self, jid: int) -> Dict[str, Any]:
@@ -344,6 +368,14 @@ class JobManager:
                 spool = os.path.join(self.settings.storage_root, "gpu_hosts", f"gpu{gpu}")
                 os.makedirs(os.path.join(spool, "inbox"), exist_ok=True)
                 os.makedirs(os.path.join(spool, "done"), exist_ok=True)
+                # a previous host's unread inbox entries belong to jobs that were failed as
+                # its orphans: never let the new host train them behind the manager's back
+                inbox = os.path.join(spool, "inbox")
+                for n in os.listdir(inbox):
+                    try:
+                        os.remove(os.path.join(inbox, n))
+                    except OSError:
+                        pass
                 h = {"spool": spool, "alive": True, "jobs": set()}
                 self.hosts[gpu] = h
                 if not self.use_cpu:
@@ -394,6 +426,11 @@ class JobManager:
             h["alive"] = False
             orphans = list(h["jobs"])
             h["jobs"].clear()
+            for jid in orphans:                     # posted but never admitted by the dead host
+                try:
+                    os.remove(os.path.join(h["spool"], "inbox", f"{jid}.json"))
+                except OSError:
+                    pass
         for jid in orphans:                         # the host died under them
             with self._lock:
                 info = self.running.get(jid)

@@ -30,6 +30,7 @@ from ..data.datasets import ArrayDataset, load_dataset_for_model, load_mnist_dir
 from ..models.dsl import parse_train_config
 from ..parallel.dist import DistContext, all_reduce_max, barrier
 from . import checkpoint as ckpt
+from ..utils.locks import WriterLock
 from ..utils.tracing import trace_range
 from .engine import TrainEngine
 
@@ -198,6 +199,9 @@ class JobRun:
         self.cfg = cfg = parse_train_config(config)
         if device is None:
             device = str(ctx.device) if ctx.enabled else ("cuda" if torch.cuda.is_available() else "cpu")
+        # single writer per model dir (the reference's shared append-mode result.txt race,
+        # SURVEY §5.2): raises LockHeld BEFORE touching status.json of the job that owns it
+        self.wlock = WriterLock(model_dir) if chief else None
         if chief:
             write_status(model_dir, state="running", pid=os.getpid(), device=device, world=ctx.world)
         self.ckpter = None
@@ -327,6 +331,7 @@ class JobRun:
         if chief:
             write_status(self.model_dir, state=state, step=eng.host_step, final_accuracy=final_acc,
                          backend=eng.backend, fallback=eng.fallback_reason)
+        self._unlock()
         return {"state": state, "step": eng.host_step, "final_accuracy": final_acc, "backend": eng.backend}
 
     def fail(self, exc: BaseException) -> None:
@@ -339,6 +344,11 @@ class JobRun:
                 self.ckpter.wait()      # never leave a half-written checkpoint thread behind
         except Exception:
             pass
+        self._unlock()
+
+    def _unlock(self) -> None:
+        if getattr(self, "wlock", None) is not None:
+            self.wlock.release()
 
 
 def run_job(model_dir: str, config: Dict[str, Any], datatype: str = "file",

@@ -1,3 +1,4 @@
+import faulthandler
 import os
 import sys
 
@@ -7,10 +8,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# A dup of the real stderr taken before pytest's per-test capture redirects fd 2: output
+# written here survives a native abort (SIGABRT inside HIP/RCCL) that loses captured text.
+_REAL_ERR = None
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP) device")
     config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.hookimpl(trylast=True)
+def pytest_sessionstart(session):
+    """Dump only the faulting thread on a fatal signal, so the test frames stay inside a
+    short output tail (pytest's own handler dumps every thread plus the extension list)."""
+    global _REAL_ERR
+    try:
+        _REAL_ERR = os.dup(sys.__stderr__.fileno())
+    except (AttributeError, OSError, ValueError):
+        _REAL_ERR = None
+        return
+    faulthandler.enable(file=_REAL_ERR, all_threads=False)
+
+
+def pytest_runtest_logstart(nodeid, location):
+    if _REAL_ERR is not None:
+        os.write(_REAL_ERR, f"[csa-test] {nodeid}\n".encode())
 
 
 def pytest_collection_modifyitems(config, items):

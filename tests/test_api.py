@@ -460,3 +460,29 @@ def test_event_loop_free_during_slow_preprocess(client, monkeypatch):
     assert lst.status_code == 200 and len(lst.json()) == 1
     assert not done_early and res.json()["message"] == "success", res.text
     assert dt < 0.1, dt
+
+
+def test_construct_twice_is_409_and_result_stays_clean(tmp_path):
+    """One job per (user, model): a second construct while the first is running gets 409
+    (reference: the second launch pkill'ed the first, apps/construction/views.py:128-129)."""
+    s = Settings(storage_root=str(tmp_path / "store"), db_path=str(tmp_path / "db.sqlite3"),
+                 executor="thread", train_backend="torch")
+    with TestClient(create_app(s, executor="thread", ngpu=0, inference_device="cpu")) as c:
+        h = _auth(c)
+        zb, tags, _ = _digit_zip(40)
+        assert c.post("/data/create/", json={"modelName": "m"}, headers=h).json() == {"message": "success"}
+        _mp(c, "/data/tag/", {"modelName": "m"}, {"file": ("tag.json", json.dumps(tags).encode(), "application/json")}, h)
+        pk = _mp(c, "/data/list/", {"file_type": "zip", "file_class": "picture"},
+                 {"file": ("d.zip", zb, "application/zip")}, h).json()["data_id"]
+        assert c.post("/preprocess/", json={"dataId": pk, "modelName": "m", "operations": []}, headers=h).status_code == 200
+        cfg = {"iter": 200, "learning_rate": 0.05, "ratio": 0.8, "optimizer_name": "AdamOptimizer",
+               "options": {"log_every": 50, "ckpt_every": 0, "batch_size": 8},
+               "net_config": {"middle_layer": [{"layer": "connect", "hidden": 16}]}}
+        r1 = c.post("/construct/construction/m/file/", json=cfg, headers=h)
+        r2 = c.post("/construct/construction/m/file/", json=cfg, headers=h)
+        assert r1.status_code == 200 and r2.status_code == 409, (r1.text, r2.text)
+        assert c.app.state.jobs.wait(r1.json()["job"], 300) == "done"
+        res = c.get("/runtime/train/m/200/", headers=h).json()
+        assert [r["step"] for r in res["every_result"]] == ["0", "50", "100", "150"]
+        assert "final_accuracy" in res
+        assert len(c.app.state.db.jobs_for(1, "m")) == 1

@@ -418,3 +418,69 @@ def test_inference_service_async_path_cpu(tmp_path):
     assert out == sync and all(o["result"] == "success" for o in out)
     assert svc.latency_ms()["n"] == 12
     svc.close()
+
+
+# ---------------------------------------------------------------- single writer per model
+def test_writer_lock_refuses_second_job_without_touching_status(tmp_path):
+    """Two JobRuns on one model dir (e.g. two packed jobs in one GPU host): the second
+    fails fast with LockHeld and leaves the first job's status/result files alone."""
+    from cloud_server_amd.runtime.trainer import JobRun
+    from cloud_server_amd.utils.locks import LockHeld
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    data = _data()
+    a = JobRun(mdir, dict(SMALL, iter=20), device="cpu", backend="torch", data=data)
+    st = open(os.path.join(mdir, STATUS)).read()
+    with pytest.raises(LockHeld):
+        JobRun(mdir, dict(SMALL, iter=20), device="cpu", backend="torch", data=data)
+    assert open(os.path.join(mdir, STATUS)).read() == st
+    while a.pending():
+        a.before_step(); a.step(); a.after_step()
+    assert a.finish()["state"] == "done"
+    # released at finish: the next run of the model may write again
+    b = JobRun(mdir, dict(SMALL, iter=30), device="cpu", backend="torch", data=data)
+    b.fail(RuntimeError("x"))
+    JobRun(mdir, dict(SMALL, iter=30), device="cpu", backend="torch", data=data)._unlock()
+
+
+def test_one_job_per_model_conflict_and_supersede(tmp_path):
+    """A second construct for a model whose job is queued/running is refused (JobConflict,
+    HTTP 409); the first job's result.txt stays one clean run.  A paused job is
+    superseded by a new construct, and resuming marks the old record 'resumed'."""
+    from cloud_server_amd.runtime.jobs import JobConflict
+    s = _settings(tmp_path, "thread")
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    jm = JobManager(s, db, executor="thread", ngpu=0)
+    try:
+        mdir = _prep_model(s, uid, "m")
+        cfg = dict(SMALL, iter=300, options=dict(SMALL["options"], log_every=20, ckpt_every=0))
+        jid = jm.submit(uid, "m", "file", cfg)
+        with pytest.raises(JobConflict):
+            jm.submit(uid, "m", "file", dict(cfg, iter=7))
+        assert json.load(open(os.path.join(mdir, "model.json")))["iter"] == 300     # not overwritten
+        other = jm.submit(uid, "m2", "file", dict(SMALL, iter=5))                  # other models are free
+        assert jm.wait(jid, 300) == "done" and jm.wait(other, 300) in ("done", "failed")
+        lines = open(os.path.join(mdir, RESULT)).read().splitlines()
+        steps = [int(l.split(",")[0].split(":")[1]) for l in lines if l.startswith("step:")]
+        assert steps == list(range(0, 300, 20))
+        assert sum(l.startswith("final_accuracy:") for l in lines) == 1
+        # paused -> a new construct supersedes it; resume of a paused job marks it resumed
+        jid2 = jm.submit(uid, "m", "file", dict(cfg, iter=100000))
+        t0 = time.time()
+        while (db.get_job(jid2)["state"] != "running" or not os.path.exists(os.path.join(mdir, STATUS))
+               or json.load(open(os.path.join(mdir, STATUS))).get("step", 0) <= 300) and time.time() - t0 < 120:
+            time.sleep(0.05)
+        jm.control(jid2, "pause")
+        assert jm.wait(jid2, 120) == "paused"
+        jid3 = jm.control(jid2, "resume")["job"]
+        assert db.get_job(jid2)["state"] == "resumed"
+        with pytest.raises(JobConflict):
+            jm.submit(uid, "m", "file", cfg)
+        jm.control(jid3, "pause")
+        assert jm.wait(jid3, 120) == "paused"
+        jid4 = jm.submit(uid, "m", "file", dict(cfg, iter=1))
+        assert db.get_job(jid3)["state"] == "stopped" and "superseded" in db.get_job(jid3)["error"]
+        assert jm.wait(jid4, 120) in ("done", "failed")
+    finally:
+        jm.shutdown()
