@@ -70,24 +70,54 @@ def decode_mnist_u8(img_bytes: bytes) -> np.ndarray:
         return np.asarray(im, dtype=np.uint8).reshape(-1)
 
 
+class BatcherClosed(RuntimeError):
+    """The batcher's model entry was replaced (newer checkpoint / LRU eviction)."""
+
+
 class _Batcher:
     """Micro-batching: one thread per (model, prep) takes the first queued request, then
-    every request already waiting (up to ``max_batch``) and runs them as ONE batch."""
+    every request already waiting (up to ``max_batch``) and runs them as ONE batch.
+
+    ``close`` and ``submit`` serialise on a lock: every request enqueued before the close
+    sentinel is still served, and a ``submit`` after ``close`` raises ``BatcherClosed``
+    (the caller re-resolves the model entry) instead of parking a Future behind the
+    sentinel of an exited thread."""
 
     def __init__(self, fn: Callable[[np.ndarray], np.ndarray], max_batch: int = 256):
         self.fn, self.max_batch = fn, max_batch
         self.q: "queue.Queue[Optional[Tuple[np.ndarray, Future]]]" = queue.Queue()
         self.batches = self.items = 0
+        self.closed = False
+        self._lk = threading.Lock()
         self.t = threading.Thread(target=self._loop, name="csa-infer-batch", daemon=True)
         self.t.start()
 
     def submit(self, x: np.ndarray) -> Future:
         f: Future = Future()
-        self.q.put((x, f))
+        with self._lk:
+            if self.closed:
+                raise BatcherClosed("model entry replaced")
+            self.q.put((x, f))
         return f
 
     def close(self) -> None:
-        self.q.put(None)
+        with self._lk:
+            if self.closed:
+                return
+            self.closed = True
+            self.q.put(None)
+
+    def _serve(self, items) -> None:
+        try:
+            out = self.fn(np.stack([x for x, _ in items]))
+            for (_, f), v in zip(items, out):
+                f.set_result(int(v))
+        except Exception as exc:            # every waiter sees the failure
+            for _, f in items:
+                if not f.done():
+                    f.set_exception(exc)
+        self.batches += 1
+        self.items += len(items)
 
     def _loop(self) -> None:
         while True:
@@ -105,16 +135,7 @@ class _Batcher:
                     stop = True
                     break
                 items.append(it)
-            try:
-                out = self.fn(np.stack([x for x, _ in items]))
-                for (_, f), v in zip(items, out):
-                    f.set_result(int(v))
-            except Exception as exc:            # every waiter sees the failure
-                for _, f in items:
-                    if not f.done():
-                        f.set_exception(exc)
-            self.batches += 1
-            self.items += len(items)
+            self._serve(items)
             if stop:
                 return
 
@@ -132,6 +153,13 @@ class _Entry:
     def __init__(self, net: DigitNet, cfg, hip):
         self.net, self.cfg, self.hip = net, cfg, hip
         self.batchers: Dict[str, _Batcher] = {}
+        self.retired = False
+
+    def retire(self) -> None:
+        """Dropped from the cache (caller holds the service lock): close its batchers."""
+        self.retired = True
+        for bt in self.batchers.values():
+            bt.close()
 
 
 class InferenceService:
@@ -179,14 +207,11 @@ class InferenceService:
             self.misses += 1
             # drop older checkpoints of the same model
             for k in [k for k in self._cache if k[0] == key[0]]:
-                for bt in self._cache[k].batchers.values():
-                    bt.close()
-                del self._cache[k]
+                self._cache.pop(k).retire()
             self._cache[key] = ent
             while len(self._cache) > self.capacity:
                 _, old = self._cache.popitem(last=False)
-                for bt in old.batchers.values():
-                    bt.close()
+                old.retire()
         return ent
 
     def _load(self, model_dir: str) -> Optional[DigitNet]:
@@ -213,10 +238,26 @@ class InferenceService:
 
     def _batcher(self, ent: _Entry, prep: str) -> _Batcher:
         with self._lock:
+            if ent.retired:
+                raise BatcherClosed("model entry replaced")
             b = ent.batchers.get(prep)
             if b is None:
                 b = ent.batchers[prep] = _Batcher(lambda xs, e=ent, p=prep: self._run_u8(e, xs, p))
             return b
+
+    def _submit(self, model_dir: str, x: np.ndarray, prep: str) -> Optional[Future]:
+        """Queue one decoded image on the current entry's batcher.  An entry replaced
+        between lookup and submit (a newer checkpoint loaded by another request) closed
+        its batchers: look the model up again and queue on the new entry."""
+        for _ in range(8):
+            ent = self._entry(model_dir)
+            if ent is None:
+                return None
+            try:
+                return self._batcher(ent, prep).submit(x)
+            except BatcherClosed:
+                continue
+        raise RuntimeError("model entry kept changing while submitting")
 
     @staticmethod
     def _decode(img_bytes: bytes, prep: str) -> np.ndarray:
@@ -242,10 +283,10 @@ class InferenceService:
             x = self._decode(img_bytes, prep)
         except Exception as exc:
             return {"result": "fail", "message": f"cannot decode image: {exc}"}
-        ent = self._entry(model_dir)
-        if ent is None:
+        fut = self._submit(model_dir, x, prep)
+        if fut is None:
             return dict(FAIL_NO_MODEL)
-        v = self._batcher(ent, prep).submit(x).result()
+        v = fut.result()
         self.lat.append(time.perf_counter() - t0)
         return {"result": "success", "message": str(int(v))}
 
@@ -259,10 +300,10 @@ class InferenceService:
             x = await run_in_threadpool(self._decode, img_bytes, prep)
         except Exception as exc:
             return {"result": "fail", "message": f"cannot decode image: {exc}"}
-        ent = await run_in_threadpool(self._entry, model_dir)
-        if ent is None:
+        fut = await run_in_threadpool(self._submit, model_dir, x, prep)
+        if fut is None:
             return dict(FAIL_NO_MODEL)
-        v = await asyncio.wrap_future(self._batcher(ent, prep).submit(x))
+        v = await asyncio.wrap_future(fut)
         self.lat.append(time.perf_counter() - t0)
         return {"result": "success", "message": str(int(v))}
 
@@ -286,6 +327,5 @@ class InferenceService:
     def close(self) -> None:
         with self._lock:
             for ent in self._cache.values():
-                for bt in ent.batchers.values():
-                    bt.close()
+                ent.retire()
             self._cache.clear()

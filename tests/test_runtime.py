@@ -484,3 +484,48 @@ def test_one_job_per_model_conflict_and_supersede(tmp_path):
         assert jm.wait(jid4, 120) in ("done", "failed")
     finally:
         jm.shutdown()
+
+
+def test_inference_reload_while_requests_in_flight(tmp_path):
+    """A newer checkpoint loaded by one request closes the old entry's batchers; requests
+    that resolved the old entry first must still complete (served by the old batcher or
+    re-queued on the new entry), never hang behind the close sentinel."""
+    import threading
+    from cloud_server_amd.serve.inference import BatcherClosed, _Batcher
+    mdir = str(tmp_path / "m")
+    os.makedirs(mdir)
+    data = _data()
+    run_job(mdir, dict(SMALL, iter=10), device="cpu", backend="torch", data=data)
+    svc = InferenceService(device="cpu")
+    b = io.BytesIO()
+    Image.fromarray(synthetic_mnist(1, seed=9).images[0].reshape(28, 28)).save(b, format="PNG")
+    img = b.getvalue()
+    assert svc.predict(mdir, img, prep="mnist")["result"] == "success"
+    stale = svc._entry(mdir)
+    out, errs = [], []
+
+    def client():
+        try:
+            for _ in range(20):
+                out.append(svc.predict(mdir, img, prep="mnist")["result"])
+        except Exception as exc:       # pragma: no cover - reported below
+            errs.append(exc)
+    ts = [threading.Thread(target=client) for _ in range(4)]
+    for t in ts:
+        t.start()
+    run_job(mdir, dict(SMALL, iter=20), device="cpu", backend="torch", data=data)   # newer ckpt
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts) and not errs, errs
+    assert out == ["success"] * 80
+    assert stale.retired and all(bt.closed for bt in stale.batchers.values())
+    with pytest.raises(BatcherClosed):                # a stale entry never grows a new batcher
+        svc._batcher(stale, "reference")
+    # submit after close fails fast; items queued before the close are still served
+    bt = _Batcher(lambda xs: xs[:, 0])
+    f = bt.submit(np.array([7], np.int64))
+    bt.close()
+    assert f.result(5) == 7
+    with pytest.raises(BatcherClosed):
+        bt.submit(np.array([1], np.int64))
+    svc.close()
