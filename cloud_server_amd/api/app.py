@@ -94,11 +94,26 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
     jobs = JobManager(settings, db, executor=executor, ngpu=ngpu)
     dev = inference_device or getattr(settings, "infer_device", "auto")
     if dev == "auto":
-        try:                        # device_count() does not initialise HIP on this image
-            dev = "cuda:0" if torch.cuda.device_count() > 0 else "cpu"
+        # the serving GPU: the last one (device_count() does not initialise HIP on this
+        # image); its scheduler slot is reserved below so packed training avoids it first
+        try:
+            n = torch.cuda.device_count()
         except Exception:
-            dev = "cpu"
-    infer = InferenceService(device=dev)
+            n = 0
+        dev = f"cuda:{max(min(n, jobs.ngpu) - 1, 0)}" if n > 0 and jobs.ngpu > 0 else "cpu"
+    serve_dev = torch.device(dev)
+    if serve_dev.type == "cuda":
+        serve_dev = torch.device("cuda", serve_dev.index or 0)
+        jobs.reserve_serving(serve_dev.index)
+    infer = InferenceService(device=str(serve_dev))
+
+    def on_serve_device(fn, *a, **kw):
+        """Run ``fn`` with the serving GPU current (GPU preprocessing opens no context on
+        another device of the API process)."""
+        if serve_dev.type != "cuda":
+            return fn(*a, **kw)
+        with torch.cuda.device(serve_dev):
+            return fn(*a, **kw)
 
     @contextlib.asynccontextmanager
     async def lifespan(_app):
@@ -497,7 +512,7 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
             if ops:
                 if not os.path.exists(tag):
                     return J({"message": "error", "detail": "upload tag.json first"}, 500)
-                await run_in_threadpool(pipeline.run, os.path.join(mdir, "data"), tag, ops,
+                await run_in_threadpool(on_serve_device, pipeline.run, os.path.join(mdir, "data"), tag, ops,
                                         backend=settings.preprocess_backend)
         except Exception as exc:
             return J({"message": "error", "detail": str(exc)}, 500)

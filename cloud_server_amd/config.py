@@ -19,7 +19,8 @@ local defaults.
 | CSA_CORS_ORIGINS      | (none)                          | comma list of allowed CORS origins ("*" = any) |
 | CSA_HEARTBEAT_S       | 900                             | a running job silent this long is killed + failed |
 | CSA_ENABLE_DEMO       | 0                               | mount the demo "bills" routes (off, as in the reference) |
-| CSA_INFER_DEVICE      | auto (cuda:0 when a GPU exists)  | device of the inference service (HIP forward) |
+| CSA_INFER_DEVICE      | auto (the last GPU when one exists) | device of the inference service (HIP forward) and GPU preprocessing |
+| CSA_SERVE_SLOTS       | 1                               | scheduler slots reserved on the serving GPU for the API process |
 | CSA_PACK_JOBS         | 1                               | single-GPU jobs on one GPU share a packed host process |
 | CSA_SLOTS_PER_GPU     | 4 packed / 1 unpacked           | concurrent jobs per GPU (profiles/r2_multitenant.md) |
 """
@@ -58,6 +59,7 @@ class Settings:
     infer_device: str = field(default_factory=lambda: _env("CSA_INFER_DEVICE", "auto"))
     pack_jobs: bool = field(default_factory=lambda: _env("CSA_PACK_JOBS", "1") == "1")
     slots_per_gpu: int = field(default_factory=lambda: int(_env("CSA_SLOTS_PER_GPU", "0")))
+    serve_slots: int = field(default_factory=lambda: int(_env("CSA_SERVE_SLOTS", "1")))
 
     def __post_init__(self):
         if not self.db_path:

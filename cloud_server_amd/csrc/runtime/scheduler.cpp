@@ -126,6 +126,18 @@ int csa_sched_release(void* h, int64_t job) {
   return freed;
 }
 
+// Pin `job` to one slot of GPU `gpu` outside the queue (the API server's resident
+// inference models and GPU preprocessing live there: their HBM and CU time is not a
+// training job's to take).  Returns 0, or -1 if the GPU id is bad or has no free slot.
+// `csa_sched_release(job)` frees it like any job.
+int csa_sched_reserve(void* h, int64_t job, int gpu) {
+  Sched& s = *static_cast<Sched*>(h);
+  std::lock_guard<std::mutex> lk(s.mu);
+  if (gpu < 0 || gpu >= s.ngpu || s.load[gpu] >= s.slots_per_gpu) return -1;
+  place(s, job, {gpu});
+  return 0;
+}
+
 // Remove a queued (not yet admitted) job.  Returns 1 if it was queued.
 int csa_sched_cancel(void* h, int64_t job) {
   Sched& s = *static_cast<Sched*>(h);

@@ -148,6 +148,20 @@ class JobManager:
         except Exception:
             return 0
 
+    SERVE_JOB = -1000          # scheduler owner id of the API process's serving slots
+
+    def reserve_serving(self, gpu: int) -> int:
+        """Take ``settings.serve_slots`` slots of GPU ``gpu`` for the API process (its
+        resident inference graphs and GPU preprocessing share that GPU with training), so
+        least-loaded placement steers jobs elsewhere.  Never takes a GPU's last slot.
+        Returns the number of slots reserved."""
+        n = int(getattr(self.settings, "serve_slots", 1) or 0)
+        if self.use_cpu or not 0 <= gpu < self.ngpu or n >= self.slots_per_gpu:
+            return 0
+        got = sum(1 for _ in range(n) if self.sched.reserve(self.SERVE_JOB, gpu))
+        self.serve_reserved = (gpu, got)
+        return got
+
     # ------------------------------------------------------------------ public API
     def submit(self, owner: int, model: str, datatype: str, config: Dict[str, Any],
                ngpus: int = 1, resume_of: Optional[int] = None) -> int:

@@ -18,9 +18,7 @@ from ..ops import build as _build
 
 class NativeScheduler:
     def __init__(self, ngpu: int, slots_per_gpu: int = 4, max_skip: int = 8):
-        path = _build.RUNTIME_LIB
-        if not os.path.exists(path):
-            _build.build_runtime()
+        path = _build.build_runtime()        # stamp-checked: rebuilds only a stale library
         lib = C.CDLL(path)
         lib.csa_sched_create.restype = C.c_void_p
         lib.csa_sched_create.argtypes = [C.c_int, C.c_int, C.c_int]
@@ -29,6 +27,7 @@ class NativeScheduler:
         lib.csa_sched_next.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int), C.c_int]
         lib.csa_sched_release.argtypes = [C.c_void_p, C.c_int64]
         lib.csa_sched_cancel.argtypes = [C.c_void_p, C.c_int64]
+        lib.csa_sched_reserve.argtypes = [C.c_void_p, C.c_int64, C.c_int]
         lib.csa_sched_load.argtypes = [C.c_void_p, C.c_int]
         lib.csa_sched_queued.argtypes = [C.c_void_p]
         self.lib = lib
@@ -56,6 +55,9 @@ class NativeScheduler:
 
     def cancel(self, job: int) -> bool:
         return bool(self.lib.csa_sched_cancel(self.h, job))
+
+    def reserve(self, job: int, gpu: int) -> bool:
+        return self.lib.csa_sched_reserve(self.h, job, gpu) == 0
 
     def load(self, gpu: int) -> int:
         return self.lib.csa_sched_load(self.h, gpu)
@@ -121,6 +123,14 @@ class PyScheduler:
                     del self._q[i]
                     return True
         return False
+
+    def reserve(self, job: int, gpu: int) -> bool:
+        with self._mu:
+            if not 0 <= gpu < self.ngpu or self._load[gpu] >= self.slots:
+                return False
+            self._load[gpu] += 1
+            self._owners[gpu].append(job)
+            return True
 
     def load(self, gpu: int) -> int:
         return self._load[gpu] if 0 <= gpu < self.ngpu else -1

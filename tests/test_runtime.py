@@ -529,3 +529,27 @@ def test_inference_reload_while_requests_in_flight(tmp_path):
     with pytest.raises(BatcherClosed):
         bt.submit(np.array([1], np.int64))
     svc.close()
+
+
+def test_scheduler_reserve_serving_slot():
+    """The API process's serving slot: least-loaded placement avoids that GPU first and
+    it never takes a GPU's last slot (runtime.jobs.JobManager.reserve_serving)."""
+    for S in (NativeScheduler, PyScheduler):
+        s = S(2, 2)
+        assert s.reserve(-1000, 1) and s.load(1) == 1
+        s.submit(1, 1); s.submit(2, 1); s.submit(3, 1); s.submit(4, 1)
+        assert s.next() == (1, [0]) and s.next() == (2, [0]) and s.next() == (3, [1])
+        assert s.next() is None and not s.reserve(-1000, 1) and not s.reserve(-1000, 7)
+        assert s.release(-1000) == 1 and s.next() == (4, [1])
+
+
+def test_job_manager_reserves_serving_slot(tmp_path):
+    s = _settings(tmp_path, "thread")
+    s.slots_per_gpu = 4
+    jm = JobManager(s, Database(s.db_path), executor="thread", ngpu=2)
+    try:
+        assert jm.reserve_serving(1) == 1 and jm.sched.load(1) == 1 and jm.sched.load(0) == 0
+        s.serve_slots = 4
+        assert jm.reserve_serving(0) == 0            # would take the GPU's last slot
+    finally:
+        jm.shutdown()
