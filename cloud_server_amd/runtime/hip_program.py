@@ -95,8 +95,12 @@ class Unit:
 class HipProgram:
     WGRAD_STRIPES = 16
 
-    def __init__(self, eng):
+    def __init__(self, eng, forward_only: bool = False):
+        """``forward_only``: the serving program (``serve.hip_infer``) — the same forward
+        launches over another engine's weights, with no gradient, optimizer, staging or
+        collective state (``eng`` then needs only cfg/device/model/flat/ctx/data/stream)."""
         self.e = eng
+        self.forward_only = forward_only
         self.lib = K.load(required=True)
         if eng.device.type != "cuda":
             raise Unsupported("HIP program needs a GPU device")
@@ -109,11 +113,15 @@ class HipProgram:
         self.sync_bn = bool(eng.model.sync_bn)
         self.W = eng.ctx.world if self.sync_bn else 1
         self.views = eng.model.state.views(eng.flat)
-        self.gviews = eng.model.state.views(eng.flat_grad)
+        self.gviews = {} if forward_only else eng.model.state.views(eng.flat_grad)
         self._lower()
         self._plan_fused()
         self._plan_pair()
         self._alloc()
+        self._plan_splits()
+        if forward_only:
+            self.staged = False
+            return
         self._plan_lowrank()
         self.zero_regions: List[torch.Tensor] = []
         self._collect_zero_regions()
@@ -273,7 +281,8 @@ class HipProgram:
         folds (``csa_head_part``).  Data parallel keeps the materialised gradients: they
         must be all-reduced before any update."""
         e, B = self.e, self.B
-        self.fused = (not e.ctx.enabled) and os.environ.get("CSA_FUSED_UPDATE", "1") == "1"
+        self.fused = (not e.ctx.enabled and not self.forward_only
+                      and os.environ.get("CSA_FUSED_UPDATE", "1") == "1")
         # measured on MI355X (profiles/r2_dense_fused.md): the row-group kernel (one
         # 1024-thread workgroup per 16 input features) replaces fc1's split-K pair + its
         # share of the flat optimizer (bench 0.1166 -> 0.1107 ms/step); CSA_FUSED_DENSE=0
@@ -455,6 +464,7 @@ class HipProgram:
     def _alloc(self) -> None:
         dev, B = self.e.device, self.B
         f32 = dict(device=dev, dtype=torch.float32)
+        fo = self.forward_only
         prev: Optional[Unit] = None
         for u in self.units:
             u.x = prev.y if prev is not None else None
@@ -473,8 +483,9 @@ class HipProgram:
                     R = self.lib.csa_bn_slab_rows()
                     u.bn_tab = torch.zeros(4, C_, **f32)
                     u.bn_slab = torch.zeros(R, 2, C_, **f32)
-                    u.bn_bslab = torch.zeros(R, 2, C_, **f32)
-                    u.bn_k = torch.zeros(2, C_, **f32)
+                    if not fo:
+                        u.bn_bslab = torch.zeros(R, 2, C_, **f32)
+                        u.bn_k = torch.zeros(2, C_, **f32)
             elif u.kind == "pool":
                 ph, pw = lp.out_shape.hw
                 u.y = torch.zeros(B, ph, pw, lp.out_shape.c, **f32)
@@ -487,10 +498,10 @@ class HipProgram:
                     u.argmax = torch.zeros(B, ph, pw, lp.out_shape.c, device=dev, dtype=torch.uint8)
                 else:
                     u.y = torch.zeros(B, oh, ow, lp.out_shape.c, **f32)
-                u.dc = torch.zeros(B, oh, ow, lp.out_shape.c, **f32)
+                u.dc = None if fo else torch.zeros(B, oh, ow, lp.out_shape.c, **f32)
             else:
                 u.y = torch.zeros(B, lp.spec.hidden, **f32)
-            u.dy = torch.zeros_like(u.y)
+            u.dy = None if fo else torch.zeros_like(u.y)
             # forward BN slab for the transform consuming this unit's output
             prev = u
         # forward stat slabs: the unit BEFORE a transform with norm produces the slab
@@ -503,6 +514,8 @@ class HipProgram:
                 tf.slab = torch.zeros(nslab, 2, src.y.shape[3], **f32)
                 tf.nslab = nslab
                 tf.count = float(B * ph * pw * self.W)
+                if fo:
+                    continue
                 # backward slab is produced by THIS unit's dgrad
                 C = src.y.shape[3]
                 if u.kind == "dense" and u.fused:
@@ -523,7 +536,7 @@ class HipProgram:
             # BatchNorm tables [mean | rstd | a | b][C] written once per step by the
             # bn_act_apply that materialises xt (the fused dense backward's epilogue reads
             # them instead of reducing the statistic slab again)
-            if u.kind == "dense" and u.fused:
+            if u.kind == "dense" and u.fused and not fo:
                 # partial input-gradient slabs + per-row-group arrival tickets when the
                 # kernel splits a row group over column blocks (the last arriver resets
                 # its ticket; zero-initialised here)
@@ -534,7 +547,7 @@ class HipProgram:
             u.in_tf.bn_tab = (torch.zeros(4, u.in_tf.slab.shape[2], **f32)
                               if u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") != "1"
                               else None)
-        self.dlast = self.units[-1].dy     # head input grad
+        self.dlast = self.units[-1].dy     # head input grad (None: forward only)
         self.idx = None
         if self.head_rg:
             K = self.dlast[0].numel()
@@ -546,6 +559,16 @@ class HipProgram:
             self.head_kw = K * 10
             self.head_mloss = torch.zeros(G, **f32)
             self.head_mcorr = torch.zeros(G, dtype=torch.int32, device=dev)
+
+    def _plan_splits(self) -> None:
+        """Split-K factor of each dense forward (> 1: its output is an atomic accumulator
+        that must start at zero)."""
+        B = self.B
+        for u in self.units:
+            if u.kind == "dense":
+                fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
+                u.splits_fwd = (self.lib.csa_dd_fwd_splits(B, fout, fin) if u.direct
+                                else self.lib.csa_dense_fwd_splits(B, fout, fin))
 
     def _collect_zero_regions(self) -> None:
         """Accumulators that must start every step at zero.  ``zero_regions`` are cleared
@@ -563,8 +586,6 @@ class HipProgram:
             lp = u.layer
             if u.kind == "dense":
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
-                u.splits_fwd = (self.lib.csa_dd_fwd_splits(B, fout, fin) if u.direct
-                                else self.lib.csa_dense_fwd_splits(B, fout, fin))
                 if u.splits_fwd > 1:
                     regs.append(u.y)
                 if u.fused:

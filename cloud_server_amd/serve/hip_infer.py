@@ -3,10 +3,19 @@
 Reference path (C25/C28, apps/construction/views.py:198-268 -> construct_inference.py:
 293-347): a fresh TF process per request, one image, argmax on ``/cpu:0``.
 
-Here a model's forward is the TRAINING program's forward (``HipProgram._forward``: the
-fused conv pair, BN-apply + activation folded into the consumers, MFMA dense layers) with
-BatchNorm on its running statistics, plus a logits GEMM and an argmax, captured ONCE per
-batch bucket into a HIP graph.  A request batch is:
+Here a model is loaded ONCE per (model, checkpoint) into a resident weight state — one
+``DigitNet`` holding the flat parameters and the BatchNorm running statistics on the
+serving GPU — and every batch bucket runs the training program's forward
+(``HipProgram(forward_only=True)``: the fused conv pair, BN-apply + activation folded
+into the consumers, MFMA dense layers) over THOSE weights, plus a logits GEMM and an
+argmax.  A bucket owns only its activations and its I/O staging; there is no gradient,
+optimizer or batch-stream state anywhere on the serving path.
+
+Every bucket of both preps is captured into a HIP graph when the model loads, in
+``thread_local`` capture mode and under a process-wide capture lock — never lazily on a
+request thread — so concurrent GPU work from other threads of the API process (another
+model's batcher, GPU preprocessing) can neither invalidate a capture nor be broken by
+one.  A request batch is:
 
     pinned host staging -> H2D (one copy) -> graph replay -> D2H of the [n] argmax
 
@@ -19,15 +28,21 @@ from __future__ import annotations
 
 import dataclasses
 import threading
+from types import SimpleNamespace
 from typing import Dict, List, Optional
 
 import numpy as np
 import torch
 
-from ..data.datasets import ArrayDataset
 from ..models.dsl import TrainConfig
 
 BUCKETS = (1, 4, 16, 64, 256)
+PREPS = ("reference", "mnist")
+
+# graph captures in this process are serialised (thread_local mode keeps other threads'
+# unrelated GPU calls legal during a capture; the lock keeps two captures from sharing
+# the allocator's capture pools)
+CAPTURE_LOCK = threading.Lock()
 
 
 def bucket_for(n: int) -> int:
@@ -37,102 +52,140 @@ def bucket_for(n: int) -> int:
     return BUCKETS[-1]
 
 
-class _Bucket:
-    """One captured forward of ``B`` rows for one prep kind."""
+class ServeState:
+    """A model's resident forward state on one device: flat weights + BN running stats."""
 
-    def __init__(self, cfg: TrainConfig, state: Dict[str, torch.Tensor], B: int, device: torch.device,
-                 prep: str):
-        from ..runtime.engine import TrainEngine
+    def __init__(self, cfg: TrainConfig, state: Dict[str, torch.Tensor], device: torch.device):
+        from ..models.cnn import DigitNet
+        self.cfg, self.device = cfg, device
+        self.model = DigitNet(cfg.plan(), device=device, seed=cfg.seed, bn_mode=cfg.bn_mode)
+        self.model.import_state(state)
+        self.model.eval()
+        self.flat = self.model.flat.data
+
+
+class _FwdEngine:
+    """The engine surface ``HipProgram(forward_only=True)`` reads: config, device, the
+    shared model/weights, a disabled distributed context, and a dataset/stream of ``B``
+    rows that are simply the bucket's input buffer (row r reads input r)."""
+
+    def __init__(self, st: ServeState, B: int):
+        from ..parallel.dist import DistContext
+        dev = st.device
+        self.cfg = dataclasses.replace(st.cfg, batch_size=B)
+        self.device, self.model, self.flat = dev, st.model, st.flat
+        self.flat_grad = None
+        self.ctx = DistContext(device=dev)
+        self.data = SimpleNamespace(images=torch.zeros(B, 784, dtype=torch.uint8, device=dev),
+                                    labels=torch.zeros(B, dtype=torch.int64, device=dev))
+        self.stream = SimpleNamespace(rows=torch.arange(B, device=dev).view(1, B),
+                                      cursor=torch.zeros(1, dtype=torch.int64, device=dev), wrap=1)
+
+
+class _Bucket:
+    """One captured forward of ``B`` rows for one prep kind over a shared ServeState."""
+
+    def __init__(self, st: ServeState, B: int, prep: str):
         from ..runtime.hip_program import HipProgram
         from ..ops import fused as K
-        self.B, self.prep, self.device = B, prep, device
-        dummy = ArrayDataset(np.zeros((B, 784), np.uint8), np.zeros(B, np.int64))
-        c = dataclasses.replace(cfg, batch_size=B)
-        self.eng = eng = TrainEngine(c, dummy, device=device, backend="hip", use_graph=False)
-        if not isinstance(eng.program, HipProgram):
-            raise RuntimeError(f"no HIP lowering: {eng.fallback_reason}")
-        eng.model.import_state(state)
-        eng.model.eval()
-        eng.stream.rows[0].copy_(torch.arange(B, device=device))    # row r reads input r
-        eng.stream.cursor.zero_()
-        self.logits = torch.zeros(B, 10, device=device)
-        self.pred = torch.zeros(B, dtype=torch.int64, device=device)
-        # host staging (pinned) and its device twin
-        shape = (B, 400) if prep == "reference" else (B, 784)
-        self.h_in = torch.zeros(shape, dtype=torch.uint8, pin_memory=True)
-        self.d_in = torch.zeros(shape, dtype=torch.uint8, device=device)
-        self.h_out = torch.zeros(B, dtype=torch.int64, pin_memory=True)
-        self._lib = K
         from ..preprocess import gpu as G
-        self._G = G
-        self.graph = None
+        self.B, self.prep, self.device = B, prep, st.device
+        self.eng = _FwdEngine(st, B)
+        self.program = HipProgram(self.eng, forward_only=True)
+        dev = st.device
+        self.logits = torch.zeros(B, 10, device=dev)
+        self.pred = torch.zeros(B, dtype=torch.int64, device=dev)
+        shape = (B, 400) if prep == "reference" else (B, 784)
+        self.h_in = torch.zeros(shape, dtype=torch.uint8, pin_memory=True)   # host staging
+        self.d_in = torch.zeros(shape, dtype=torch.uint8, device=dev)
+        self.h_out = torch.zeros(B, dtype=torch.int64, pin_memory=True)
+        self._K, self._G = K, G
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
         self._capture()
 
     def _body(self) -> None:
         img = self.eng.data.images
         if self.prep == "reference":
             rc = self._G._lib().csa_img_infer_prep_u8(self.d_in.data_ptr(), img.data_ptr(), self.B,
-                                                      self._lib.stream())
+                                                      self._K.stream())
             if rc != 0:
                 raise RuntimeError(f"csa_img_infer_prep_u8 failed: {rc}")
         else:
             img.copy_(self.d_in)
-        self.eng.program.predict_logits_into(self.logits)
+        self.program.predict_logits_into(self.logits)
         torch.argmax(self.logits, dim=1, out=self.pred)
 
     def _capture(self) -> None:
-        s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            self._body()                      # warm-up (library init, allocator)
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body()
-        self.graph = g
+        with CAPTURE_LOCK:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._body()                      # warm-up (library init, lazy buffers)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._body()
+            self.graph = g
 
-    def run(self, x: np.ndarray) -> np.ndarray:
-        """``x`` uint8 [n, 400] (reference: 20x20 decoded) or [n, 784] (mnist), n <= B."""
+    def logits_u8(self, x: np.ndarray) -> torch.Tensor:
+        """Replay on ``x`` (n <= B rows) and return the [n, 10] logits (device tensor, a
+        view of this bucket's output: copy before the next replay)."""
         n = x.shape[0]
         self.h_in[:n].numpy()[...] = x
         if n < self.B:
             self.h_in[n:].zero_()
         self.d_in.copy_(self.h_in, non_blocking=True)
         self.graph.replay()
+        return self.logits[:n]
+
+    def run(self, x: np.ndarray) -> np.ndarray:
+        """``x`` uint8 [n, 400] (reference: 20x20 decoded) or [n, 784] (mnist), n <= B."""
+        n = x.shape[0]
+        self.logits_u8(x)
         self.h_out.copy_(self.pred, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         return self.h_out[:n].numpy().copy()
 
 
 class HipPredictor:
-    """All buckets of one (model, checkpoint): built lazily, one lock (one stream)."""
+    """Every bucket of one (model, checkpoint), captured at construction; one lock."""
 
-    def __init__(self, cfg: TrainConfig, state: Dict[str, torch.Tensor], device: torch.device):
-        self.cfg, self.state, self.device = cfg, state, device
-        self._buckets: Dict[tuple, _Bucket] = {}
+    def __init__(self, cfg: TrainConfig, state: Dict[str, torch.Tensor], device: torch.device,
+                 buckets=BUCKETS, preps=PREPS):
+        self.cfg, self.device = cfg, device
         self.lock = threading.Lock()
+        with torch.cuda.device(device):
+            self.state = ServeState(cfg, state, device)
+            self._buckets: Dict[tuple, _Bucket] = {(B, p): _Bucket(self.state, B, p)
+                                                   for B in buckets for p in preps}
+        self.buckets = tuple(buckets)
+
+    def _bucket(self, n: int, prep: str) -> _Bucket:
+        for B in self.buckets:
+            if n <= B:
+                return self._buckets[(B, prep)]
+        return self._buckets[(self.buckets[-1], prep)]
 
     def predict_u8(self, x: np.ndarray, prep: str) -> np.ndarray:
         out: List[np.ndarray] = []
         with self.lock, torch.cuda.device(self.device):
-            i = 0
+            i, cap = 0, self.buckets[-1]
             while i < x.shape[0]:
-                n = min(x.shape[0] - i, BUCKETS[-1])
-                B = bucket_for(n)
-                key = (B, prep)
-                b = self._buckets.get(key)
-                if b is None:
-                    b = self._buckets[key] = _Bucket(self.cfg, self.state, B, self.device, prep)
-                out.append(b.run(x[i:i + n]))
+                n = min(x.shape[0] - i, cap)
+                out.append(self._bucket(n, prep).run(x[i:i + n]))
                 i += n
         return np.concatenate(out) if out else np.zeros(0, np.int64)
 
+    def logits_u8(self, x: np.ndarray, prep: str) -> np.ndarray:
+        """[n, 10] fp32 logits of ``x`` (n <= the largest bucket): the numerics check."""
+        with self.lock, torch.cuda.device(self.device):
+            return self._bucket(x.shape[0], prep).logits_u8(x).cpu().numpy()
+
 
 def try_build(cfg: TrainConfig, state: Dict[str, torch.Tensor], device: torch.device) -> Optional[HipPredictor]:
-    """A HIP predictor when the device is a GPU and the net lowers to the HIP kernels."""
+    """A HIP predictor when the device is a GPU and the net lowers to the HIP kernels
+    (raises ``Unsupported`` otherwise; the caller falls back to the eager forward)."""
     if device.type != "cuda":
         return None
-    p = HipPredictor(cfg, state, device)
-    p.predict_u8(np.zeros((1, 400), np.uint8), "reference")      # raises if it cannot lower
-    return p
+    return HipPredictor(cfg, state, device)

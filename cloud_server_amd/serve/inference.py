@@ -173,9 +173,18 @@ class InferenceService:
         self.use_hip = use_hip
         self._cache: "OrderedDict[Tuple[str, int], _Entry]" = OrderedDict()
         self._lock = threading.Lock()
+        self._loading: Dict[str, threading.Lock] = {}
         self.hits = self.misses = 0
         self.lat = deque(maxlen=20000)      # server-side seconds per request (decode -> digit)
         self.hip_error = ""
+
+    def _lookup(self, key) -> Optional[_Entry]:
+        with self._lock:
+            ent = self._cache.get(key)
+            if ent is not None:
+                self._cache.move_to_end(key)
+                self.hits += 1
+            return ent
 
     def _entry(self, model_dir: str) -> Optional[_Entry]:
         last = ckpt.latest(model_dir)
@@ -183,12 +192,28 @@ class InferenceService:
             return None
         step, path = last
         key = (os.path.abspath(model_dir), step)
+        ent = self._lookup(key)
+        if ent is not None:
+            return ent
         with self._lock:
-            ent = self._cache.get(key)
+            load_lock = self._loading.setdefault(key[0], threading.Lock())
+        with load_lock:                      # one load (and one set of captures) per model
+            ent = self._lookup(key)
             if ent is not None:
-                self._cache.move_to_end(key)
-                self.hits += 1
                 return ent
+            ent = self._load_entry(path)
+            with self._lock:
+                self.misses += 1
+                # drop older checkpoints of the same model
+                for k in [k for k in self._cache if k[0] == key[0]]:
+                    self._cache.pop(k).retire()
+                self._cache[key] = ent
+                while len(self._cache) > self.capacity:
+                    _, old = self._cache.popitem(last=False)
+                    old.retire()
+        return ent
+
+    def _load_entry(self, path: str) -> _Entry:
         obj = ckpt.load(path)
         cfg = parse_train_config(json.loads(obj["config"]))
         net = DigitNet(cfg.plan(), device=self.device, bn_mode=cfg.bn_mode)
@@ -202,17 +227,7 @@ class InferenceService:
             except Exception as exc:        # outside the HIP family: eager torch forward
                 self.hip_error = repr(exc)
                 hip = None
-        ent = _Entry(net, cfg, hip)
-        with self._lock:
-            self.misses += 1
-            # drop older checkpoints of the same model
-            for k in [k for k in self._cache if k[0] == key[0]]:
-                self._cache.pop(k).retire()
-            self._cache[key] = ent
-            while len(self._cache) > self.capacity:
-                _, old = self._cache.popitem(last=False)
-                old.retire()
-        return ent
+        return _Entry(net, cfg, hip)
 
     def _load(self, model_dir: str) -> Optional[DigitNet]:
         ent = self._entry(model_dir)
