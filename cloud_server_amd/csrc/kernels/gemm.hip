@@ -652,3 +652,178 @@ CSA_API int csa_dense_bwd(const float* dY, const float* W, float* dX, int M, int
   if (rc) return -rc;
   return grid_slabs(pd, M, Kin);
 }
+
+// ===================================================================================
+// Wide convolutions as implicit GEMMs on the same f32 MFMA body.
+//
+// The direct conv kernels (conv.hip, conv_pair.hip) keep a conv's weights and BatchNorm
+// tables in LDS, which bounds them to <= 128 channels.  The DSL accepts any
+// filter:[kh, kw, cout] (construct_distribute.py:222-233), so a conv with more channels
+// runs as three GEMMs whose operands are gathered on the fly by loader functors — no
+// im2col buffer is ever materialised:
+//   forward  Z[m = (b,oy,ox)][co]   = im2col(X)[m][k = (i,j,ci)] @ W[k][co] (+ bias)
+//   wgrad    dW[k][co] (+db)        = im2col(X)^T @ dZ           (ones row -> db)
+//   dgrad    dX[p = (b,y,x)][ci]    = dZ~[p][k' = (i,j,co)] @ W~[k'][ci]
+// where dZ~ gathers dZ[b][(y+PT-i)/SH][(x+PL-j)/SW][co] (zero unless the division is
+// exact and in range) and W~[k'][ci] = W[i][j][ci][co].  HWIO weights make k = (i,j,ci)
+// row-major exactly the im2col order.  Activation / pool / BatchNorm around a wide conv
+// run as standalone units (norm_pool.hip), so these GEMMs carry no transforms.
+// ===================================================================================
+namespace csa {
+
+struct GConvGeom { int B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout; };
+
+// im2col(X)[m][k].  T = false: elem(r = m, c = k) (forward A, K contiguous in ci);
+// T = true: elem(r = k, c = m) (weight-gradient A; ONES: row k == Kd reads 1 -> db).
+template <bool T, bool ONES = false>
+struct LoadIm2col {
+  const float* x; GConvGeom g; FastDiv dOW, dOHW, dCin, dKW; int M, Kd;
+  static constexpr bool KCONTIG = !T;
+  static constexpr bool VEC4 = false;
+  __device__ float4 raw4(int, int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void bind(const BNTables&) {}
+  __device__ __forceinline__ long addr(int m, int k, bool& ok) const {
+    int b, pix, oy, ox, tap, ci, i, j;
+    dOHW.divmod(m, b, pix);
+    dOW.divmod(pix, oy, ox);
+    dCin.divmod(k, tap, ci);
+    dKW.divmod(tap, i, j);
+    const int yy = oy * g.SH - g.PT + i, xx = ox * g.SW - g.PL + j;
+    ok = m < M && k < Kd && yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
+    return ok ? (((long)b * g.H + yy) * g.W + xx) * g.Cin + ci : 0;
+  }
+  __device__ float raw(int r, int c) const {
+    bool ok;
+    return x[addr(T ? c : r, T ? r : c, ok)];
+  }
+  __device__ float post(float v, int r, int c) const {
+    const int m = T ? c : r, k = T ? r : c;
+    if (ONES && k == Kd) return m < M ? 1.f : 0.f;
+    bool ok;
+    addr(m, k, ok);
+    return ok ? v : 0.f;
+  }
+};
+
+// dZ~[p][k'] for the input gradient: p = (b, y, x) input pixel, k' = (i, j, co).
+struct LoadConvDZ {
+  const float* dz; GConvGeom g; FastDiv dW, dHW, dCout, dKW; int P, Kd;
+  static constexpr bool KCONTIG = true;
+  static constexpr bool VEC4 = false;
+  __device__ float4 raw4(int, int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void bind(const BNTables&) {}
+  __device__ __forceinline__ long addr(int p, int k, bool& ok) const {
+    int b, pix, y, x, tap, co, i, j;
+    dHW.divmod(p, b, pix);
+    dW.divmod(pix, y, x);
+    dCout.divmod(k, tap, co);
+    dKW.divmod(tap, i, j);
+    const int ty = y + g.PT - i, tx = x + g.PL - j;
+    const int oy = ty / g.SH, ox = tx / g.SW;     // only used when ty, tx >= 0 and exact
+    ok = p < P && k < Kd && ty >= 0 && tx >= 0 && oy * g.SH == ty && ox * g.SW == tx &&
+         oy < g.OH && ox < g.OW;
+    return ok ? (((long)b * g.OH + oy) * g.OW + ox) * g.Cout + co : 0;
+  }
+  __device__ float raw(int r, int c) const {
+    bool ok;
+    return dz[addr(r, c, ok)];
+  }
+  __device__ float post(float v, int r, int c) const {
+    bool ok;
+    addr(r, c, ok);
+    return ok ? v : 0.f;
+  }
+};
+
+// W~[k' = (i,j,co)][ci] = W[i][j][ci][co], read as elem(r = ci, c = k') (K contiguous in co).
+struct LoadConvWT {
+  const float* w; int Cin, Cout, Kd; FastDiv dCout;
+  static constexpr bool KCONTIG = true;
+  static constexpr bool VEC4 = false;
+  __device__ float4 raw4(int, int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void bind(const BNTables&) {}
+  __device__ __forceinline__ long addr(int ci, int k, bool& ok) const {
+    int tap, co;
+    dCout.divmod(k, tap, co);
+    ok = ci < Cin && k < Kd;
+    return ok ? ((long)tap * Cin + ci) * Cout + co : 0;
+  }
+  __device__ float raw(int r, int c) const {
+    bool ok;
+    return w[addr(r, c, ok)];
+  }
+  __device__ float post(float v, int r, int c) const { return (r < Cin && c < Kd) ? v : 0.f; }
+};
+
+static bool gconv_ok(const GConvGeom& g) {
+  const long M = (long)g.B * g.OH * g.OW, P = (long)g.B * g.H * g.W;
+  const long K1 = (long)g.KH * g.KW * g.Cin, K2 = (long)g.KH * g.KW * g.Cout;
+  // FastDiv is exact below 2^22; the launch grid is one 32-bit dimension
+  return g.B > 0 && g.Cin > 0 && g.Cout > 0 && g.KH > 0 && g.KW > 0 && g.SH > 0 && g.SW > 0 &&
+         g.OH > 0 && g.OW > 0 && M < (1 << 22) && P < (1 << 22) && K1 < (1 << 22) && K2 < (1 << 22);
+}
+
+static GConvGeom gconv_geom(const int* v) {
+  return GConvGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12]};
+}
+
+}  // namespace csa
+
+// geom = [B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout] (as csa_conv_fwd)
+CSA_API int csa_gconv_fwd_splits(const int* geom) {
+  const GConvGeom g = gconv_geom(geom);
+  return plan_gemm(g.B * g.OH * g.OW, g.Cout, g.KH * g.KW * g.Cin, true).splits;
+}
+
+// Z[B][OH][OW][Cout] (+)= conv(X) + bias.  Z zeroed by the caller when splits > 1.
+CSA_API int csa_gconv_fwd(const float* X, const float* W, const float* bias, float* Z, const int* geom,
+                          hipStream_t st) {
+  const GConvGeom g = gconv_geom(geom);
+  if (!gconv_ok(g)) return -1;
+  const int M = g.B * g.OH * g.OW, N = g.Cout, K = g.KH * g.KW * g.Cin;
+  const Plan p = plan_gemm(M, N, K, true);
+  const LoadIm2col<false> la{X, g, FastDiv(g.OW), FastDiv(g.OH * g.OW), FastDiv(g.Cin), FastDiv(g.KW), M, K};
+  const LoadColMajor<false> lb{W, (long)N, N, K};                 // B(k, n) = W[k][n]
+  const EpiStore epi{Z, (long)N, M, N, bias, p.splits > 1, nullptr, 1.f};
+  return launch_gemm(p, la, lb, epi, M, N, K, BNRef{}, 0, nullptr, 0, st);
+}
+
+CSA_API int csa_gconv_wgrad_splits(const int* geom, int has_bias) {
+  const GConvGeom g = gconv_geom(geom);
+  return plan_gemm(g.KH * g.KW * g.Cin + (has_bias ? 1 : 0), g.Cout, g.B * g.OH * g.OW, true).splits;
+}
+
+// dW[KH*KW*Cin][Cout] (+)= im2col(X)^T @ dZ * scale, db (+)= colsum(dZ) * scale.
+// Accumulated with atomics when split (caller zeroes dW / db, see *_splits).
+CSA_API int csa_gconv_wgrad(const float* X, const float* dZ, float* dW, float* db, const int* geom,
+                            float scale, hipStream_t st) {
+  const GConvGeom g = gconv_geom(geom);
+  if (!gconv_ok(g)) return -1;
+  const int M = g.B * g.OH * g.OW, Kd = g.KH * g.KW * g.Cin, N = g.Cout;
+  const int Mg = Kd + (db ? 1 : 0);
+  const Plan p = plan_gemm(Mg, N, M, true);
+  const LoadColMajor<false> lb{dZ, (long)N, N, M};                // B(k = m, n) = dZ[m][n]
+  const EpiStore epi{dW, (long)N, Kd, N, nullptr, p.splits > 1, db, scale};
+  const FastDiv a(g.OW), b(g.OH * g.OW), c(g.Cin), d(g.KW);
+  if (db) return launch_gemm(p, LoadIm2col<true, true>{X, g, a, b, c, d, M, Kd}, lb, epi, Mg, N, M,
+                             BNRef{}, 0, nullptr, 0, st);
+  return launch_gemm(p, LoadIm2col<true>{X, g, a, b, c, d, M, Kd}, lb, epi, Mg, N, M, BNRef{}, 0, nullptr,
+                     0, st);
+}
+
+CSA_API int csa_gconv_dgrad_splits(const int* geom) {
+  const GConvGeom g = gconv_geom(geom);
+  return plan_gemm(g.B * g.H * g.W, g.Cin, g.KH * g.KW * g.Cout, true).splits;
+}
+
+// dX[B][H][W][Cin] (+)= conv-transpose(dZ).  dX zeroed by the caller when splits > 1.
+CSA_API int csa_gconv_dgrad(const float* dZ, const float* W, float* dX, const int* geom, hipStream_t st) {
+  const GConvGeom g = gconv_geom(geom);
+  if (!gconv_ok(g)) return -1;
+  const int P = g.B * g.H * g.W, N = g.Cin, K = g.KH * g.KW * g.Cout;
+  const Plan p = plan_gemm(P, N, K, true);
+  const LoadConvDZ la{dZ, g, FastDiv(g.W), FastDiv(g.H * g.W), FastDiv(g.Cout), FastDiv(g.KW), P, K};
+  const LoadConvWT lb{W, g.Cin, g.Cout, K, FastDiv(g.Cout)};
+  const EpiStore epi{dX, (long)N, P, N, nullptr, p.splits > 1, nullptr, 1.f};
+  return launch_gemm(p, la, lb, epi, P, N, K, BNRef{}, 0, nullptr, 0, st);
+}

@@ -83,6 +83,13 @@ _SIGS = {
     "csa_dd_dgrad_slabs": (I, []),
     "csa_dd_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P]),
     "csa_dd_wgrad": (I, [P, P, I, I, I, I, F, F, P, P, P, P, P, P, P, P, I, F, P, P]),
+    # wide convolutions (> 128 channels) as implicit MFMA GEMMs (gemm.hip)
+    "csa_gconv_fwd_splits": (I, [P]),
+    "csa_gconv_fwd": (I, [P, P, P, P, P, P]),
+    "csa_gconv_wgrad_splits": (I, [P, I]),
+    "csa_gconv_wgrad": (I, [P, P, P, P, P, F, P]),
+    "csa_gconv_dgrad_splits": (I, [P]),
+    "csa_gconv_dgrad": (I, [P, P, P, P, P]),
     # standalone BatchNorm / activation / max-pool units (norm_pool.hip)
     "csa_bn_slab_rows": (I, []),
     "csa_bn_stats": (I, [P, L, I, P, I, P]),

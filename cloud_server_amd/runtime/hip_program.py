@@ -18,6 +18,11 @@ max-pool routing; ``csa_conv_dgrad``; ``csa_conv_wgrad`` as an implicit MFMA GEM
 then gradient all-reduce (data parallel) and ONE fused optimizer launch which also
 zeroes next step's atomic accumulators and updates BN running statistics.
 
+A conv with more than 128 input or output channels (beyond the direct kernels' LDS
+tables) is a **gconv unit**: forward, input gradient and weight gradient as implicit
+MFMA GEMMs whose loaders gather the im2col / transposed operands on the fly
+(``csa_gconv_*`` in gemm.hip); its activation, pool and norm run as standalone units.
+
 Layer orders the consumer transform cannot express — a 2-D norm after a dense layer, a
 norm over > 128 channels or directly before the head, a pool that does not directly
 follow a conv, act/norm sequences like ``act norm`` — become **standalone units**
@@ -74,7 +79,7 @@ class Transform:
 
 @dataclass
 class Unit:
-    kind: str                               # "conv" | "dense"
+    kind: str                               # "conv" | "dense" | "gconv" | "bn" | "pool"
     layer: LayerPlan
     act: Optional[ActSpec] = None           # conv: fused output act
     pool: Optional[LayerPlan] = None        # conv: fused pool
@@ -414,10 +419,15 @@ class HipProgram:
         while i < len(layers):
             lp = layers[i]
             sp = lp.spec
+            if isinstance(sp, ConvSpec) and (lp.in_shape.c > 128 or sp.cout > 128):
+                # wide conv: implicit-GEMM unit on a materialised input; the act / pool /
+                # norm after it become standalone units
+                materialise()
+                units.append(Unit("gconv", lp))
+                i += 1
+                continue
             if isinstance(sp, (ConvSpec, DenseSpec)):
                 kind = "conv" if isinstance(sp, ConvSpec) else "dense"
-                if kind == "conv" and (lp.in_shape.c > 128 or sp.cout > 128):
-                    raise Unsupported("conv with more than 128 channels")   # conv.hip tiling
                 tf = as_transform(kind)
                 if tf is None:
                     materialise()
@@ -490,6 +500,9 @@ class HipProgram:
                 ph, pw = lp.out_shape.hw
                 u.y = torch.zeros(B, ph, pw, lp.out_shape.c, **f32)
                 u.argmax = torch.zeros(B, ph, pw, lp.out_shape.c, device=dev, dtype=torch.uint8)
+            elif u.kind == "gconv":
+                oh, ow = lp.out_shape.hw
+                u.y = torch.zeros(B, oh, ow, lp.spec.cout, **f32)
             elif u.kind == "conv":
                 oh, ow = lp.out_shape.hw
                 if u.pool is not None:
@@ -569,6 +582,8 @@ class HipProgram:
                 fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
                 u.splits_fwd = (self.lib.csa_dd_fwd_splits(B, fout, fin) if u.direct
                                 else self.lib.csa_dense_fwd_splits(B, fout, fin))
+            elif u.kind == "gconv":
+                u.splits_fwd = self.lib.csa_gconv_fwd_splits(self._conv_geom(u.layer, B))
 
     def _collect_zero_regions(self) -> None:
         """Accumulators that must start every step at zero.  ``zero_regions`` are cleared
@@ -601,6 +616,16 @@ class HipProgram:
                 if self.lib.csa_dense_wgrad_splits(B, fin, fout) > 1:
                     flat.append(self.gviews[f"{lp.name}.weight"].view(-1))
                     flat.append(self.gviews[f"{lp.name}.bias"])
+            elif u.kind == "gconv":
+                geom = self._conv_geom(lp, B)
+                if u.splits_fwd > 1:
+                    regs.append(u.y.view(-1))
+                if k > 0 and self.lib.csa_gconv_dgrad_splits(geom) > 1:
+                    regs.append(self.units[k - 1].dy.view(-1))
+                if self.lib.csa_gconv_wgrad_splits(geom, int(bool(lp.spec.bias))) > 1:
+                    flat.append(self.gviews[f"{lp.name}.weight"].view(-1))
+                    if lp.spec.bias:
+                        flat.append(self.gviews[f"{lp.name}.bias"])
             elif u.kind == "bn":
                 if u.norm is not None:        # atomic stat rows (forward and backward)
                     regs += [u.bn_slab.view(-1), u.bn_bslab.view(-1)]
@@ -800,6 +825,10 @@ class HipProgram:
                 self._standalone_bwd(u, self.units[k - 1] if k > 0 else None, st)
                 self._grad_ready(k)
                 continue
+            if u.kind == "gconv":
+                self._gconv_bwd(u, self.units[k - 1] if k > 0 else None, st)
+                self._grad_ready(k)
+                continue
             lp, tf = u.layer, u.in_tf
             bn = self._bn_args(tf)
             in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
@@ -948,6 +977,9 @@ class HipProgram:
             if u.kind in ("bn", "pool"):
                 self._standalone_fwd(u, st)
                 continue
+            if u.kind == "gconv":
+                self._gconv_fwd(u, st)
+                continue
             lp, tf = u.layer, u.in_tf
             bn = self._bn_args(tf)
             in_act, in_alpha = _act_id(tf.act), _alpha(tf.act)
@@ -1034,6 +1066,25 @@ class HipProgram:
                                          float(self.model.bn_momentum), 0, K.ptr(u.bn_tab), st), "bn_finalize")
         self._rc(lib.csa_bn_apply(K.ptr(u.x), K.ptr(u.y), n, C_, K.ptr(u.bn_tab), act, alpha, st), "bn_apply")
 
+    def _gconv_fwd(self, u: Unit, st) -> None:
+        lp = u.layer
+        V = self.views
+        self._rc(self.lib.csa_gconv_fwd(
+            K.ptr(u.x), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]) if lp.spec.bias else None,
+            K.ptr(u.y), self._conv_geom(lp, self.B), st), "gconv_fwd")
+
+    def _gconv_bwd(self, u: Unit, prev: Optional[Unit], st) -> None:
+        """Input gradient (reads the pre-update weights) then weight gradient."""
+        lp = u.layer
+        geom = self._conv_geom(lp, self.B)
+        if prev is not None:
+            self._rc(self.lib.csa_gconv_dgrad(K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]),
+                                              K.ptr(prev.dy), geom, st), "gconv_dgrad")
+        G = self.gviews
+        self._rc(self.lib.csa_gconv_wgrad(
+            K.ptr(u.x), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]) if lp.spec.bias else None,
+            geom, 1.0, st), "gconv_wgrad")
+
     def _standalone_bwd(self, u: Unit, prev: Optional[Unit], st) -> None:
         lib = self.lib
         dx = prev.dy if prev is not None else None
@@ -1076,7 +1127,7 @@ class HipProgram:
         # split-K forward outputs (and, with batch statistics, the forward BN slabs) are
         # atomic accumulators that the training step's optimizer launch re-zeroes
         for u in self.units:
-            if u.kind == "dense" and u.splits_fwd > 1:
+            if u.kind in ("dense", "gconv") and u.splits_fwd > 1:
                 u.y.zero_()
             if not self._eval_bn and u.in_tf.has_bn:
                 u.in_tf.slab.zero_()

@@ -119,9 +119,32 @@ CASES = {
         {"layer": "pool"},
         {"layer": "connect", "hidden": 32},
     ],
+    # > 128 channels (construct_distribute.py:222-233 takes any filter): implicit-GEMM
+    # gconv units with standalone act / pool / norm, next to direct convs
+    "wide_conv_192": [
+        {"layer": "conv", "filter": [3, 3, 192], "isBias": "True", "stride": [2, 2]},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool"},
+        {"layer": "conv", "filter": [2, 2, 16]},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "connect", "hidden": 32},
+    ],
+    "wide_conv_chain": [
+        {"layer": "conv", "filter": [3, 3, 8], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool"},
+        {"layer": "conv", "filter": [3, 3, 160], "padding": "VALID"},
+        {"layer": "norm"},
+        {"layer": "active", "active_func": "leaky_relu"},
+        {"layer": "conv", "filter": [2, 2, 136], "isBias": "True", "stride": [2, 2]},
+        {"layer": "active", "active_func": "sigmoid"},
+        {"layer": "connect", "hidden": 24},
+    ],
 }
 STANDALONE = {"dense_norm_head": ("bn",), "pool_after_norm_act": ("bn", "pool"),
-              "wide_norm_pool_first": ("bn", "pool")}
+              "wide_norm_pool_first": ("bn", "pool"), "wide_conv_192": ("gconv", "bn", "pool"),
+              "wide_conv_chain": ("gconv", "bn")}
 
 
 def _run_one(cfg, backend, ds, name=None):
