@@ -221,10 +221,15 @@ class TrainEngine:
         self.host_step += 1
 
     def group_steps(self) -> int:
-        """Steps per multi-step graph (1: grouping off — eager, data parallel, or
-        CSA_GRAPH_STEPS=1)."""
+        """Steps per multi-step graph (1: grouping off — eager, or CSA_GRAPH_STEPS=1).
+        Under data parallelism every collective of a step is already captured in the
+        single-step graph (RCCL kernels, or the xGMI peer-buffer kernels whose channel
+        sequence numbers live on the device), so k steps capture the same way; the
+        per-call-site path choice is made eagerly at warm-up, before any capture."""
         k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
-        return k if (self.use_graph and k > 1 and not self.ctx.enabled) else 1
+        if self.ctx.enabled and os.environ.get("CSA_DP_GRAPH_STEPS", "1") != "1":
+            return 1
+        return k if (self.use_graph and k > 1) else 1
 
     def prepare_group_graph(self) -> None:
         """Capture the k-step graph now (capture does not execute; call after the first

@@ -210,6 +210,11 @@ class HipProgram:
             u.lr_act = (0, 0.0) if u.xt is not None else (_act_id(u.in_tf.act), _alpha(u.in_tf.act))
             u.lr_x = torch.zeros(W * B, fin, device=dev)
             u.lr_dy = torch.zeros(W * B, fout, device=dev)
+            # every rank forms the SAME global dW, so the optimizer update of W / b runs
+            # inside that weight-gradient launch (csa_dd_wgrad update mode: dW never exists)
+            # where the variables live — as ApplyAdagrad on the PS did
+            # (construct_distribute.py:355-357, 372-373)
+            u.lr_update = os.environ.get("CSA_LOWRANK_UPDATE", "1") == "1"
             for p in ("weight", "bias"):
                 n = f"{u.layer.name}.{p}"
                 taken.append((offs[n], offs[n] + self.gviews[n].numel()))
@@ -251,6 +256,9 @@ class HipProgram:
             for u in self.lr_units:
                 lp = u.layer
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if u.lr_update:
+                    self._dd_wgrad_update(u, u.lr_x, u.lr_dy, W * B, u.lr_act, ss)
+                    continue
                 self._rc(lib.csa_dense_wgrad(
                     K.ptr(u.lr_x), K.ptr(u.lr_dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
                     W * B, fin, fout, None, 0, 0, 0.0, 0.0, None, None, u.lr_act[0], u.lr_act[1], 1.0, ss),
@@ -324,9 +332,10 @@ class HipProgram:
         # CSA_DENSE_DIRECT: "fwd" (default) = forward GEMMs only, "1" = forward + backward
         # (+ in-kernel update), "0" = off — measured per launch in profiles/r2_dense_direct.md
         mode = os.environ.get("CSA_DENSE_DIRECT", "fwd")
-        direct = mode in ("1", "fwd") and not (e.ctx.enabled and e.sync.strategy == "lowrank")
+        direct = mode in ("1", "fwd")
+        lowrank = e.ctx.enabled and e.sync.strategy == "lowrank"
         for u in self.units:
-            u.direct = u.direct_bwd = u.direct_update = False
+            u.direct = u.direct_bwd = u.direct_update = u.lr_update = False
             if u.kind != "dense" or not direct:
                 continue
             fin = u.layer.in_shape.numel
@@ -335,7 +344,7 @@ class HipProgram:
             u.direct = True
             if u.fused:
                 continue                         # backward + update: csa_dense_bwd_update
-            u.direct_bwd = mode == "1"
+            u.direct_bwd = mode == "1" and not lowrank     # lowrank: wgrad from gathered operands
             u.direct_update = bool(u.direct_bwd and self.fused and self.head_rg)
 
     # ------------------------------------------------------------------ conv pair
@@ -668,7 +677,7 @@ class HipProgram:
         self.keep_ranges = []
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind != "dense" or u.fused or u.direct_update:
+            if u.kind != "dense" or u.fused or u.direct_update or u.lr_update:
                 continue
             fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
             m = B * (self.e.ctx.world if u in getattr(self, "lr_units", []) else 1)
@@ -1267,22 +1276,30 @@ class HipProgram:
         xin = u.xt if u.xt is not None else u.x.view(B, -1)
         act = (0, 0.0) if u.xt is not None else (_act_id(tf.act), _alpha(tf.act))
         if u.direct_update:
-            offs = self.model.state.offsets
-            ow, ob = offs[f"{lp.name}.weight"], offs[f"{lp.name}.bias"]
-            sl = e.slots
-            s0 = sl[0] if sl.shape[0] > 0 else None
-            s1 = sl[1] if sl.shape[0] > 1 else None
-            self._rc(lib.csa_dd_wgrad(
-                K.ptr(xin), K.ptr(u.dy), B, fin, fout, act[0], act[1], 1.0, None, None,
-                K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
-                K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
-                K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
-                e.opt_id, float(e.lr), K.ptr(e.dstep), st), "dd_wgrad(update)")
+            self._dd_wgrad_update(u, xin, u.dy, B, act, st)
         else:
             self._rc(lib.csa_dd_wgrad(
                 K.ptr(xin), K.ptr(u.dy), B, fin, fout, act[0], act[1], 1.0,
                 K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
                 None, None, None, None, None, None, -1, 0.0, None, st), "dd_wgrad")
+
+    def _dd_wgrad_update(self, u: Unit, x: torch.Tensor, dy: torch.Tensor, M: int, act, st) -> None:
+        """Weight gradient X^T dY over ``M`` rows with the optimizer update of W / b applied
+        in the same launch (csa_dd_wgrad update mode; the head advanced the step counter)."""
+        e, lp = self.e, u.layer
+        fin, fout = lp.in_shape.numel, lp.spec.hidden
+        offs = self.model.state.offsets
+        ow, ob = offs[f"{lp.name}.weight"], offs[f"{lp.name}.bias"]
+        sl = e.slots
+        s0 = sl[0] if sl.shape[0] > 0 else None
+        s1 = sl[1] if sl.shape[0] > 1 else None
+        V = self.views
+        self._rc(self.lib.csa_dd_wgrad(
+            K.ptr(x), K.ptr(dy), M, fin, fout, act[0], act[1], 1.0, None, None,
+            K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
+            K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
+            K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
+            e.opt_id, float(e.lr), K.ptr(e.dstep), st), "dd_wgrad(update)")
 
     def _dense_bwd_update(self, u: Unit, prev: Optional[Unit], st) -> None:
         """Dense backward + optimizer update of W / b in one launch (dense_update.hip)."""
@@ -1314,7 +1331,7 @@ class HipProgram:
         ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
         skip = set()
         for u in self.units:
-            if u.kind == "dense" and (u.fused or u.direct_update):
+            if u.kind == "dense" and (u.fused or u.direct_update or u.lr_update):
                 skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
         if not skip:
             return []

@@ -264,6 +264,10 @@ class JobRun:
         """May the next ``k`` steps run as one multi-step launch?  Only the group's LAST step
         may be a log point (after_step handles it); fault / hang injection steps run alone."""
         step = self.eng.host_step
+        if self.ctx.enabled and self.eng.device.type == "cuda":
+            period = self.ctl_every * self.log_every        # comm probe steps run alone
+            if any(s % period == 1 for s in range(step, step + k)):
+                return False
         return (step + k <= self.cfg.iter
                 and all((s % self.log_every) != 0 for s in range(step, step + k - 1))
                 and not (step <= self.fault_at < step + k) and not (step <= self.hang_at < step + k))

@@ -65,13 +65,22 @@ def test_lowrank_strategy_matches_single_gpu(pg, monkeypatch):
     assert a.backend == "hip", a.fallback_reason
     names = [u.layer.name for u in a.program.lr_units]
     assert len(names) == 2, names                      # fc1 (materialised BN input) and fc2
+    # the gathered global dW is applied inside the weight-gradient launch (no dW buffer,
+    # the optimizer launch skips those spans) and the forward GEMMs are register-direct
+    assert all(u.lr_update and u.direct for u in a.program.lr_units)
+    skipped = {a.model.state.offsets[f"{n}.weight"] for n in names}
+    assert not any(lo <= o < hi for lo, hi in a.program.opt_segments for o in skipped), a.program.opt_segments
     # dense-last flat layout: the all-reduced remainder (conv, BN, head) is ONE leading range
     assert len(a.program.lr_ranges) == 1 and a.program.lr_ranges[0][0] == 0, a.program.lr_ranges
     first_dense = min(a.model.state.offsets[f"{n}.weight"] for n in names)
     assert a.program.lr_ranges[0][1] <= first_dense
     b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
-    for _ in range(20):
+    for _ in range(4):
         a.step(); b.step()
+    # multi-step graphs under data parallelism: 16 more steps as two 8-step launches
+    assert a.group_steps() == 8
+    a.run_steps(16); b.run_steps(16)
+    assert a.graph_k is not None and a.host_step == b.host_step == 20
     torch.cuda.synchronize()
     assert a.sync._choice["lr_x"] is not None and a.sync._choice["lr_dy"] is not None, a.sync._choice
     a.sync.check()
