@@ -136,6 +136,7 @@ class TrainEngine:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.graph = None
         self.graph_k = None      # CSA_GRAPH_STEPS steps captured in one graph (run_steps)
+        self.warmed = False      # _warm_up ran (a packed host re-captures without it)
 
     # ---------------- pieces used by the programs (device ops only) ----------------
     def adam_lr_tensor(self) -> torch.Tensor:
@@ -197,6 +198,7 @@ class TrainEngine:
         for b, v in bufs:
             b.copy_(v)
         self.program.reset_after_warmup() if hasattr(self.program, "reset_after_warmup") else None
+        self.warmed = True
 
     def _capture(self) -> None:
         self._warm_up()

@@ -104,8 +104,12 @@ class PackedJobs:
                 n -= 1
 
     def _capture(self) -> None:
+        # only engines that never ran warm up (allocator / library init off-graph); a job
+        # already hosted keeps its state untouched and is simply captured again, so an
+        # admission or retirement costs one graph capture, not 2 eager steps per tenant
         for e in self.engines:
-            e._warm_up()
+            if not e.warmed:
+                e._warm_up()
         main = torch.cuda.current_stream(self.device)
         streams = [torch.cuda.Stream(self.device) for _ in self.engines]
         g = torch.cuda.CUDAGraph()

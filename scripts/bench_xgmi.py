@@ -44,7 +44,7 @@ def worker(rank, world, port, q):
                 call()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for _ in range(50):
                 call()
         g.replay(); torch.cuda.synchronize()

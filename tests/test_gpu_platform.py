@@ -172,3 +172,65 @@ def test_node_status_reports_gpus_on_device():
     assert "vram" in g or "asic" in g, sorted(g)
     assert isinstance(st["Topology"], list)
     print("gpu0 fields:", sorted(g))
+
+
+def test_packed_run_steps_equal_single_packed_steps():
+    """PackedJobs.run_steps(n) (8-step multi-job graphs, groups never crossing a half of a
+    job's row table: stream_chunk 12 forces half switches inside the run) == n single
+    packed steps: same host/device step, cursor and weights (gpu_host's default path)."""
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    from cloud_server_amd.runtime.multijob import PackedJobs
+
+    def engs():
+        out = []
+        for seed in (1, 2):
+            c = _cfg(100, seed=seed)
+            c.update(optimizer_name="AdagradOptimizer", learning_rate=1e-3)
+            out.append(TrainEngine(parse_train_config(c), synthetic_mnist(2000, seed=seed), device="cuda:0",
+                                   backend="hip", stream_chunk=12))
+        return out
+    a, b = PackedJobs(engs()), PackedJobs(engs())
+    a.step(); b.step()
+    a.run_steps(40)
+    for _ in range(40):
+        b.step()
+    a.sync_device()
+    assert a.graph_k is not None and a.host_step == b.host_step == 41
+    for x, y in zip(a.engines, b.engines):
+        assert x.host_step == y.host_step == 41 and int(x.dstep.item()) == int(y.dstep.item()) == 41
+        assert torch.equal(x.stream.cursor, y.stream.cursor)
+        torch.testing.assert_close(x.flat, y.flat, rtol=1e-3, atol=5e-4)
+
+
+def test_packed_readmission_recaptures_without_rewarming():
+    """Admitting a job into a running pack re-captures the graph without re-running the
+    hosted jobs' warm-up (their weights / step counters are untouched by the re-pack) and
+    the stall is one capture; the hosted job then continues exactly as a lone run."""
+    import time
+    from cloud_server_amd.models.dsl import parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    from cloud_server_amd.runtime.multijob import PackedJobs
+
+    def eng(seed):
+        c = _cfg(100, seed=seed)
+        c.update(optimizer_name="AdagradOptimizer", learning_rate=1e-3)
+        return TrainEngine(parse_train_config(c), synthetic_mnist(2000, seed=seed), device="cuda:0", backend="hip")
+    old, solo = eng(1), eng(1)
+    p1 = PackedJobs([old])
+    for _ in range(10):
+        p1.step(); solo.step()
+    p1.sync_device()
+    before = old.flat.clone()
+    new = eng(2)
+    p2 = PackedJobs([old, new])
+    t0 = time.perf_counter()
+    p2._capture()
+    torch.cuda.synchronize()
+    stall = time.perf_counter() - t0
+    assert torch.equal(old.flat, before) and int(old.dstep.item()) == 10     # nothing ran
+    print(f"re-pack stall with one new job: {stall * 1e3:.1f} ms")
+    for _ in range(10):
+        p2.step(); solo.step()
+    p2.sync_device()
+    torch.testing.assert_close(old.flat, solo.flat, rtol=1e-3, atol=5e-4)
