@@ -38,6 +38,7 @@ import torch.distributed as dist
 from ..utils.tracing import trace_range
 from .dist import DistContext
 from . import xgmi as _xg
+from ..utils.graphs import capture
 
 DEFAULT_BUCKET_BYTES = 32 << 20   # one bucket covers the sample model's 9.1 MB gradient
 
@@ -195,7 +196,7 @@ class GradSync:
                 fn()                          # eager warm-up (RCCL communicator paths)
             torch.cuda.current_stream(dev).wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with capture(g):
                 for _ in range(10):
                     fn()
             g.replay()

@@ -33,6 +33,7 @@ from ..ops import optim_ref
 from ..parallel.dist import DistContext
 from ..parallel.dp import GradSync
 from ..utils.tracing import trace_range
+from ..utils.graphs import capture
 
 RING = 4096
 
@@ -205,7 +206,7 @@ class TrainEngine:
         g = torch.cuda.CUDAGraph()
         # thread_local: the RCCL watchdog thread queries events of earlier collectives while
         # this thread captures; in "global" mode that query aborts the process
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with capture(g):
             self.program.run()
         self.graph = g
         # capture does not execute: the cursor/step still point at this step
@@ -239,7 +240,7 @@ class TrainEngine:
         k = self.group_steps()
         if k > 1 and self.graph is not None and self.graph_k is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with capture(g):
                 for _ in range(k):
                     self.program.run()
             self.graph_k = g

@@ -32,6 +32,7 @@ import torch
 
 from .engine import TrainEngine
 from ..utils.tracing import trace_range
+from ..utils.graphs import capture
 
 
 def prefer_packed_kernels() -> None:
@@ -68,7 +69,7 @@ class PackedJobs:
         back (the jobs drift within the graph instead of joining after every step)."""
         streams = self._streams
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with capture(g):
             cap = torch.cuda.current_stream(self.device)
             for e, s in zip(self.engines, streams):
                 s.wait_stream(cap)
@@ -113,7 +114,7 @@ class PackedJobs:
         main = torch.cuda.current_stream(self.device)
         streams = [torch.cuda.Stream(self.device) for _ in self.engines]
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with capture(g):
             cap = torch.cuda.current_stream(self.device)
             for e, s in zip(self.engines, streams):
                 s.wait_stream(cap)            # fork: each job a branch of the graph

@@ -35,14 +35,16 @@ import numpy as np
 import torch
 
 from ..models.dsl import TrainConfig
+from ..utils.graphs import capture
 
 BUCKETS = (1, 4, 16, 64, 256)
 PREPS = ("reference", "mnist")
 
-# graph captures in this process are serialised (thread_local mode keeps other threads'
-# unrelated GPU calls legal during a capture; the lock keeps two captures from sharing
-# the allocator's capture pools)
-CAPTURE_LOCK = threading.Lock()
+# Graph captures AND graph destructions in this process are serialised: thread_local
+# capture mode keeps other threads' unrelated GPU calls legal during a capture, but a
+# graph executable destroyed while a capture is in progress aborts the process (see
+# utils/graphs.py), and a retired model's buckets may die on any request thread.
+CAPTURE_LOCK = threading.RLock()
 
 
 def bucket_for(n: int) -> int:
@@ -124,9 +126,15 @@ class _Bucket:
             torch.cuda.current_stream(self.device).wait_stream(s)
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with capture(g):
                 self._body()
             self.graph = g
+
+    def __del__(self):
+        g, self.graph = getattr(self, "graph", None), None
+        if g is not None:
+            with CAPTURE_LOCK:          # never destroyed while another thread captures
+                del g
 
     def logits_u8(self, x: np.ndarray) -> torch.Tensor:
         """Replay on ``x`` (n <= B rows) and return the [n, 10] logits (device tensor, a

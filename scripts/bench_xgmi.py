@@ -24,6 +24,7 @@ SIZES = [("lowrank remainder AR one-shot", 1, 25 * 1024), ("lowrank remainder AR
 def worker(rank, world, port, q):
     import torch.distributed as dist
     from cloud_server_amd.parallel import xgmi as X
+    from cloud_server_amd.utils.graphs import capture
     torch.cuda.set_device(0 if torch.cuda.device_count() == 1 else rank)
     dev = torch.device("cuda", torch.cuda.current_device())
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -44,7 +45,7 @@ def worker(rank, world, port, q):
                 call()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with capture(g):
             for _ in range(50):
                 call()
         g.replay(); torch.cuda.synchronize()

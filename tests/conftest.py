@@ -34,6 +34,13 @@ def pytest_sessionstart(session):
 def pytest_runtest_logstart(nodeid, location):
     if _REAL_ERR is not None:
         os.write(_REAL_ERR, f"[csa-test] {nodeid}\n".encode())
+    if os.environ.get("CSA_FATAL_TRACE", "0") == "1":
+        # native backtrace of the thread that aborts (HIP / RCCL / c10d), chained in front
+        # of faulthandler's Python stack (csrc/runtime/fatal_trace.cpp); re-armed before
+        # every test because runtimes initialised by a test may install their own handlers
+        import ctypes
+        from cloud_server_amd.ops import build as _b
+        ctypes.CDLL(_b.build_runtime()).csa_install_fatal_trace()
 
 
 def pytest_collection_modifyitems(config, items):

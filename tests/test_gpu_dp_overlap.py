@@ -112,3 +112,37 @@ def test_collective_autotune_records_both_paths(pg, monkeypatch):
     for n in a.model.state.shapes:          # lowrank uses the dense-last layout: compare by name
         torch.testing.assert_close(a.model.state.view(n, a.flat), b.model.state.view(n, b.flat),
                                    rtol=2e-3, atol=2e-5)
+
+
+def test_capture_finalizes_garbage_graphs_before_capturing():
+    """Regression test of the round-2 GPU-suite abort (profiles/r3_gpu_suite_abort.md): a
+    CUDAGraph left in a reference cycle by an earlier engine must be destroyed BEFORE a new
+    capture begins, never by a garbage collection triggered inside the capture."""
+    import gc
+    import weakref
+    from cloud_server_amd.utils.graphs import capture
+    x = torch.zeros(8, device="cuda:0")
+    old = torch.cuda.CUDAGraph()
+    with capture(old):
+        x.add_(1)
+
+    class Holder:                       # engine <-> program style reference cycle
+        pass
+    h = Holder()
+    h.graph, h.self_ref = old, h
+    seen = []
+    weakref.finalize(h, lambda: seen.append(torch.cuda.is_current_stream_capturing()))
+    del h, old
+    gc.disable()                       # the cycle survives until someone collects
+    try:
+        g = torch.cuda.CUDAGraph()
+        with capture(g):
+            for _ in range(200):
+                [object() for _ in range(100)]   # allocations that would trigger a collection
+            x.add_(1)
+    finally:
+        gc.enable()
+    assert seen == [False]            # finalised, and not while capturing
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0]) == 2.0         # the first graph was captured, never replayed

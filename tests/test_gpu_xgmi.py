@@ -14,6 +14,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from cloud_server_amd.utils.graphs import capture
+
 pytestmark = pytest.mark.gpu
 
 
@@ -75,7 +77,7 @@ def _worker(rank: int, world: int, port: int, q) -> None:
         torch.cuda.current_stream().wait_stream(st)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        with capture(graph):
             gr.all_gather([(inp, gout)])
             red.copy_(inp)
             comm.channel("graph_ar", red.nbytes).all_reduce([red])
@@ -184,7 +186,7 @@ def _worker_twoshot(rank: int, world: int, port: int, q) -> None:
         res["sequence"] = all(bool(torch.all(v == sum(i + r for r in range(world))).item()) for i, v in outs)
         buf = torch.zeros(50000, device=dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with capture(g):
             ch.all_reduce([buf], protocol="twoshot")
         ok = True
         for it in range(10):
