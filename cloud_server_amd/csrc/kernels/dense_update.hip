@@ -73,7 +73,18 @@ struct DUArgs {
   int cs;                   // column blocks per row group (> 1: partial hand-off)
   float* part;              // [groups * cs][DU_PART] input-gradient partials (write-through)
   unsigned* cnt;            // [groups] arrival tickets (zero between launches)
+  // head epilogue (the LAST dense layer of the fused program; head_row_kernel ran before):
+  // this layer's OUTPUT is the head input hy [M][N]; the block reduces the head's weight
+  // gradient for its share of the N features, one block the bias gradient and metrics
+  const float* hy;          // [M][N] (null: no head epilogue)
+  const float* hdl;         // [M][10] dlogits (scaled)
+  float* hgw; float* hgb;   // dWh [N][10], dbh [10] (plain stores into the flat gradient)
+  const float* hrl; const int* hrc;   // [M] per-row loss / correct
+  float* ring_loss; int* ring_correct; int ring; float ldiv;
 };
+
+constexpr int DU_HNC = 10;           // head classes
+constexpr int DU_HPF = 12;           // prefetched (hy, dl) pairs per thread
 
 // diagnostics: s_memrealtime stamps (100 MHz, one clock for all XCDs) of EVERY block,
 // [block][8] = start, dY staged, W landed, MFMA + update done, fold done, dX stored, end
@@ -117,7 +128,89 @@ __device__ __forceinline__ void du_store_w(const DUArgs& a, const float4 (&wv)[D
 // NSLOT = optimizer slots (0 SGD, 1 Adagrad, 2 Adam / Adadelta): unused slot registers
 // are not allocated.  WAVES = 16 (one block per row group, all N <= 512 columns) or 4
 // (128 columns per block, cs blocks per row group: narrow layers use more CUs).
-template <int NSLOT, int WAVES>
+// Head epilogue, part 1: this block's dWh rows [hn0, hn1) — output o = (n, j) handled by
+// THREADS / outs m-slices; the (hy, dl) operands of the first DU_HPF rows of the slice are
+// requested at kernel start so their latency hides under the layer's own work.
+struct DUHead {
+  int hn0, outs, nsl, o, sl;
+  float hv[DU_HPF], dv[DU_HPF];
+};
+
+template <int THREADS>
+__device__ __forceinline__ void du_head_prefetch(const DUArgs& a, int grp, int groups, int cb, int nb, DUHead& h) {
+  const int hper = (nb + groups - 1) / groups;
+  h.hn0 = cb + grp * hper;
+  const int nh = max(0, min(hper, cb + nb - h.hn0));
+  h.outs = nh * DU_HNC;
+  h.nsl = h.outs > 0 && h.outs <= THREADS ? THREADS / h.outs : 0;   // 0: direct loop (no prefetch)
+  const int t = threadIdx.x;
+  h.o = h.outs > 0 ? t % h.outs : 0;
+  h.sl = h.outs > 0 ? t / h.outs : THREADS;
+  const int n = h.hn0 + h.o / DU_HNC, j = h.o % DU_HNC;
+  if (h.nsl == 0) return;
+#pragma unroll
+  for (int u = 0; u < DU_HPF; ++u) {
+    const int m = min(h.sl + u * h.nsl, a.M - 1);
+    h.hv[u] = a.hy[(long)m * a.N + min(n, a.N - 1)];
+    h.dv[u] = a.hdl[m * DU_HNC + j];
+  }
+}
+
+template <int THREADS>
+__device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float* s_hw) {
+  const int t = threadIdx.x;
+  if (h.nsl == 0) {                                       // more outputs than threads
+    for (int o = t; o < h.outs; o += THREADS) {
+      const int n = h.hn0 + o / DU_HNC, j = o % DU_HNC;
+      float v = 0.f;
+      for (int m = 0; m < a.M; ++m) v = fmaf(a.hy[(long)m * a.N + n], a.hdl[m * DU_HNC + j], v);
+      a.hgw[(long)n * DU_HNC + j] = v;
+    }
+  }
+  float acc = 0.f;
+  if (h.sl < h.nsl) {
+    const int n = h.hn0 + h.o / DU_HNC, j = h.o % DU_HNC;
+#pragma unroll
+    for (int u = 0; u < DU_HPF; ++u) {
+      pin(h.hv[u]); pin(h.dv[u]);
+      if (h.sl + u * h.nsl < a.M) acc = fmaf(h.hv[u], h.dv[u], acc);
+    }
+    for (int m = h.sl + DU_HPF * h.nsl; m < a.M; m += h.nsl)      // beyond the prefetch
+      acc = fmaf(a.hy[(long)m * a.N + n], a.hdl[m * DU_HNC + j], acc);
+    s_hw[t] = acc;
+  }
+  __syncthreads();
+  if (h.nsl > 0 && t < h.outs) {                          // slices folded in fixed order
+    float v = 0.f;
+    for (int q = 0; q < h.nsl; ++q) v += s_hw[q * h.outs + t];
+    a.hgw[(long)(h.hn0 + t / DU_HNC) * DU_HNC + t % DU_HNC] = v;
+  }
+  if (blockIdx.x == gridDim.x - 1) {                      // dbh and the step's metrics
+    const int lane = t & 63, w = t >> 6;
+    if (w == 0) {
+      float db[DU_HNC];
+#pragma unroll
+      for (int j = 0; j < DU_HNC; ++j) db[j] = lane < a.M ? a.hdl[lane * DU_HNC + j] : 0.f;
+#pragma unroll
+      for (int j = 0; j < DU_HNC; ++j) {
+        const float v = wave_sum(db[j]);
+        if (lane == 0) a.hgb[j] = v;
+      }
+    } else if (w == 1) {
+      float l = lane < a.M ? a.hrl[lane] : 0.f;
+      float c = lane < a.M ? (float)a.hrc[lane] : 0.f;
+      l = wave_sum(l);
+      c = wave_sum(c);
+      if (lane == 0) {
+        const int pos = (int)((*a.step - 1) % a.ring);    // the head advanced the counter
+        a.ring_loss[pos] = l / a.ldiv;
+        a.ring_correct[pos] = (int)(c + 0.5f);
+      }
+    }
+  }
+}
+
+template <int NSLOT, int WAVES, bool HEAD>
 __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) {
   constexpr int THREADS = 64 * WAVES, NB = du_nb(WAVES), SN = NB + 4, HW = 16 * WAVES;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -140,6 +233,9 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
   const int C = a.bn.C > 0 ? a.bn.C : 1;
   constexpr int nslot = NSLOT;
   DU_STAMP(0);
+  __shared__ float s_hw[HEAD ? THREADS : 1];
+  DUHead hd;
+  if (HEAD) du_head_prefetch<THREADS>(a, grp, groups, cb, nb, hd);
 
   // ---- every load, issued in the order it is consumed (vmcnt retires in order).  Two
   // column halves: half j = block columns [HW j, HW (j + 1)) = every wave's sub-tile j, so
@@ -313,6 +409,7 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
     }
   }
   DU_STAMP(3);
+  if (HEAD) du_head_finish<THREADS>(a, hd, s_hw);
   if (!dgrad) {                                            // uniform: first layer
     du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
     return;
@@ -463,14 +560,30 @@ CSA_API int csa_dense_bwd_update_ws(int K, int N, long long* ws) {
   return (int)cs;
 }
 
-template <int NSLOT, int WAVES>
-static void du_launch(const DUArgs& a, int blocks, hipStream_t st) {
-  static const bool attr = hipFuncSetAttribute((const void*)dense_bwd_update_kernel<NSLOT, WAVES>,
+template <int NSLOT, int WAVES, bool HEAD>
+static void du_launch3(const DUArgs& a, int blocks, hipStream_t st) {
+  static const bool attr = hipFuncSetAttribute((const void*)dense_bwd_update_kernel<NSLOT, WAVES, HEAD>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)DU_LDS_MAX) == hipSuccess;
   (void)attr;
-  hipLaunchKernelGGL((dense_bwd_update_kernel<NSLOT, WAVES>), dim3((unsigned)blocks), dim3(64 * WAVES),
+  hipLaunchKernelGGL((dense_bwd_update_kernel<NSLOT, WAVES, HEAD>), dim3((unsigned)blocks), dim3(64 * WAVES),
                      du_lds_floats(a.M, WAVES) * sizeof(float), st, a);
 }
+
+template <int NSLOT, int WAVES>
+static void du_launch(const DUArgs& a, int blocks, hipStream_t st) {
+  if (a.hy) du_launch3<NSLOT, WAVES, true>(a, blocks, st);
+  else du_launch3<NSLOT, WAVES, false>(a, blocks, st);
+}
+
+CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
+                                      const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
+                                      int bn_C, float bn_count, float bn_eps, const float* bn_scale,
+                                      const float* bn_offset, float* bwd_slab, const float* Xw, int opt, float lr,
+                                      const int64_t* step, float* s0w, float* s1w, float* s0b, float* s1b,
+                                      float scale, const float* bn_tab, float* part, unsigned* cnt,
+                                      const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
+                                      const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
+                                      hipStream_t st);
 
 CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
                                  const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
@@ -478,7 +591,25 @@ CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* 
                                  const float* bn_offset, float* bwd_slab, const float* Xw, int opt, float lr,
                                  const int64_t* step, float* s0w, float* s1w, float* s0b, float* s1b,
                                  float scale, const float* bn_tab, float* part, unsigned* cnt, hipStream_t st) {
+  return csa_dense_bwd_update_head(dY, W, bias, dX, M, K, N, x_fwd, act, alpha, bn_slab, bn_nslab, bn_C, bn_count,
+                                   bn_eps, bn_scale, bn_offset, bwd_slab, Xw, opt, lr, step, s0w, s1w, s0b, s1b,
+                                   scale, bn_tab, part, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                   nullptr, nullptr, 1, 1.f, st);
+}
+
+// ... plus the head epilogue (hy != null): dWh / dbh of the row-per-workgroup head and the
+// step's metric ring entry are reduced by this launch (see DUArgs).
+CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
+                                 const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
+                                 int bn_C, float bn_count, float bn_eps, const float* bn_scale,
+                                 const float* bn_offset, float* bwd_slab, const float* Xw, int opt, float lr,
+                                 const int64_t* step, float* s0w, float* s1w, float* s0b, float* s1b,
+                                 float scale, const float* bn_tab, float* part, unsigned* cnt,
+                                      const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
+                                      const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
+                                      hipStream_t st) {
   if (!csa_dense_bwd_update_ok(M, K, N, bn_slab ? bn_C : 0)) return -1;
+  if (hy && (!hdl || !hgw || !hgb || !hrl || !hrc || !ring_loss || !ring_correct || ring < 1 || !step)) return -2;
   if (!Xw || !W || !dY) return -2;
   DUArgs a{};
   a.M = M; a.K = K; a.N = N; a.dY = dY; a.W = W; a.bias = bias; a.dX = dX; a.x_fwd = x_fwd;
@@ -490,6 +621,8 @@ CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* 
   const int groups = (K + DU_FT - 1) / DU_FT;
   a.cs = du_cs(K, N);
   a.part = part; a.cnt = cnt;
+  a.hy = hy; a.hdl = hdl; a.hgw = hgw; a.hgb = hgb; a.hrl = hrl; a.hrc = hrc;
+  a.ring_loss = ring_loss; a.ring_correct = ring_correct; a.ring = ring; a.ldiv = ldiv;
   if (a.cs > 1 && dX && (!part || !cnt)) return -2;
   const int blocks = groups * a.cs;
   const int ns = opt_nslots(opt);

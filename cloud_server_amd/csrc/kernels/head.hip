@@ -683,6 +683,126 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
   HEAD_STAMP(5);
 }
 
+// ---------------------------------------------------------------------------------
+// One batch ROW per 256-thread workgroup (the fused one-GPU program, round 3).  The
+// head's gradient REDUCTIONS over the batch (dWh, dbh, loss, #correct) are not done
+// here: every workgroup writes only its row's outputs, and the last dense layer's fused
+// backward (dense_update.hip, "head epilogue") folds them while it runs anyway:
+//   dh[m][:]   = act'(dlogits[m] . Wh^T)            (plain stores: that kernel's dY)
+//   dl[m][:]   = dlogits[m] (already / M and grad-scaled)
+//   rloss[m], rcorr[m]
+// The chain is one batched round trip (the row of h and all of Wh, one thread per k),
+// 40 FMAs, ten wave reductions folded in fixed order, one lane's softmax, 10 FMAs per k.
+// Block 0 advances the device step counter (and the staged batch stream's cursor)
+// before any parameter update of the step reads it.
+// ---------------------------------------------------------------------------------
+constexpr int HR_T = 256;
+constexpr int HR_KPT = 4;               // k per thread: K <= 1024
+
+struct HeadRowArgs {
+  const float* h; int M, K; int in_act; float in_alpha;
+  const float* w; const float* b;
+  const int64_t* labels; const int64_t* idx; const int64_t* cursor;
+  int loss; float grad_scale;
+  float* dh; float* dl; float* rloss; int* rcorr;
+  int64_t* step; int64_t* adv_cursor; long wrap;
+};
+
+__global__ __launch_bounds__(HR_T) void head_row_kernel(HeadRowArgs a) {
+  __shared__ float s_part[HR_T / 64][NCLS];
+  __shared__ float s_dl[NCLS];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K = a.K;
+  if (m == 0 && tid == 0) {
+    *a.step += 1;
+    if (a.adv_cursor) {
+      const int64_t c = *a.adv_cursor + 1;
+      *a.adv_cursor = (a.wrap > 0 && c >= a.wrap) ? 0 : c;
+    }
+  }
+  // every load first: this thread's h values and Wh rows (clamped addresses), the bias
+  // and the row's label (the label chain runs under the h / Wh loads)
+  float hv[HR_KPT], wv[HR_KPT][NCLS];
+#pragma unroll
+  for (int u = 0; u < HR_KPT; ++u) {
+    const int k = min(u * HR_T + tid, K - 1);
+    hv[u] = a.h[(long)m * K + k];
+#pragma unroll
+    for (int j = 0; j < NCLS; j += 2) {
+      const float2 t = *reinterpret_cast<const float2*>(a.w + (long)k * NCLS + j);
+      wv[u][j] = t.x; wv[u][j + 1] = t.y;
+    }
+  }
+  float bias = lane < NCLS ? a.b[lane] : 0.f;
+  int label = 0;
+  if (wave == 0) {
+    if (!a.idx) label = (int)a.labels[m];
+    else label = (int)a.labels[(a.cursor ? a.idx + a.cursor[0] * a.M : a.idx)[m]];
+  }
+  float acc[NCLS];
+#pragma unroll
+  for (int j = 0; j < NCLS; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < HR_KPT; ++u) {
+    const bool ok = u * HR_T + tid < K;
+    hv[u] = ok ? act_fwd(hv[u], a.in_act, a.in_alpha) : 0.f;     // post-activation value
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) acc[j] = fmaf(hv[u], wv[u][j], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NCLS; ++j) {
+    const float t = wave_sum_dpp(acc[j]);
+    if (lane == 0) s_part[wave][j] = t;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    // lane j < 10: logit j (waves folded in fixed order), softmax / mse over the 10 lanes
+    float z = -INFINITY;
+    if (lane < NCLS) z = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane] + bias;
+    const float mx = wave_max(z);
+    // argmax: lowest class index attaining the max (the reference's tf.argmax)
+    const unsigned long long hit = __ballot(lane < NCLS && z == mx);
+    const int am = __builtin_ctzll(hit);
+    float d = 0.f, lterm = 0.f;
+    if (a.loss == 0) {
+      const float e = lane < NCLS ? __expf(z - mx) : 0.f;
+      const float se = wave_sum(e);
+      const float lse = mx + __logf(se);
+      if (lane < NCLS) {
+        d = (__expf(z - lse) - (lane == label ? 1.f : 0.f)) * (a.grad_scale / (float)a.M);
+        lterm = lane == label ? lse - z : 0.f;
+      }
+    } else if (lane < NCLS) {
+      const float t = z - (lane == label ? 1.f : 0.f);
+      lterm = t * t;
+      d = t * (2.f * a.grad_scale / (float)(a.M * NCLS));
+    }
+    const float ls = wave_sum(lterm);
+    if (lane < NCLS) {
+      s_dl[lane] = d;
+      a.dl[(long)m * NCLS + lane] = d;
+    }
+    if (lane == 0) {
+      a.rloss[m] = ls;
+      a.rcorr[m] = am == label ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  float dl[NCLS];
+#pragma unroll
+  for (int j = 0; j < NCLS; ++j) dl[j] = s_dl[j];
+#pragma unroll
+  for (int u = 0; u < HR_KPT; ++u) {
+    const int k = u * HR_T + tid;
+    if (k >= K) break;
+    float g = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) g = fmaf(dl[j], wv[u][j], g);
+    if (a.in_act) g = act_bwd(g, hv[u], hv[u], a.in_act, a.in_alpha);
+    a.dh[(long)m * K + k] = g;
+  }
+}
+
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.
 __global__ __launch_bounds__(HT) void head_generic_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -754,6 +874,20 @@ CSA_API int csa_head_part2(const float* h, int M, int K, int in_act, float in_al
                            const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,
                            int loss, float grad_scale, float* dh, float* part, float* mpart, int* mcorr,
                            float* logits_out, int64_t* step, int64_t* adv_cursor, long wrap, hipStream_t st);
+
+// Row-per-workgroup head (see head_row_kernel): 0 when K is outside its family.
+CSA_API int csa_head_row_ok(int M, int K) { return M >= 1 && K >= 1 && K <= HR_KPT * HR_T && K % 2 == 0 ? 1 : 0; }
+
+CSA_API int csa_head_row(const float* h, int M, int K, int in_act, float in_alpha, const float* w, const float* b,
+                         const int64_t* labels, const int64_t* idx, const int64_t* cursor, int loss,
+                         float grad_scale, float* dh, float* dl, float* rloss, int* rcorr, int64_t* step,
+                         int64_t* adv_cursor, long wrap, hipStream_t st) {
+  if (!csa_head_row_ok(M, K) || !dh || !dl || !rloss || !rcorr) return -1;
+  HeadRowArgs a{h, M, K, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, dl, rloss, rcorr,
+                step, adv_cursor, wrap};
+  hipLaunchKernelGGL(head_row_kernel, dim3((unsigned)M), dim3(HR_T), 0, st, a);
+  return (int)hipGetLastError();
+}
 
 CSA_API int csa_head_part(const float* h, int M, int K, int in_act, float in_alpha, const float* w,
                           const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,

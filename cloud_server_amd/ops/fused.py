@@ -58,6 +58,10 @@ _SIGS = {
     "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
                                  P, P, P, P, F, P, P, P, P]),
     "csa_dense_bwd_update_ws": (I, [I, I, P]),
+    "csa_dense_bwd_update_head": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
+                                      P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, P]),
+    "csa_head_row_ok": (I, [I, I]),
+    "csa_head_row": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, L, P]),
     "csa_head_part_rows": (I, [I, I]),
     "csa_du_debug": (I, [P]),
     "csa_opt_debug": (I, [P]),

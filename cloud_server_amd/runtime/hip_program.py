@@ -318,12 +318,19 @@ class HipProgram:
             u.fused = (bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C))
                        and groups >= int(os.environ.get("CSA_FUSED_DENSE_MIN_GROUPS", "1")))
         self.head_rg = 0
+        self.head_row = False
         if self.fused and self.head_tf.norm is None:
             last = self.units[-1]
             K = last.layer.spec.hidden if last.kind == "dense" else last.layer.out_shape.numel
             if last.kind == "conv" and last.pool is not None:
                 K = last.pool.out_shape.numel
-            self.head_rg = int(self.lib.csa_head_part_rows(B, K))
+            # one batch row per workgroup; the head's batch reductions (dWh, dbh, metrics)
+            # ride in the last dense layer's fused backward (csa_head_row + the head epilogue
+            # of csa_dense_bwd_update_head) — no partial rows for the optimizer to fold
+            self.head_row = (last.kind == "dense" and last.fused and bool(self.lib.csa_head_row_ok(B, K))
+                             and os.environ.get("CSA_HEAD_ROW", "1") == "1")
+            if not self.head_row:
+                self.head_rg = int(self.lib.csa_head_part_rows(B, K))
         # register-direct MFMA dense kernels (dense_direct.hip): forward, input gradient and
         # weight gradient; on one GPU the weight-gradient launch applies the optimizer update
         # itself (the head advanced the step counter), so dW never exists in memory
@@ -345,7 +352,7 @@ class HipProgram:
             if u.fused:
                 continue                         # backward + update: csa_dense_bwd_update
             u.direct_bwd = mode == "1" and not lowrank     # lowrank: wgrad from gathered operands
-            u.direct_update = bool(u.direct_bwd and self.fused and self.head_rg)
+            u.direct_update = bool(u.direct_bwd and self.fused and (self.head_rg or self.head_row))
 
     # ------------------------------------------------------------------ conv pair
     def _plan_pair(self) -> None:
@@ -570,6 +577,10 @@ class HipProgram:
                               if u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") != "1"
                               else None)
         self.dlast = self.units[-1].dy     # head input grad (None: forward only)
+        if getattr(self, "head_row", False):
+            self.hdl = torch.zeros(B, 10, **f32)                            # dlogits rows
+            self.hrl = torch.zeros(B, **f32)                                # per-row loss
+            self.hrc = torch.zeros(B, dtype=torch.int32, device=dev)        # per-row correct
         self.idx = None
         if self.head_rg:
             K = self.dlast[0].numel()
@@ -686,6 +697,11 @@ class HipProgram:
                     n = f"{u.layer.name}.{p}"
                     lo = offs[n]
                     self.keep_ranges.append((lo, lo + (self.gviews[n].numel() // 4) * 4))
+        if getattr(self, "head_row", False):
+            for n in ("head.weight", "head.bias"):
+                lo = offs[n]
+                if self.gviews[n].numel() >= 4:
+                    self.keep_ranges.append((lo, lo + (self.gviews[n].numel() // 4) * 4))
         self.ps_mode = self.e.sync.strategy == "ps" and self.e.ctx.enabled
         regions = regs + (flat if self.ps_mode else [])
         # the optimizer's zero list holds 16; any further accumulators are cleared at the
@@ -713,7 +729,7 @@ class HipProgram:
         e = self.e
         img = e.data.images
         imsz = img[0].numel() if img.dim() > 1 else 0
-        self.staged = (self.pair is not None and bool(self.head_rg) and img.dtype == torch.uint8
+        self.staged = (self.pair is not None and bool(self.head_rg or self.head_row) and img.dtype == torch.uint8
                        and imsz % 4 == 0 and os.environ.get("CSA_STAGE_BATCH", "1") == "1")
         self.stage_img = self.stage_lbl = None
         if self.staged:
@@ -799,7 +815,16 @@ class HipProgram:
         # ---------------- head (loss, head grads, input grad, metrics) ----------------
         last = self.units[-1]
         hin = last.y.view(B, -1)
-        if self.head_rg:
+        if self.head_row:
+            staged = getattr(self, "staged", False)
+            self._rc(lib.csa_head_row(
+                K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
+                K.ptr(V["head.weight"]), K.ptr(V["head.bias"]),
+                K.ptr(self.stage_lbl if staged else e.data.labels), None if staged else K.ptr(rows),
+                None if staged else K.ptr(cur), 0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
+                K.ptr(last.dy), K.ptr(self.hdl), K.ptr(self.hrl), K.ptr(self.hrc), K.ptr(e.dstep),
+                K.ptr(cur) if staged else None, e.stream.wrap if staged else 0, st), "head_row")
+        elif self.head_rg:
             staged = getattr(self, "staged", False)
             self._rc(lib.csa_head_part2(
                 K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
@@ -1312,14 +1337,24 @@ class HipProgram:
         s0 = sl[0] if sl.shape[0] > 0 else None
         s1 = sl[1] if sl.shape[0] > 1 else None
         xw = u.xt if u.xt is not None else u.x.view(B, -1)
-        self._rc(lib.csa_dense_bwd_update(
+        if self.head_row and u is self.units[-1]:
+            # the head's batch reductions ride along: dWh / dbh into the flat gradient (the
+            # optimizer updates them), the step's loss / #correct into the metric ring
+            G = self.gviews
+            head = (K.ptr(u.y), K.ptr(self.hdl), K.ptr(G["head.weight"]), K.ptr(G["head.bias"]),
+                    K.ptr(self.hrl), K.ptr(self.hrc), K.ptr(e.ring_loss), K.ptr(e.ring_correct),
+                    e.ring_correct.numel(), float(B if e.cfg.loss_name == "entropy" else B * 10))
+        else:
+            head = (None, None, None, None, None, None, None, None, 1, 1.0)
+        self._rc(lib.csa_dense_bwd_update_head(
             K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
             K.ptr(prev.dy) if prev is not None else None, B, fin, fout,
             K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
             K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
             K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
             K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
-            1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), st), "dense_bwd_update")
+            1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), *head, st),
+            "dense_bwd_update")
 
     def _opt_segments(self):
         """Flat [lo, hi) spans the optimizer launch updates: everything except the

@@ -1,12 +1,9 @@
 #!/bin/bash
-# One iteration of the kernel loop: step numerics tests, bench, per-kernel microbench with
-# GEMM stamps.  Stops at the first failing GPU step.
+# Iteration loop: HIP step numerics tests, bench (default), isolated launch list + graph step.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_hip_step.py tests/test_gpu_dp_overlap.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/hip_tests.log 2>&1
-rc=$?; tail -5 gpurun_out/hip_tests.log
-[ $rc -gt 1 ] && exit $rc
-timeout -k 10 300 python bench.py --steps 3000 --warmup 300 > gpurun_out/bench_iter.json 2> gpurun_out/bench_iter.err || { tail -20 gpurun_out/bench_iter.err; exit 3; }
-cat gpurun_out/bench_iter.json
-MB_GEMM=1 timeout -k 10 300 python scripts/microbench.py --reps 100 > gpurun_out/micro.txt 2>&1 || { tail -20 gpurun_out/micro.txt; exit 4; }
-grep -v amdgpu.ids gpurun_out/micro.txt
-exit $rc
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_hip_step.py ${TESTS_EXTRA} > gpurun_out/iter_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/iter_tests.log; [ $rc -ne 0 ] && { grep -B5 -A25 "Error\|FAILED" gpurun_out/iter_tests.log | head -80; exit $rc; }
+timeout -k 10 300 python bench.py > gpurun_out/iter_bench.json 2> gpurun_out/iter_bench.err || { tail -20 gpurun_out/iter_bench.err; exit 4; }
+cat gpurun_out/iter_bench.json
+timeout -k 10 200 python scripts/microbench.py > gpurun_out/iter_mb.txt 2>&1 || { tail -20 gpurun_out/iter_mb.txt; exit 5; }
+grep -v amdgpu.ids gpurun_out/iter_mb.txt

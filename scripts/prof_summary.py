@@ -18,7 +18,8 @@ from collections import defaultdict
 def load_db(path: str):
     c = sqlite3.connect(path)
     rows = c.execute(
-        "select s.kernel_name, d.end - d.start, d.grid_size_x, d.workgroup_size_x, "
+        "select s.kernel_name, d.end - d.start, d.grid_size_x * d.grid_size_y * d.grid_size_z, "
+        "d.workgroup_size_x * d.workgroup_size_y * d.workgroup_size_z, "
         "s.arch_vgpr_count, s.accum_vgpr_count, s.group_segment_size "
         "from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id").fetchall()
     return rows
@@ -42,6 +43,7 @@ def main() -> int:
         e = agg[name]
         e[0] += 1
         e[1] += ns / 1e3
+        # grid sizes are in work-items per dimension: workgroups = product(grid) / product(wg)
         e[2], e[3], e[4], e[5], e[6] = grid // max(wg, 1), wg, vg, ag, lds
     total = sum(v[1] for v in agg.values())
     print(f"| kernel | calls | total µs | mean µs | share | WGs | WG size | VGPR | AGPR | LDS B |")
