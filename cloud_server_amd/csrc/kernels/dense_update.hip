@@ -81,6 +81,7 @@ struct DUArgs {
   float* hgw; float* hgb;   // dWh [N][10], dbh [10] (plain stores into the flat gradient)
   const float* hrl; const int* hrc;   // [M] per-row loss / correct
   float* ring_loss; int* ring_correct; int ring; float ldiv;
+  int hact; float halpha;   // the head's input transform: the head reads act(hy)
 };
 
 constexpr int DU_HNC = 10;           // head classes
@@ -163,7 +164,8 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
     for (int o = t; o < h.outs; o += THREADS) {
       const int n = h.hn0 + o / DU_HNC, j = o % DU_HNC;
       float v = 0.f;
-      for (int m = 0; m < a.M; ++m) v = fmaf(a.hy[(long)m * a.N + n], a.hdl[m * DU_HNC + j], v);
+      for (int m = 0; m < a.M; ++m)
+        v = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), a.hdl[m * DU_HNC + j], v);
       a.hgw[(long)n * DU_HNC + j] = v;
     }
   }
@@ -173,10 +175,10 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
 #pragma unroll
     for (int u = 0; u < DU_HPF; ++u) {
       pin(h.hv[u]); pin(h.dv[u]);
-      if (h.sl + u * h.nsl < a.M) acc = fmaf(h.hv[u], h.dv[u], acc);
+      if (h.sl + u * h.nsl < a.M) acc = fmaf(act_fwd(h.hv[u], a.hact, a.halpha), h.dv[u], acc);
     }
     for (int m = h.sl + DU_HPF * h.nsl; m < a.M; m += h.nsl)      // beyond the prefetch
-      acc = fmaf(a.hy[(long)m * a.N + n], a.hdl[m * DU_HNC + j], acc);
+      acc = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), a.hdl[m * DU_HNC + j], acc);
     s_hw[t] = acc;
   }
   __syncthreads();
@@ -583,7 +585,7 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
                                       float scale, const float* bn_tab, float* part, unsigned* cnt,
                                       const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
                                       const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
-                                      hipStream_t st);
+                                      int hact, float halpha, hipStream_t st);
 
 CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
                                  const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
@@ -594,7 +596,7 @@ CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* 
   return csa_dense_bwd_update_head(dY, W, bias, dX, M, K, N, x_fwd, act, alpha, bn_slab, bn_nslab, bn_C, bn_count,
                                    bn_eps, bn_scale, bn_offset, bwd_slab, Xw, opt, lr, step, s0w, s1w, s0b, s1b,
                                    scale, bn_tab, part, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                   nullptr, nullptr, 1, 1.f, st);
+                                   nullptr, nullptr, 1, 1.f, 0, 0.f, st);
 }
 
 // ... plus the head epilogue (hy != null): dWh / dbh of the row-per-workgroup head and the
@@ -607,7 +609,7 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
                                  float scale, const float* bn_tab, float* part, unsigned* cnt,
                                       const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
                                       const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
-                                      hipStream_t st) {
+                                      int hact, float halpha, hipStream_t st) {
   if (!csa_dense_bwd_update_ok(M, K, N, bn_slab ? bn_C : 0)) return -1;
   if (hy && (!hdl || !hgw || !hgb || !hrl || !hrc || !ring_loss || !ring_correct || ring < 1 || !step)) return -2;
   if (!Xw || !W || !dY) return -2;
@@ -623,6 +625,7 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
   a.part = part; a.cnt = cnt;
   a.hy = hy; a.hdl = hdl; a.hgw = hgw; a.hgb = hgb; a.hrl = hrl; a.hrc = hrc;
   a.ring_loss = ring_loss; a.ring_correct = ring_correct; a.ring = ring; a.ldiv = ldiv;
+  a.hact = hact; a.halpha = halpha;
   if (a.cs > 1 && dX && (!part || !cnt)) return -2;
   const int blocks = groups * a.cs;
   const int ns = opt_nslots(opt);

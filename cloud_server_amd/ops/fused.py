@@ -59,7 +59,7 @@ _SIGS = {
                                  P, P, P, P, F, P, P, P, P]),
     "csa_dense_bwd_update_ws": (I, [I, I, P]),
     "csa_dense_bwd_update_head": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
-                                      P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, P]),
+                                      P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, I, F, P]),
     "csa_head_row_ok": (I, [I, I]),
     "csa_head_row": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, L, P]),
     "csa_head_part_rows": (I, [I, I]),

@@ -1343,9 +1343,10 @@ class HipProgram:
             G = self.gviews
             head = (K.ptr(u.y), K.ptr(self.hdl), K.ptr(G["head.weight"]), K.ptr(G["head.bias"]),
                     K.ptr(self.hrl), K.ptr(self.hrc), K.ptr(e.ring_loss), K.ptr(e.ring_correct),
-                    e.ring_correct.numel(), float(B if e.cfg.loss_name == "entropy" else B * 10))
+                    e.ring_correct.numel(), float(B if e.cfg.loss_name == "entropy" else B * 10),
+                    _act_id(self.head_tf.act), _alpha(self.head_tf.act))
         else:
-            head = (None, None, None, None, None, None, None, None, 1, 1.0)
+            head = (None, None, None, None, None, None, None, None, 1, 1.0, 0, 0.0)
         self._rc(lib.csa_dense_bwd_update_head(
             K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
             K.ptr(prev.dy) if prev is not None else None, B, fin, fout,
