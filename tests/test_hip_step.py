@@ -245,8 +245,8 @@ def test_batch_sizes_match_torch(batch):
 
 def test_fused_update_path_active_and_matches_unfused(monkeypatch):
     """Single-GPU program: the dense layers' backward applies the optimizer in-kernel
-    (csa_dense_bwd_update) and the head writes partial gradients folded by the small
-    optimizer launch.  Several Adam / Adagrad steps match the unfused program (materialised
+    (csa_dense_bwd_update) and the row-per-workgroup head's batch reductions (dWh, dbh,
+    metric ring) ride in the last dense layer's fused backward.  Several Adam / Adagrad steps match the unfused program (materialised
     gradients + the flat optimizer) and the metric ring agrees."""
     ds = synthetic_mnist(600, seed=17)
     for opt in ("AdamOptimizer", "AdagradOptimizer"):
@@ -257,7 +257,7 @@ def test_fused_update_path_active_and_matches_unfused(monkeypatch):
         a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "0")
         b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
-        assert a.program.fused and a.program.head_rg > 0
+        assert a.program.fused and a.program.head_row and a.program.head_rg == 0
         assert [u.fused for u in a.program.units if u.kind == "dense"] == [True, True]
         assert not b.program.fused
         for _ in range(5):
