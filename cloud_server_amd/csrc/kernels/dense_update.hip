@@ -85,7 +85,7 @@ struct DUArgs {
 };
 
 constexpr int DU_HNC = 10;           // head classes
-constexpr int DU_HPF = 12;           // prefetched (hy, dl) pairs per thread
+
 
 // diagnostics: s_memrealtime stamps (100 MHz, one clock for all XCDs) of EVERY block,
 // [block][8] = start, dY staged, W landed, MFMA + update done, fold done, dX stored, end
@@ -129,78 +129,64 @@ __device__ __forceinline__ void du_store_w(const DUArgs& a, const float4 (&wv)[D
 // NSLOT = optimizer slots (0 SGD, 1 Adagrad, 2 Adam / Adadelta): unused slot registers
 // are not allocated.  WAVES = 16 (one block per row group, all N <= 512 columns) or 4
 // (128 columns per block, cs blocks per row group: narrow layers use more CUs).
-// Head epilogue, part 1: this block's dWh rows [hn0, hn1) — output o = (n, j) handled by
-// THREADS / outs m-slices; the (hy, dl) operands of the first DU_HPF rows of the slice are
-// requested at kernel start so their latency hides under the layer's own work.
+// Head epilogue.  Block (row group grp, column block cblk) owns the dWh rows
+// n in [hn0, hn0 + nh) of its column block (nh = ceil(nb / groups)).  Its operands are tiny
+// — hy[:, hn0 .. hn0 + nh) (M x nh, contiguous per row) and all of dl (M x 10) — and are
+// requested right after the layer's own loads (vmcnt retires in order), staged to LDS at
+// the end, then one thread per (n, j) output sums the batch in fixed order.
+constexpr int DU_HMAXR = 8;          // staged dWh rows per block (more: direct global loop)
+
 struct DUHead {
-  int hn0, outs, nsl, o, sl;
-  float hv[DU_HPF], dv[DU_HPF];
+  int hn0, nh;
+  float hy[DU_HMAXR];      // lane (m = t / 8, r = t % 8) of threads t < 8 M
+  float dl[2];             // dl elements t and t + THREADS (THREADS >= 256 > M * 10 / 2)
 };
 
 template <int THREADS>
 __device__ __forceinline__ void du_head_prefetch(const DUArgs& a, int grp, int groups, int cb, int nb, DUHead& h) {
   const int hper = (nb + groups - 1) / groups;
   h.hn0 = cb + grp * hper;
-  const int nh = max(0, min(hper, cb + nb - h.hn0));
-  h.outs = nh * DU_HNC;
-  h.nsl = h.outs > 0 && h.outs <= THREADS ? THREADS / h.outs : 0;   // 0: direct loop (no prefetch)
-  const int t = threadIdx.x;
-  h.o = h.outs > 0 ? t % h.outs : 0;
-  h.sl = h.outs > 0 ? t / h.outs : THREADS;
-  const int n = h.hn0 + h.o / DU_HNC, j = h.o % DU_HNC;
-  if (h.nsl == 0) return;
-#pragma unroll
-  for (int u = 0; u < DU_HPF; ++u) {
-    const int m = min(h.sl + u * h.nsl, a.M - 1);
-    h.hv[u] = a.hy[(long)m * a.N + min(n, a.N - 1)];
-    h.dv[u] = a.hdl[m * DU_HNC + j];
-  }
+  h.nh = max(0, min(hper, cb + nb - h.hn0));
+  const int t = threadIdx.x, m = t / DU_HMAXR, r = t % DU_HMAXR;
+  h.hy[0] = a.hy[(long)min(m, a.M - 1) * a.N + min(h.hn0 + min(r, max(h.nh - 1, 0)), a.N - 1)];
+  const int n10 = a.M * DU_HNC;
+  h.dl[0] = a.hdl[min(t, n10 - 1)];
+  h.dl[1] = a.hdl[min(t + THREADS, n10 - 1)];
 }
 
 template <int THREADS>
 __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float* s_hw) {
-  const int t = threadIdx.x;
-  if (h.nsl == 0) {                                       // more outputs than threads
-    for (int o = t; o < h.outs; o += THREADS) {
-      const int n = h.hn0 + o / DU_HNC, j = o % DU_HNC;
-      float v = 0.f;
-      for (int m = 0; m < a.M; ++m)
-        v = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), a.hdl[m * DU_HNC + j], v);
-      a.hgw[(long)n * DU_HNC + j] = v;
-    }
-  }
-  float acc = 0.f;
-  if (h.sl < h.nsl) {
-    const int n = h.hn0 + h.o / DU_HNC, j = h.o % DU_HNC;
-#pragma unroll
-    for (int u = 0; u < DU_HPF; ++u) {
-      pin(h.hv[u]); pin(h.dv[u]);
-      if (h.sl + u * h.nsl < a.M) acc = fmaf(act_fwd(h.hv[u], a.hact, a.halpha), h.dv[u], acc);
-    }
-    for (int m = h.sl + DU_HPF * h.nsl; m < a.M; m += h.nsl)      // beyond the prefetch
-      acc = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), a.hdl[m * DU_HNC + j], acc);
-    s_hw[t] = acc;
-  }
+  // s_hw: [64][DU_HMAXR] act(hy) | [64][10] dl
+  const int t = threadIdx.x, M = a.M;
+  float* s_y = s_hw;
+  float* s_d = s_hw + 64 * DU_HMAXR;
+  pin(h.hy[0]); pin(h.dl[0]); pin(h.dl[1]);
+  if (t < M * DU_HMAXR) s_y[t] = act_fwd(h.hy[0], a.hact, a.halpha);
+  if (t < M * DU_HNC) s_d[t] = h.dl[0];
+  if (t + THREADS < M * DU_HNC) s_d[t + THREADS] = h.dl[1];
   __syncthreads();
-  if (h.nsl > 0 && t < h.outs) {                          // slices folded in fixed order
+  const int outs = h.nh * DU_HNC;
+  for (int o = t; o < outs; o += THREADS) {
+    const int rr = o / DU_HNC, j = o - rr * DU_HNC, n = h.hn0 + rr;
     float v = 0.f;
-    for (int q = 0; q < h.nsl; ++q) v += s_hw[q * h.outs + t];
-    a.hgw[(long)(h.hn0 + t / DU_HNC) * DU_HNC + t % DU_HNC] = v;
+    if (h.nh <= DU_HMAXR) {
+      for (int m = 0; m < M; ++m) v = fmaf(s_y[m * DU_HMAXR + rr], s_d[m * DU_HNC + j], v);
+    } else {
+      for (int m = 0; m < M; ++m) v = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), s_d[m * DU_HNC + j], v);
+    }
+    a.hgw[(long)n * DU_HNC + j] = v;
   }
   if (blockIdx.x == gridDim.x - 1) {                      // dbh and the step's metrics
     const int lane = t & 63, w = t >> 6;
     if (w == 0) {
-      float db[DU_HNC];
-#pragma unroll
-      for (int j = 0; j < DU_HNC; ++j) db[j] = lane < a.M ? a.hdl[lane * DU_HNC + j] : 0.f;
-#pragma unroll
-      for (int j = 0; j < DU_HNC; ++j) {
-        const float v = wave_sum(db[j]);
-        if (lane == 0) a.hgb[j] = v;
+      if (lane < DU_HNC) {
+        float v = 0.f;
+        for (int m = 0; m < M; ++m) v += s_d[m * DU_HNC + lane];
+        a.hgb[lane] = v;
       }
     } else if (w == 1) {
-      float l = lane < a.M ? a.hrl[lane] : 0.f;
-      float c = lane < a.M ? (float)a.hrc[lane] : 0.f;
+      float l = lane < M ? a.hrl[lane] : 0.f;
+      float c = lane < M ? (float)a.hrc[lane] : 0.f;
       l = wave_sum(l);
       c = wave_sum(c);
       if (lane == 0) {
@@ -235,9 +221,8 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
   const int C = a.bn.C > 0 ? a.bn.C : 1;
   constexpr int nslot = NSLOT;
   DU_STAMP(0);
-  __shared__ float s_hw[HEAD ? THREADS : 1];
+  __shared__ float s_hw[HEAD ? 64 * (DU_HMAXR + DU_HNC) : 1];
   DUHead hd;
-  if (HEAD) du_head_prefetch<THREADS>(a, grp, groups, cb, nb, hd);
 
   // ---- every load, issued in the order it is consumed (vmcnt retires in order).  Two
   // column halves: half j = block columns [HW j, HW (j + 1)) = every wave's sub-tile j, so
@@ -303,6 +288,8 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
   const bool eitem = tid < 256;
   const float* xsrc = tf && a.x_fwd ? a.x_fwd : a.Xw;      // address select (same [M][K] shape)
   float4 xf = *reinterpret_cast<const float4*>(xsrc + (long)min(em, M - 1) * K + f0 + min(fq, nf - 4));
+  // (5) head epilogue operands (last dense layer only)
+  if (HEAD) du_head_prefetch<THREADS>(a, grp, groups, cb, nb, hd);
 
   const float lr = opt_step_lr(a.opt, a.lr, a.step);
   du_f32x4 dacc[4];
