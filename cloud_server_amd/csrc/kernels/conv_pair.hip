@@ -837,6 +837,178 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
   CP_STAMP(15);
 }
 
+// ---------------------------------------------------------------------------------------
+// Small-pair VALU forward (round 3).  For the DSL's typical first pair — the sample's
+// conv[2,2,10] -> conv[2,2,20] -> pool is 40 MACs per conv-B output — the MFMA forward
+// above spent its time in dependent LDS phases (offset tables, 16x16x4 tiles for K = 4,
+// per-tile epilogues: stamps convA 2.2 us, convB+pool 3.4 us of a 12.9 us launch).  Here
+// every phase is one pass of plain FMAs over LDS with the whole workgroup busy:
+//   loads   weights of both convs, biases and the band's uint8 input rows in ONE batch
+//   conv A  one thread per c1 value of the band's tile (+ act A, zero outside the image)
+//   conv B  one thread per (unit pixel, output channel): the pool window's positions
+//           (+ bias, act B, max + argmax) with every weight read once per position
+//   stats   per-channel {sum, sum^2} of the band folded in fixed order, one row per band
+//           workgroup or an atomic fold into nslab rows
+// Family (cpv_ok): C0 <= 4, C1 <= 16, C2 <= 32, kernels <= 3x3, and the weights / input
+// tile fit one register batch of the workgroup.
+constexpr int CPV_T = 256;
+constexpr int CPV_MAXC1 = 16, CPV_MAXC2 = 32, CPV_MAXTAPS = 9;
+constexpr int CPV_UW = 8, CPV_UX = 2;                  // per-thread load batch (weights, x)
+
+struct CPVFwdArgs {
+  CPGeom g;
+  const uint8_t* img; const int64_t* idx; const int64_t* cursor;
+  const float* wA; const float* bA; int actA; float alphaA;
+  const float* wB; const float* bB; int actB; float alphaB;
+  float* y; uint8_t* argmax; float* stat; int nslab;
+};
+
+__host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 1 + g.KAw - 1; }
+
+__global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
+  const CPGeom& g = a.g;
+  __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
+  __shared__ float s_b[CPV_MAXC1 + CPV_MAXC2];
+  __shared__ float s_x[CPV_UX * CPV_T];
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // c1 tile | unit outputs
+  const int b = blockIdx.x / g.nbands, band = blockIdx.x % g.nbands;
+  const int pr0 = band * g.PR, pr1 = min(g.PH, pr0 + g.PR);
+  const int r2a = g.pool ? 2 * pr0 : pr0, r2b = g.pool ? min(g.H2, 2 * pr1) : pr1;
+  const CPBand t = cp_band(g, r2a, r2b);
+  const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
+  const int nwA = KA * g.C1, nw = nwA + KB * g.C2, nb = g.C1 + g.C2;
+  const int nX = t.TXH * t.TXW * g.C0;
+  const int tid = threadIdx.x;
+  CP_STAMP(0);
+  // ---- one batch of loads: weights + biases first, then the image rows (the staged
+  // image is at a fixed address; otherwise its row index chain runs under the weights)
+  float wv[CPV_UW];
+#pragma unroll
+  for (int u = 0; u < CPV_UW; ++u) {
+    const int e = u * CPV_T + tid;
+    const float* p = e < nwA ? a.wA + e : (e < nw ? a.wB + (e - nwA) : a.wA);
+    wv[u] = *p;
+  }
+  float bv = 0.f;
+  if (tid < nb) bv = tid < g.C1 ? (a.bA ? a.bA[tid] : 0.f) : (a.bB ? a.bB[tid - g.C1] : 0.f);
+  const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
+  const int y0 = t.c1y0 - g.PTA, x0 = -g.PLB - g.PLA;
+  uint8_t xv[CPV_UX];
+  bool xok[CPV_UX];
+#pragma unroll
+  for (int u = 0; u < CPV_UX; ++u) {
+    const int e = u * CPV_T + tid;
+    const int c = e % g.C0, rem = e / g.C0, xx = rem % t.TXW, r = rem / t.TXW;
+    const int yy = y0 + r, xg = x0 + xx;
+    xok[u] = e < nX && yy >= 0 && yy < g.H && xg >= 0 && xg < g.W;
+    xv[u] = src[xok[u] ? ((long)yy * g.W + xg) * g.C0 + c : 0];
+  }
+#pragma unroll
+  for (int u = 0; u < CPV_UW; ++u) pin(wv[u]);
+#pragma unroll
+  for (int u = 0; u < CPV_UW; ++u) {
+    const int e = u * CPV_T + tid;
+    if (e < nw) s_w[e] = wv[u];
+  }
+  if (tid < nb) s_b[tid] = bv;
+#pragma unroll
+  for (int u = 0; u < CPV_UX; ++u) {
+    const int e = u * CPV_T + tid;
+    if (e < nX) s_x[e] = xok[u] ? (float)xv[u] * (1.0f / 255.0f) : 0.f;
+  }
+  __syncthreads();
+  CP_STAMP(1);
+  // ---- conv A: the c1 tile [T1H][T1W][C1] (zero outside [0, H1) x [0, W1))
+  float* s_c1 = smem;
+  const int n1 = t.T1H * t.T1W * g.C1;
+  for (int e = tid; e < n1; e += CPV_T) {
+    const int c1 = e % g.C1, pix = e / g.C1, tx = pix % t.T1W, ty = pix / t.T1W;
+    const int yy = t.c1y0 + ty, xx = tx - g.PLB;
+    float v = 0.f;
+    if (yy >= 0 && yy < g.H1 && xx >= 0 && xx < g.W1) {
+      float acc = s_b[c1];
+      for (int i = 0; i < g.KAh; ++i)
+        for (int j = 0; j < g.KAw; ++j) {
+          const float* xr = s_x + ((ty + i) * t.TXW + tx + j) * g.C0;
+          const float* wr = s_w + ((i * g.KAw + j) * g.C0) * g.C1 + c1;
+          for (int c0 = 0; c0 < g.C0; ++c0) acc = fmaf(xr[c0], wr[c0 * g.C1], acc);
+        }
+      v = act_fwd(acc, a.actA, a.alphaA);
+    }
+    s_c1[e] = v;
+  }
+  __syncthreads();
+  CP_STAMP(2);
+  // ---- conv B (+ act B, + max-pool): one thread per (unit pixel, channel)
+  const int ow = g.pool ? g.PW : g.W2;
+  const int nunit = (g.pool ? (pr1 - pr0) : (r2b - r2a)) * ow;
+  const int nout = nunit * g.C2;
+  float* s_out = s_c1 + ((n1 + 3) & ~3);                  // [nunit][C2] outputs for the stats
+  const float* wB = s_w + nwA;
+  const int npos = g.pool ? 4 : 1;
+  for (int o = tid; o < nout; o += CPV_T) {
+    const int c2 = o % g.C2, u = o / g.C2, py = u / ow, px = u - py * ow;
+    float best = -INFINITY;
+    int am = 0;
+    for (int pos = 0; pos < npos; ++pos) {
+      const int y2 = g.pool ? 2 * (pr0 + py) + (pos >> 1) : r2a + py;
+      const int x2 = g.pool ? 2 * px + (pos & 1) : px;
+      if (y2 >= g.H2 || x2 >= g.W2) continue;
+      float acc = s_b[g.C1 + c2];
+      for (int i = 0; i < g.KBh; ++i)
+        for (int j = 0; j < g.KBw; ++j) {
+          const float* cr = s_c1 + ((y2 - r2a + i) * t.T1W + x2 + j) * g.C1;
+          const float* wr = wB + ((i * g.KBw + j) * g.C1) * g.C2 + c2;
+#pragma unroll 4
+          for (int c1 = 0; c1 < g.C1; ++c1) acc = fmaf(cr[c1], wr[c1 * g.C2], acc);
+        }
+      const float v = act_fwd(acc, a.actB, a.alphaB);
+      if (v > best) { best = v; am = pos; }
+    }
+    const long off = g.pool ? (((long)b * g.PH + pr0) * g.PW) * g.C2 + o
+                            : (((long)b * g.H2 + r2a) * g.W2) * g.C2 + o;
+    a.y[off] = best;
+    if (g.pool && a.argmax) a.argmax[off] = (uint8_t)am;
+    s_out[o] = best;
+  }
+  CP_STAMP(3);
+  if (a.stat) {                                           // per-channel sums, fixed order
+    __syncthreads();
+    if (tid < 2 * g.C2) {
+      const int c = tid % g.C2, sq = tid / g.C2;
+      float acc = 0.f;
+      for (int u = 0; u < nunit; ++u) {
+        const float v = s_out[u * g.C2 + c];
+        acc += sq ? v * v : v;
+      }
+      float* row = a.stat + (size_t)(blockIdx.x % a.nslab) * 2 * g.C2;
+      if (a.nslab >= (int)gridDim.x) row[tid] = acc;     // one row per workgroup: plain store
+      else atomicAdd(&row[tid], acc);
+    }
+  }
+  CP_STAMP(4);
+}
+
+static bool cpv_ok(const CPGeom& g) {
+  if (getenv("CSA_CP_MFMA")) return false;               // force the MFMA family (A/B)
+  if (g.C0 > 4 || g.C1 > CPV_MAXC1 || g.C2 > CPV_MAXC2) return false;
+  if (g.KAh * g.KAw > CPV_MAXTAPS || g.KBh * g.KBw > CPV_MAXTAPS) return false;
+  if (g.pool && (g.PH * 2 > g.H2 + 1 || g.PW * 2 > g.W2 + 1)) return false;
+  const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
+  if (KA * g.C1 + KB * g.C2 > CPV_UW * CPV_T) return false;
+  const int rows = g.pool ? 2 * g.PR : g.PR;
+  const int TXH = rows + g.KBh - 1 + g.KAh - 1;
+  if (TXH * cpv_txw(g) * g.C0 > CPV_UX * CPV_T) return false;
+  return true;
+}
+
+static size_t cpv_fwd_lds(const CPGeom& g) {
+  const int rows = g.pool ? 2 * g.PR : g.PR;
+  const int T1H = rows + g.KBh - 1, T1W = g.W2 + g.KBw - 1;
+  const int units = (g.pool ? g.PR * g.PW : g.PR * g.W2);
+  return (size_t)(((T1H * T1W * g.C1 + 3) & ~3) + units * g.C2) * sizeof(float);
+}
+
 static bool cp_geom(const int* v, CPGeom& g) {
   g = CPGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15],
              v[16], v[17], v[18], v[19], v[20], 0, 0};
@@ -922,6 +1094,11 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.bB = bB; a.actB = actB; a.alphaB = alphaB; a.y = y; a.argmax = argmax; a.stat = stat;
   a.nslab = nslab < 1 ? 1 : nslab;
+  if (cpv_ok(a.g)) {
+    CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab};
+    hipLaunchKernelGGL(cpv_fwd_kernel, dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
+    return (int)hipGetLastError();
+  }
   static bool attr = hipFuncSetAttribute((const void*)conv_pair_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
