@@ -139,7 +139,7 @@ constexpr int DU_HMAXR = 8;          // staged dWh rows per block (more: direct 
 struct DUHead {
   int hn0, nh;
   float hy[2];             // staged hy elements e = t + u THREADS: m = e / 8, r = e % 8 (e < 8 M)
-  float dl[2];             // dl elements t and t + THREADS (THREADS >= 256 > M * 10 / 2)
+  float dl[3];             // dl elements t + u THREADS (M * 10 <= 640 <= 3 * 256)
 };
 
 template <int THREADS>
@@ -154,8 +154,8 @@ __device__ __forceinline__ void du_head_prefetch(const DUArgs& a, int grp, int g
     h.hy[u] = a.hy[(long)min(m, a.M - 1) * a.N + min(h.hn0 + min(r, max(h.nh - 1, 0)), a.N - 1)];
   }
   const int n10 = a.M * DU_HNC;
-  h.dl[0] = a.hdl[min(t, n10 - 1)];
-  h.dl[1] = a.hdl[min(t + THREADS, n10 - 1)];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) h.dl[u] = a.hdl[min(t + u * THREADS, n10 - 1)];
 }
 
 template <int THREADS>
@@ -164,11 +164,12 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
   const int t = threadIdx.x, M = a.M;
   float* s_y = s_hw;
   float* s_d = s_hw + 64 * DU_HMAXR;
-  pin(h.hy[0]); pin(h.hy[1]); pin(h.dl[0]); pin(h.dl[1]);
+  pin(h.hy[0]); pin(h.hy[1]); pin(h.dl[0]); pin(h.dl[1]); pin(h.dl[2]);
   if (t < M * DU_HMAXR) s_y[t] = act_fwd(h.hy[0], a.hact, a.halpha);
   if (t + THREADS < M * DU_HMAXR) s_y[t + THREADS] = act_fwd(h.hy[1], a.hact, a.halpha);
-  if (t < M * DU_HNC) s_d[t] = h.dl[0];
-  if (t + THREADS < M * DU_HNC) s_d[t + THREADS] = h.dl[1];
+#pragma unroll
+  for (int u = 0; u < 3; ++u)
+    if (t + u * THREADS < M * DU_HNC) s_d[t + u * THREADS] = h.dl[u];
   __syncthreads();
   const int outs = h.nh * DU_HNC;
   for (int o = t; o < outs; o += THREADS) {
