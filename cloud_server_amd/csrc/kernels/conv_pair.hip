@@ -989,6 +989,289 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
   CP_STAMP(4);
 }
 
+// Small-pair VALU backward (round 3).  One workgroup per (image, band) as the MFMA
+// backward, but every phase is one FMA pass over LDS with all 256 threads:
+//   loads   both weight blocks, the band's input rows, the route operands (dz, y, argmax
+//           of the unit rows the band's dc2 tile touches) and both BatchNorm slabs — one
+//           batch, every load in flight before the first use
+//   P1      BN tables (fwd slab -> mean / rstd / a, bwd slab -> S1 / S2, rows summed in
+//           fixed order) and the c1 tile recomputed from the input rows
+//   P2      route: dc2 tile = act_B'(BN'(dz)) placed at the argmax position of each unit
+//   P3      conv-B weight gradient (owned conv-B pixels) | dc1 of the owned c1 pixels
+//           through act A | conv-B bias gradient
+//   P4      conv-A weight / bias gradients; weight gradients leave as one atomic per
+//           (workgroup, weight) into stripe blockIdx % S, folded by the optimizer
+constexpr int CPV_UR = 4;                                // route operand batch per thread
+constexpr int CPV_US = 8;                                // slab values per thread (fwd + bwd)
+
+struct CPVBwdTile {
+  int o2a, o2b, o1a, o1b;        // owned conv-B output rows / owned c1 rows
+  int d2a, d2b;                  // dc2 tile rows (owned conv-B rows + halo for dc1)
+  int c1a, c1b, T1W;             // c1 tile rows; columns tx <-> c1 x = tx - PLB
+  int xa, TXH, TXW;              // x tile: rows xa .., cols tx <-> x = tx - PLB - PLA
+  int ua, ub;                    // unit rows of the route operands
+};
+
+__host__ __device__ inline CPVBwdTile cpv_bwd_tile(const CPGeom& g, int band) {
+  CPVBwdTile t;
+  const int pr0 = band * g.PR, pr1 = min(g.PH, pr0 + g.PR);
+  const bool last = band == g.nbands - 1;
+  t.o2a = g.pool ? 2 * pr0 : pr0;
+  t.o2b = g.pool ? (last ? g.H2 : 2 * pr1) : pr1;
+  t.o1a = t.o2a;
+  t.o1b = last ? g.H1 : t.o2b;
+  t.d2a = max(0, min(t.o2a, t.o1a + g.PTB - g.KBh + 1));
+  t.d2b = min(g.H2, max(t.o2b, t.o1b + g.PTB));
+  t.c1a = min(t.o2a - g.PTB, t.o1a);
+  t.c1b = max(t.o2b - g.PTB + g.KBh - 1, t.o1b);
+  t.T1W = g.W2 + g.KBw - 1;
+  t.xa = t.c1a - g.PTA;
+  t.TXH = (t.c1b - t.c1a) + g.KAh - 1;
+  t.TXW = t.T1W + g.KAw - 1;
+  t.ua = g.pool ? t.d2a / 2 : t.d2a;
+  t.ub = g.pool ? min(g.PH, (t.d2b + 1) / 2) : t.d2b;
+  return t;
+}
+
+struct CPVBwdLds { int x, c1, dc2, dc1, red, end; };
+
+__host__ __device__ inline CPVBwdLds cpv_bwd_lds(const CPGeom& g, const CPVBwdTile& t) {
+  CPVBwdLds L;
+  int o = 0;
+  L.x = o; o += (t.TXH * t.TXW * g.C0 + 3) & ~3;
+  L.c1 = o; o += ((t.c1b - t.c1a) * t.T1W * g.C1 + 3) & ~3;
+  L.dc2 = o; o += ((t.d2b - t.d2a) * g.W2 * g.C2 + 3) & ~3;
+  L.dc1 = o; o += ((t.o1b - t.o1a) * g.W1 * g.C1 + 3) & ~3;
+  L.red = o; o += (32 + 16) * 2 * CPV_MAXC2;            // slab rows (fwd | bwd) staged for the fold
+  L.end = o;
+  return L;
+}
+
+__global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
+  const CPGeom& g = a.g;
+  __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
+  __shared__ float s_bA[CPV_MAXC1];
+  __shared__ float s_bn[6 * CPV_MAXC2];                 // mean | rstd | a | S1 | S2 | -
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int b = blockIdx.x / g.nbands, band = blockIdx.x % g.nbands;
+  const CPVBwdTile t = cpv_bwd_tile(g, band);
+  const CPVBwdLds L = cpv_bwd_lds(g, t);
+  float* s_x = smem + L.x;
+  float* s_c1 = smem + L.c1;
+  float* s_dc2 = smem + L.dc2;
+  float* s_dc1 = smem + L.dc1;
+  float* s_red = smem + L.red;
+  const int tid = threadIdx.x;
+  const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
+  const int nwA = KA * g.C1, nw = nwA + KB * g.C2;
+  const int C2x2 = 2 * g.C2;
+  const int ow = g.pool ? g.PW : g.W2;
+  const int nroute = (t.ub - t.ua) * ow * g.C2;
+  const long rbase = ((long)b * (g.pool ? g.PH : g.H2) + t.ua) * ow * g.C2;
+  const int nX = t.TXH * t.TXW * g.C0;
+  const int nsf = a.bn_on ? a.bn.nslab * C2x2 : 0, nsb = a.bn_on ? a.bwd_nslab * C2x2 : 0;
+  CP_STAMP(8);
+  // ---- one batch of loads
+  float wv[CPV_UW];
+#pragma unroll
+  for (int u = 0; u < CPV_UW; ++u) {
+    const int e = u * CPV_T + tid;
+    wv[u] = *(e < nwA ? a.wA + e : (e < nw ? a.wB + (e - nwA) : a.wA));
+  }
+  const float bav = (a.bA && tid < g.C1) ? a.bA[tid] : 0.f;
+  float rz[CPV_UR], ry[CPV_UR];
+  int ram[CPV_UR];
+#pragma unroll
+  for (int u = 0; u < CPV_UR; ++u) {
+    const int e = min(u * CPV_T + tid, max(nroute - 1, 0));
+    rz[u] = a.dz[rbase + e];
+    ry[u] = a.y[rbase + e];
+    ram[u] = g.pool ? (int)a.argmax[rbase + e] : 0;
+  }
+  float sv[CPV_US];
+#pragma unroll
+  for (int u = 0; u < CPV_US; ++u) {
+    const int e = u * CPV_T + tid;
+    const float* p = e < nsf ? a.bn.slab + e : (e < nsf + nsb ? a.bwd_slab + (e - nsf) : a.wA);
+    sv[u] = *p;
+  }
+  float sc = 0.f, of = 0.f;
+  if (a.bn_on && tid < g.C2) { sc = a.bn.scale[tid]; of = a.bn.offset[tid]; }
+  const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
+  uint8_t xv[CPV_UX];
+  bool xok[CPV_UX];
+#pragma unroll
+  for (int u = 0; u < CPV_UX; ++u) {
+    const int e = u * CPV_T + tid;
+    const int c = e % g.C0, rem = e / g.C0, xx = rem % t.TXW, r = rem / t.TXW;
+    const int yy = t.xa + r, xg = xx - g.PLB - g.PLA;
+    xok[u] = e < nX && yy >= 0 && yy < g.H && xg >= 0 && xg < g.W;
+    xv[u] = src[xok[u] ? ((long)yy * g.W + xg) * g.C0 + c : 0];
+  }
+  // ---- LDS stores
+#pragma unroll
+  for (int u = 0; u < CPV_UW; ++u) {
+    pin(wv[u]);
+    const int e = u * CPV_T + tid;
+    if (e < nw) s_w[e] = wv[u];
+  }
+  if (tid < g.C1) s_bA[tid] = bav;
+#pragma unroll
+  for (int u = 0; u < CPV_US; ++u) {
+    pin(sv[u]);
+    const int e = u * CPV_T + tid;
+    if (e < nsf + nsb) s_red[e] = sv[u];
+  }
+#pragma unroll
+  for (int u = 0; u < CPV_UX; ++u) {
+    const int e = u * CPV_T + tid;
+    if (e < nX) s_x[e] = xok[u] ? (float)xv[u] * (1.0f / 255.0f) : 0.f;
+  }
+  const int n2 = (t.d2b - t.d2a) * g.W2 * g.C2;
+  for (int e = tid; e < n2; e += CPV_T) s_dc2[e] = 0.f;
+  __syncthreads();
+  CP_STAMP(9);
+  // ---- P1: BN tables (rows summed in fixed order) | c1 tile
+  if (a.bn_on && tid < g.C2) {
+    const int c = tid;
+    float s1 = 0.f, s2 = 0.f, b1 = 0.f, b2 = 0.f;
+    for (int r = 0; r < a.bn.nslab; ++r) { s1 += s_red[r * C2x2 + c]; s2 += s_red[r * C2x2 + g.C2 + c]; }
+    for (int r = 0; r < a.bwd_nslab; ++r) { b1 += s_red[nsf + r * C2x2 + c]; b2 += s_red[nsf + r * C2x2 + g.C2 + c]; }
+    const float mean = s1 / a.bn.count;
+    const float var = fmaxf(s2 / a.bn.count - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + a.bn.eps);
+    s_bn[c] = mean;
+    s_bn[CPV_MAXC2 + c] = rstd;
+    s_bn[2 * CPV_MAXC2 + c] = sc * rstd;
+    s_bn[3 * CPV_MAXC2 + c] = b1;
+    s_bn[4 * CPV_MAXC2 + c] = b2;
+    if (blockIdx.x == 0) {
+      a.doffset[c] = b1;
+      a.dscale[c] = b2;
+      if (a.run_mean) {
+        a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
+        a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var;
+      }
+    }
+  }
+  (void)of;
+  const int n1 = (t.c1b - t.c1a) * t.T1W * g.C1;
+  for (int e = tid; e < n1; e += CPV_T) {
+    const int c1 = e % g.C1, pix = e / g.C1, tx = pix % t.T1W, ty = pix / t.T1W;
+    const int yy = t.c1a + ty, xx = tx - g.PLB;
+    float v = 0.f;
+    if (yy >= 0 && yy < g.H1 && xx >= 0 && xx < g.W1) {
+      float acc = s_bA[c1];
+      for (int i = 0; i < g.KAh; ++i)
+        for (int j = 0; j < g.KAw; ++j) {
+          const float* xr = s_x + ((ty + i) * t.TXW + tx + j) * g.C0;
+          const float* wr = s_w + ((i * g.KAw + j) * g.C0) * g.C1 + c1;
+          for (int c0 = 0; c0 < g.C0; ++c0) acc = fmaf(xr[c0], wr[c0 * g.C1], acc);
+        }
+      v = act_fwd(acc, a.actA, a.alphaA);
+    }
+    s_c1[e] = v;
+  }
+  __syncthreads();
+  CP_STAMP(10);
+  // ---- P2: route into the dc2 tile (registers hold the operands since the prologue)
+  {
+    const float inv_n = a.bn_on ? 1.0f / a.bn.count : 0.f;
+#pragma unroll
+    for (int u = 0; u < CPV_UR; ++u) {
+      const int e = u * CPV_T + tid;
+      if (e >= nroute) break;
+      const int c = e % g.C2, pix = e / g.C2, px = pix % ow, uy = pix / ow;
+      float gv = rz[u];
+      if (a.bn_on) {
+        const float xhat = (ry[u] - s_bn[c]) * s_bn[CPV_MAXC2 + c];
+        gv = s_bn[2 * CPV_MAXC2 + c] * (gv - s_bn[3 * CPV_MAXC2 + c] * inv_n - xhat * s_bn[4 * CPV_MAXC2 + c] * inv_n);
+      }
+      gv = act_bwd(gv, ry[u], ry[u], a.actB, a.alphaB);
+      const int y2 = g.pool ? 2 * (t.ua + uy) + (ram[u] >> 1) : t.ua + uy;
+      const int x2 = g.pool ? 2 * px + (ram[u] & 1) : px;
+      if (y2 >= t.d2a && y2 < t.d2b && x2 < g.W2) s_dc2[((y2 - t.d2a) * g.W2 + x2) * g.C2 + c] = gv;
+    }
+  }
+  __syncthreads();
+  CP_STAMP(11);
+  const int sidx = blockIdx.x % a.stripes;
+  // ---- P3a: conv-B weight gradient over the owned conv-B pixels
+  {
+    const int nB = KB * g.C2;
+    const float* wB = s_w + nwA;
+    (void)wB;
+    for (int o = tid; o < nB; o += CPV_T) {
+      const int c2 = o % g.C2, k = o / g.C2, c1 = k % g.C1, ij = k / g.C1, i = ij / g.KBw, j = ij - i * g.KBw;
+      float acc = 0.f;
+      for (int y2 = t.o2a; y2 < t.o2b; ++y2) {
+        const float* cr = s_c1 + ((y2 - g.PTB + i - t.c1a) * t.T1W + j) * g.C1 + c1;
+        const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2) * g.C2 + c2;
+#pragma unroll 4
+        for (int x2 = 0; x2 < g.W2; ++x2) acc = fmaf(cr[x2 * g.C1], dr[x2 * g.C2], acc);
+      }
+      atomicAdd(&a.dwB[(long)sidx * nB + o], acc);
+    }
+  }
+  // ---- P3b: dc1 of the owned c1 pixels (through act A) | P3c: conv-B bias gradient
+  {
+    const float* wB = s_w + nwA;
+    const int nd = (t.o1b - t.o1a) * g.W1 * g.C1;
+    for (int e = tid; e < nd; e += CPV_T) {
+      const int c1 = e % g.C1, pix = e / g.C1, x1 = pix % g.W1, y1 = t.o1a + pix / g.W1;
+      float acc = 0.f;
+      for (int i = 0; i < g.KBh; ++i) {
+        const int y2 = y1 + g.PTB - i;
+        if (y2 < t.d2a || y2 >= t.d2b) continue;
+        for (int j = 0; j < g.KBw; ++j) {
+          const int x2 = x1 + g.PLB - j;
+          if (x2 < 0 || x2 >= g.W2) continue;
+          const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2 + x2) * g.C2;
+          const float* wr = wB + ((i * g.KBw + j) * g.C1 + c1) * g.C2;
+#pragma unroll 4
+          for (int c2 = 0; c2 < g.C2; ++c2) acc = fmaf(dr[c2], wr[c2], acc);
+        }
+      }
+      if (a.actA) {                                        // post-activation c1 decides act'
+        const float v = s_c1[((y1 - t.c1a) * t.T1W + x1 + g.PLB) * g.C1 + c1];
+        acc = act_bwd(acc, v, v, a.actA, a.alphaA);
+      }
+      s_dc1[e] = acc;
+    }
+    if (a.hasBiasB && tid < g.C2) {
+      float acc = 0.f;
+      for (int y2 = t.o2a; y2 < t.o2b; ++y2) {
+        const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2) * g.C2 + tid;
+        for (int x2 = 0; x2 < g.W2; ++x2) acc += dr[x2 * g.C2];
+      }
+      atomicAdd(&a.dbB[(long)sidx * g.C2 + tid], acc);
+    }
+  }
+  __syncthreads();
+  CP_STAMP(12);
+  // ---- P4: conv-A weight gradient over the owned c1 pixels | conv-A bias gradient
+  {
+    const int npx = (t.o1b - t.o1a) * g.W1;
+    const int nA = KA * g.C1;
+    for (int o = tid; o < nA + (a.bA ? g.C1 : 0); o += CPV_T) {
+      float acc = 0.f;
+      if (o < nA) {
+        const int c1 = o % g.C1, k = o / g.C1, c0 = k % g.C0, ij = k / g.C0, i = ij / g.KAw, j = ij - i * g.KAw;
+        for (int p = 0; p < npx; ++p) {
+          const int y1 = t.o1a + p / g.W1, x1 = p % g.W1;
+          acc = fmaf(s_x[((y1 - g.PTA + i - t.xa) * t.TXW + x1 + g.PLB + j) * g.C0 + c0], s_dc1[p * g.C1 + c1], acc);
+        }
+        atomicAdd(&a.dwA[(long)sidx * nA + o], acc);
+      } else {
+        const int c1 = o - nA;
+        for (int p = 0; p < npx; ++p) acc += s_dc1[p * g.C1 + c1];
+        atomicAdd(&a.dbA[(long)sidx * g.C1 + c1], acc);
+      }
+    }
+  }
+  CP_STAMP(13);
+}
+
 static bool cpv_ok(const CPGeom& g) {
   if (getenv("CSA_CP_MFMA")) return false;               // force the MFMA family (A/B)
   if (g.C0 > 4 || g.C1 > CPV_MAXC1 || g.C2 > CPV_MAXC2) return false;
@@ -1000,6 +1283,27 @@ static bool cpv_ok(const CPGeom& g) {
   const int TXH = rows + g.KBh - 1 + g.KAh - 1;
   if (TXH * cpv_txw(g) * g.C0 > CPV_UX * CPV_T) return false;
   return true;
+}
+
+static bool cpv_bwd_ok(const CPBwdArgs& a) {
+  const CPGeom& g = a.g;
+  if (!cpv_ok(g)) return false;
+  if (a.bn_on && (a.bn.nslab > 32 || a.bwd_nslab > 16 ||
+                  (a.bn.nslab + a.bwd_nslab) * 2 * g.C2 > CPV_US * CPV_T)) return false;
+  for (int band = 0; band < g.nbands; ++band) {
+    const CPVBwdTile t = cpv_bwd_tile(g, band);
+    const int ow = g.pool ? g.PW : g.W2;
+    if ((t.ub - t.ua) * ow * g.C2 > CPV_UR * CPV_T) return false;
+    if (t.TXH * t.TXW * g.C0 > CPV_UX * CPV_T) return false;
+    if (cpv_bwd_lds(g, t).end * sizeof(float) > CP_LDS_MAX) return false;
+  }
+  return true;
+}
+
+static size_t cpv_bwd_lds_max(const CPGeom& g) {
+  size_t mx = 0;
+  for (int band = 0; band < g.nbands; ++band) mx = std::max(mx, (size_t)cpv_bwd_lds(g, cpv_bwd_tile(g, band)).end);
+  return mx * sizeof(float);
 }
 
 static size_t cpv_fwd_lds(const CPGeom& g) {
@@ -1128,6 +1432,13 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
   const dim3 grid((unsigned)(a.g.B * a.g.nbands));
+  if (cpv_bwd_ok(a)) {
+    static bool vattr = hipFuncSetAttribute((const void*)cpv_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)CP_LDS_MAX) == hipSuccess;
+    if (!vattr) return -3;
+    hipLaunchKernelGGL(cpv_bwd_kernel, grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
+    return (int)hipGetLastError();
+  }
   if (cp_bwd_one_batch(a))
     hipLaunchKernelGGL(conv_pair_bwd_kernel<true>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
   else
