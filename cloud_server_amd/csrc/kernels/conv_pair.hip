@@ -854,6 +854,7 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
 constexpr int CPV_T = 256;
 constexpr int CPV_MAXC1 = 16, CPV_MAXC2 = 32, CPV_MAXTAPS = 9;
 constexpr int CPV_UW = 8, CPV_UX = 2;                  // per-thread load batch (weights, x)
+constexpr int CPV_MAXKA = 16;                          // conv-A taps x C0 held in registers
 
 struct CPVFwdArgs {
   CPGeom g;
@@ -865,9 +866,11 @@ struct CPVFwdArgs {
 
 __host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 1 + g.KAw - 1; }
 
+template <int KBH, int KBW>
 __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
   const CPGeom& g = a.g;
   __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
+  __shared__ int s_koffA[CPV_MAXKA];                    // x-tile offset of conv-A tap k
   __shared__ float s_b[CPV_MAXC1 + CPV_MAXC2];
   __shared__ float s_x[CPV_UX * CPV_T];
   extern __shared__ __attribute__((aligned(16))) float smem[];   // c1 tile | unit outputs
@@ -876,17 +879,18 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
   const int r2a = g.pool ? 2 * pr0 : pr0, r2b = g.pool ? min(g.H2, 2 * pr1) : pr1;
   const CPBand t = cp_band(g, r2a, r2b);
   const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
-  const int nwA = KA * g.C1, nw = nwA + KB * g.C2, nb = g.C1 + g.C2;
+  const int nwA = KA * g.C1, nwA4 = (nwA + 3) & ~3, nw = nwA4 + KB * g.C2, nb = g.C1 + g.C2;
   const int nX = t.TXH * t.TXW * g.C0;
   const int tid = threadIdx.x;
   CP_STAMP(0);
   // ---- one batch of loads: weights + biases first, then the image rows (the staged
-  // image is at a fixed address; otherwise its row index chain runs under the weights)
+  // image is at a fixed address; otherwise its row index chain runs under the weights).
+  // LDS weights: [wA | pad to 4 | wB] (wB read as float2 / float4 rows)
   float wv[CPV_UW];
 #pragma unroll
   for (int u = 0; u < CPV_UW; ++u) {
     const int e = u * CPV_T + tid;
-    const float* p = e < nwA ? a.wA + e : (e < nw ? a.wB + (e - nwA) : a.wA);
+    const float* p = e < nwA ? a.wA + e : (e >= nwA4 && e < nw ? a.wB + (e - nwA4) : a.wA);
     wv[u] = *p;
   }
   float bv = 0.f;
@@ -916,61 +920,104 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
     const int e = u * CPV_T + tid;
     if (e < nX) s_x[e] = xok[u] ? (float)xv[u] * (1.0f / 255.0f) : 0.f;
   }
+  if (tid < KA) {
+    const int c0 = tid % g.C0, ij = tid / g.C0, i = ij / g.KAw, j = ij - i * g.KAw;
+    s_koffA[tid] = (i * t.TXW + j) * g.C0 + c0;
+  }
   __syncthreads();
   CP_STAMP(1);
-  // ---- conv A: the c1 tile [T1H][T1W][C1] (zero outside [0, H1) x [0, W1))
+  // ---- conv A: the c1 tile [T1H][T1W][C1] (zero outside [0, H1) x [0, W1)): one thread
+  // per tile pixel, its KA input values in registers, channel pairs as float2 weight reads
   float* s_c1 = smem;
-  const int n1 = t.T1H * t.T1W * g.C1;
-  for (int e = tid; e < n1; e += CPV_T) {
-    const int c1 = e % g.C1, pix = e / g.C1, tx = pix % t.T1W, ty = pix / t.T1W;
+  const int npx1 = t.T1H * t.T1W;
+  for (int pix = tid; pix < npx1; pix += CPV_T) {
+    const int tx = pix % t.T1W, ty = pix / t.T1W;
     const int yy = t.c1y0 + ty, xx = tx - g.PLB;
-    float v = 0.f;
-    if (yy >= 0 && yy < g.H1 && xx >= 0 && xx < g.W1) {
-      float acc = s_b[c1];
-      for (int i = 0; i < g.KAh; ++i)
-        for (int j = 0; j < g.KAw; ++j) {
-          const float* xr = s_x + ((ty + i) * t.TXW + tx + j) * g.C0;
-          const float* wr = s_w + ((i * g.KAw + j) * g.C0) * g.C1 + c1;
-          for (int c0 = 0; c0 < g.C0; ++c0) acc = fmaf(xr[c0], wr[c0 * g.C1], acc);
-        }
-      v = act_fwd(acc, a.actA, a.alphaA);
+    const bool in = yy >= 0 && yy < g.H1 && xx >= 0 && xx < g.W1;
+    const float* xb = s_x + (ty * t.TXW + tx) * g.C0;
+    float xk[CPV_MAXKA];
+#pragma unroll
+    for (int k = 0; k < CPV_MAXKA; ++k) xk[k] = k < KA ? xb[s_koffA[k]] : 0.f;
+    float* out = s_c1 + pix * g.C1;
+    for (int c1 = 0; c1 < g.C1; c1 += 2) {
+      float a0 = s_b[c1], a1 = s_b[c1 + 1];
+#pragma unroll
+      for (int k = 0; k < CPV_MAXKA; ++k) {
+        if (k >= KA) break;                               // uniform
+        const float2 w = *reinterpret_cast<const float2*>(s_w + k * g.C1 + c1);
+        a0 = fmaf(xk[k], w.x, a0);
+        a1 = fmaf(xk[k], w.y, a1);
+      }
+      *reinterpret_cast<float2*>(out + c1) =
+          in ? make_float2(act_fwd(a0, a.actA, a.alphaA), act_fwd(a1, a.actA, a.alphaA)) : make_float2(0.f, 0.f);
     }
-    s_c1[e] = v;
   }
   __syncthreads();
   CP_STAMP(2);
-  // ---- conv B (+ act B, + max-pool): one thread per (unit pixel, channel)
+  // ---- conv B (+ act B, + 2x2 max-pool): one thread per (unit pixel, channel pair).  Per
+  // input channel the pool window's c1 values (WR x WC) and the pair's KBH x KBW weights
+  // are loaded once and feed every (position, tap) FMA: 4 x taps x 2 FMAs per ~WR WC + taps loads
   const int ow = g.pool ? g.PW : g.W2;
   const int nunit = (g.pool ? (pr1 - pr0) : (r2b - r2a)) * ow;
   const int nout = nunit * g.C2;
-  float* s_out = s_c1 + ((n1 + 3) & ~3);                  // [nunit][C2] outputs for the stats
-  const float* wB = s_w + nwA;
-  const int npos = g.pool ? 4 : 1;
-  for (int o = tid; o < nout; o += CPV_T) {
-    const int c2 = o % g.C2, u = o / g.C2, py = u / ow, px = u - py * ow;
-    float best = -INFINITY;
-    int am = 0;
-    for (int pos = 0; pos < npos; ++pos) {
-      const int y2 = g.pool ? 2 * (pr0 + py) + (pos >> 1) : r2a + py;
-      const int x2 = g.pool ? 2 * px + (pos & 1) : px;
-      if (y2 >= g.H2 || x2 >= g.W2) continue;
-      float acc = s_b[g.C1 + c2];
-      for (int i = 0; i < g.KBh; ++i)
-        for (int j = 0; j < g.KBw; ++j) {
-          const float* cr = s_c1 + ((y2 - r2a + i) * t.T1W + x2 + j) * g.C1;
-          const float* wr = wB + ((i * g.KBw + j) * g.C1) * g.C2 + c2;
-#pragma unroll 4
-          for (int c1 = 0; c1 < g.C1; ++c1) acc = fmaf(cr[c1], wr[c1 * g.C2], acc);
-        }
-      const float v = act_fwd(acc, a.actB, a.alphaB);
-      if (v > best) { best = v; am = pos; }
+  float* s_out = s_c1 + ((npx1 * g.C1 + 3) & ~3);          // [nunit][C2] outputs for the stats
+  const float* wB = s_w + nwA4;
+  constexpr int WR = KBH + 1, WC = KBW + 1;                // pool window footprint in c1
+  const int ncp = g.C2 >> 1, npos = g.pool ? 4 : 1;
+  for (int o = tid; o < nunit * ncp; o += CPV_T) {
+    const int cp = o % ncp, u = o / ncp, py = u / ow, px = u - py * ow, c2 = 2 * cp;
+    const int y2b = g.pool ? 2 * (pr0 + py) : r2a + py, x2b = g.pool ? 2 * px : px;
+    float acc[4][2];
+    const float b0 = s_b[g.C1 + c2], b1 = s_b[g.C1 + c2 + 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { acc[q][0] = b0; acc[q][1] = b1; }
+    const float* cb = s_c1 + ((y2b - r2a) * t.T1W + x2b) * g.C1;
+    const bool wide = g.pool != 0;                           // window rows/cols beyond KBH x KBW
+    for (int c1 = 0; c1 < g.C1; ++c1) {
+      float cv[WR][WC];
+#pragma unroll
+      for (int r = 0; r < WR; ++r)
+#pragma unroll
+        for (int c = 0; c < WC; ++c)
+          cv[r][c] = (wide || (r < KBH && c < KBW)) ? cb[(r * t.T1W + c) * g.C1 + c1] : 0.f;
+      float2 wv[KBH * KBW];
+#pragma unroll
+      for (int k = 0; k < KBH * KBW; ++k)
+        wv[k] = *reinterpret_cast<const float2*>(wB + (k * g.C1 + c1) * g.C2 + c2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dy = q >> 1, dx = q & 1;
+#pragma unroll
+        for (int i = 0; i < KBH; ++i)
+#pragma unroll
+          for (int j = 0; j < KBW; ++j) {
+            acc[q][0] = fmaf(cv[dy + i][dx + j], wv[i * KBW + j].x, acc[q][0]);
+            acc[q][1] = fmaf(cv[dy + i][dx + j], wv[i * KBW + j].y, acc[q][1]);
+          }
+      }
     }
-    const long off = g.pool ? (((long)b * g.PH + pr0) * g.PW) * g.C2 + o
-                            : (((long)b * g.H2 + r2a) * g.W2) * g.C2 + o;
-    a.y[off] = best;
-    if (g.pool && a.argmax) a.argmax[off] = (uint8_t)am;
-    s_out[o] = best;
+    float best0 = -INFINITY, best1 = -INFINITY;
+    int am0 = 0, am1 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= npos) break;
+      const int y2 = y2b + (q >> 1), x2 = x2b + (q & 1);
+      if (y2 >= g.H2 || x2 >= g.W2) continue;
+      const float v0 = act_fwd(acc[q][0], a.actB, a.alphaB), v1 = act_fwd(acc[q][1], a.actB, a.alphaB);
+      if (v0 > best0) { best0 = v0; am0 = q; }
+      if (v1 > best1) { best1 = v1; am1 = q; }
+    }
+    const int oo = u * g.C2 + c2;
+    const long off = g.pool ? (((long)b * g.PH + pr0) * g.PW) * g.C2 + oo
+                            : (((long)b * g.H2 + r2a) * g.W2) * g.C2 + oo;
+    *reinterpret_cast<float2*>(a.y + off) = make_float2(best0, best1);
+    if (g.pool && a.argmax) {
+      a.argmax[off] = (uint8_t)am0;
+      a.argmax[off + 1] = (uint8_t)am1;
+    }
+    *reinterpret_cast<float2*>(s_out + oo) = make_float2(best0, best1);
   }
+  (void)nout;
   CP_STAMP(3);
   if (a.stat) {                                           // per-channel sums, fixed order
     __syncthreads();
@@ -1042,11 +1089,18 @@ __host__ __device__ inline CPVBwdLds cpv_bwd_lds(const CPGeom& g, const CPVBwdTi
   L.c1 = o; o += ((t.c1b - t.c1a) * t.T1W * g.C1 + 3) & ~3;
   L.dc2 = o; o += ((t.d2b - t.d2a) * g.W2 * g.C2 + 3) & ~3;
   L.dc1 = o; o += ((t.o1b - t.o1a) * g.W1 * g.C1 + 3) & ~3;
-  L.red = o; o += (32 + 16) * 2 * CPV_MAXC2;            // slab rows (fwd | bwd) staged for the fold
+  // slab rows (fwd | bwd) staged for the fold, later the weight-gradient slice partials
+  const int KB = g.KBh * g.KBw * g.C1, combos = g.C1 * (g.C2 / 2), nsl = combos > 0 ? (CPV_T / combos > 0 ? CPV_T / combos : 1) : 1;
+  const int partB = nsl * (KB * g.C2 + g.C2), partA = CPV_T * 2;
+  int red = (32 + 16) * 2 * CPV_MAXC2;
+  red = red > partB ? red : partB;
+  red = red > partA ? red : partA;
+  L.red = o; o += red;
   L.end = o;
   return L;
 }
 
+template <int KBH, int KBW>
 __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
   const CPGeom& g = a.g;
   __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
@@ -1063,7 +1117,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
   float* s_red = smem + L.red;
   const int tid = threadIdx.x;
   const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
-  const int nwA = KA * g.C1, nw = nwA + KB * g.C2;
+  const int nwA = KA * g.C1, nwA4 = (nwA + 3) & ~3, nw = nwA4 + KB * g.C2;
   const int C2x2 = 2 * g.C2;
   const int ow = g.pool ? g.PW : g.W2;
   const int nroute = (t.ub - t.ua) * ow * g.C2;
@@ -1076,7 +1130,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
 #pragma unroll
   for (int u = 0; u < CPV_UW; ++u) {
     const int e = u * CPV_T + tid;
-    wv[u] = *(e < nwA ? a.wA + e : (e < nw ? a.wB + (e - nwA) : a.wA));
+    wv[u] = *(e < nwA ? a.wA + e : (e >= nwA4 && e < nw ? a.wB + (e - nwA4) : a.wA));
   }
   const float bav = (a.bA && tid < g.C1) ? a.bA[tid] : 0.f;
   float rz[CPV_UR], ry[CPV_UR];
@@ -1196,77 +1250,121 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
   __syncthreads();
   CP_STAMP(11);
   const int sidx = blockIdx.x % a.stripes;
-  // ---- P3a: conv-B weight gradient over the owned conv-B pixels
+  float* s_part = s_red;                                   // slab staging is dead now: partials
+  // ---- P3a: conv-B weight (+ bias) gradient over the owned conv-B pixels.  Thread =
+  // (c1, channel pair, pixel slice): per pixel the c1 values of the KBH x KBW taps and the
+  // pair's dc2 (float2) feed taps x 2 FMAs; slices folded through LDS in fixed order.
   {
-    const int nB = KB * g.C2;
-    const float* wB = s_w + nwA;
-    (void)wB;
-    for (int o = tid; o < nB; o += CPV_T) {
-      const int c2 = o % g.C2, k = o / g.C2, c1 = k % g.C1, ij = k / g.C1, i = ij / g.KBw, j = ij - i * g.KBw;
-      float acc = 0.f;
-      for (int y2 = t.o2a; y2 < t.o2b; ++y2) {
-        const float* cr = s_c1 + ((y2 - g.PTB + i - t.c1a) * t.T1W + j) * g.C1 + c1;
-        const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2) * g.C2 + c2;
-#pragma unroll 4
-        for (int x2 = 0; x2 < g.W2; ++x2) acc = fmaf(cr[x2 * g.C1], dr[x2 * g.C2], acc);
+    const int ncp = g.C2 >> 1, combos = g.C1 * ncp, nsl = max(1, CPV_T / combos);
+    const int npx2 = (t.o2b - t.o2a) * g.W2;
+    const int nBw = KB * g.C2;
+    const int bias_off = nsl * nBw;                        // [nsl][C2] bias partials after the weights
+    if (tid < combos * nsl) {
+      const int cp = tid % ncp, c1 = (tid / ncp) % g.C1, sl = tid / combos, c2 = 2 * cp;
+      float acc[KBH * KBW][2], ab[2] = {0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KBH * KBW; ++k) { acc[k][0] = 0.f; acc[k][1] = 0.f; }
+      for (int p = sl; p < npx2; p += nsl) {
+        const int y2 = t.o2a + p / g.W2, x2 = p % g.W2;
+        const float2 d = *reinterpret_cast<const float2*>(s_dc2 + ((y2 - t.d2a) * g.W2 + x2) * g.C2 + c2);
+        const float* cr = s_c1 + ((y2 - g.PTB - t.c1a) * t.T1W + x2) * g.C1 + c1;
+        float cv[KBH * KBW];
+#pragma unroll
+        for (int i = 0; i < KBH; ++i)
+#pragma unroll
+          for (int j = 0; j < KBW; ++j) cv[i * KBW + j] = cr[(i * t.T1W + j) * g.C1];
+#pragma unroll
+        for (int k = 0; k < KBH * KBW; ++k) {
+          acc[k][0] = fmaf(cv[k], d.x, acc[k][0]);
+          acc[k][1] = fmaf(cv[k], d.y, acc[k][1]);
+        }
+        ab[0] += d.x;
+        ab[1] += d.y;
       }
-      atomicAdd(&a.dwB[(long)sidx * nB + o], acc);
+#pragma unroll
+      for (int k = 0; k < KBH * KBW; ++k)
+        *reinterpret_cast<float2*>(s_part + sl * nBw + (k * g.C1 + c1) * g.C2 + c2) = make_float2(acc[k][0], acc[k][1]);
+      if (c1 == 0) *reinterpret_cast<float2*>(s_part + bias_off + sl * g.C2 + c2) = make_float2(ab[0], ab[1]);
+    }
+    __syncthreads();
+    for (int o = tid; o < nBw + g.C2; o += CPV_T) {
+      float v = 0.f;
+      if (o < nBw) {
+        for (int q = 0; q < nsl; ++q) v += s_part[q * nBw + o];
+        atomicAdd(&a.dwB[(long)sidx * nBw + o], v);
+      } else if (a.hasBiasB) {
+        for (int q = 0; q < nsl; ++q) v += s_part[bias_off + q * g.C2 + o - nBw];
+        atomicAdd(&a.dbB[(long)sidx * g.C2 + o - nBw], v);
+      }
     }
   }
-  // ---- P3b: dc1 of the owned c1 pixels (through act A) | P3c: conv-B bias gradient
+  // ---- P3b: dc1 of the owned c1 pixels (through act A).  Thread = (pixel, c1 pair): per
+  // valid tap one float4 of dc2 and two float4 weight rows feed 8 FMAs.
   {
-    const float* wB = s_w + nwA;
-    const int nd = (t.o1b - t.o1a) * g.W1 * g.C1;
-    for (int e = tid; e < nd; e += CPV_T) {
-      const int c1 = e % g.C1, pix = e / g.C1, x1 = pix % g.W1, y1 = t.o1a + pix / g.W1;
-      float acc = 0.f;
-      for (int i = 0; i < g.KBh; ++i) {
+    const float* wB = s_w + nwA4;
+    const int npx1 = (t.o1b - t.o1a) * g.W1, nc1p = g.C1 >> 1;
+    for (int e = tid; e < npx1 * nc1p; e += CPV_T) {
+      const int c1 = 2 * (e % nc1p), pix = e / nc1p, x1 = pix % g.W1, y1 = t.o1a + pix / g.W1;
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < KBH; ++i) {
         const int y2 = y1 + g.PTB - i;
         if (y2 < t.d2a || y2 >= t.d2b) continue;
-        for (int j = 0; j < g.KBw; ++j) {
+#pragma unroll
+        for (int j = 0; j < KBW; ++j) {
           const int x2 = x1 + g.PLB - j;
           if (x2 < 0 || x2 >= g.W2) continue;
           const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2 + x2) * g.C2;
-          const float* wr = wB + ((i * g.KBw + j) * g.C1 + c1) * g.C2;
-#pragma unroll 4
-          for (int c2 = 0; c2 < g.C2; ++c2) acc = fmaf(dr[c2], wr[c2], acc);
+          const float* w0 = wB + ((i * KBW + j) * g.C1 + c1) * g.C2;
+          const float* w1 = w0 + g.C2;
+#pragma unroll 2
+          for (int c2 = 0; c2 < g.C2; c2 += 4) {
+            const float4 d = *reinterpret_cast<const float4*>(dr + c2);
+            const float4 u0 = *reinterpret_cast<const float4*>(w0 + c2);
+            const float4 u1 = *reinterpret_cast<const float4*>(w1 + c2);
+            a0 = fmaf(d.x, u0.x, a0); a0 = fmaf(d.y, u0.y, a0); a0 = fmaf(d.z, u0.z, a0); a0 = fmaf(d.w, u0.w, a0);
+            a1 = fmaf(d.x, u1.x, a1); a1 = fmaf(d.y, u1.y, a1); a1 = fmaf(d.z, u1.z, a1); a1 = fmaf(d.w, u1.w, a1);
+          }
         }
       }
       if (a.actA) {                                        // post-activation c1 decides act'
-        const float v = s_c1[((y1 - t.c1a) * t.T1W + x1 + g.PLB) * g.C1 + c1];
-        acc = act_bwd(acc, v, v, a.actA, a.alphaA);
+        const float* cv = s_c1 + ((y1 - t.c1a) * t.T1W + x1 + g.PLB) * g.C1 + c1;
+        a0 = act_bwd(a0, cv[0], cv[0], a.actA, a.alphaA);
+        a1 = act_bwd(a1, cv[1], cv[1], a.actA, a.alphaA);
       }
-      s_dc1[e] = acc;
-    }
-    if (a.hasBiasB && tid < g.C2) {
-      float acc = 0.f;
-      for (int y2 = t.o2a; y2 < t.o2b; ++y2) {
-        const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2) * g.C2 + tid;
-        for (int x2 = 0; x2 < g.W2; ++x2) acc += dr[x2 * g.C2];
-      }
-      atomicAdd(&a.dbB[(long)sidx * g.C2 + tid], acc);
+      *reinterpret_cast<float2*>(s_dc1 + pix * g.C1 + c1) = make_float2(a0, a1);
     }
   }
   __syncthreads();
   CP_STAMP(12);
-  // ---- P4: conv-A weight gradient over the owned c1 pixels | conv-A bias gradient
+  // ---- P4: conv-A weight / bias gradients over the owned c1 pixels.  Thread = (tap or the
+  // bias row, c1 pair, pixel slice); slices folded through LDS in fixed order.
   {
-    const int npx = (t.o1b - t.o1a) * g.W1;
-    const int nA = KA * g.C1;
-    for (int o = tid; o < nA + (a.bA ? g.C1 : 0); o += CPV_T) {
-      float acc = 0.f;
-      if (o < nA) {
-        const int c1 = o % g.C1, k = o / g.C1, c0 = k % g.C0, ij = k / g.C0, i = ij / g.KAw, j = ij - i * g.KAw;
-        for (int p = 0; p < npx; ++p) {
-          const int y1 = t.o1a + p / g.W1, x1 = p % g.W1;
-          acc = fmaf(s_x[((y1 - g.PTA + i - t.xa) * t.TXW + x1 + g.PLB + j) * g.C0 + c0], s_dc1[p * g.C1 + c1], acc);
-        }
-        atomicAdd(&a.dwA[(long)sidx * nA + o], acc);
-      } else {
-        const int c1 = o - nA;
-        for (int p = 0; p < npx; ++p) acc += s_dc1[p * g.C1 + c1];
-        atomicAdd(&a.dbA[(long)sidx * g.C1 + c1], acc);
+    const int npx = (t.o1b - t.o1a) * g.W1, nc1p = g.C1 >> 1;
+    const int rows = KA + (a.bA ? 1 : 0), combos = rows * nc1p, nsl = max(1, CPV_T / combos);
+    if (tid < combos * nsl) {
+      const int cp = tid % nc1p, k = (tid / nc1p) % rows, sl = tid / combos, c1 = 2 * cp;
+      int koff = 0;
+      if (k < KA) {
+        const int c0 = k % g.C0, ij = k / g.C0, i = ij / g.KAw, j = ij - i * g.KAw;
+        koff = (i * t.TXW + j) * g.C0 + c0;
       }
+      float a0 = 0.f, a1 = 0.f;
+      for (int p = sl; p < npx; p += nsl) {
+        const int y1 = t.o1a + p / g.W1, x1 = p % g.W1;
+        const float xv2 = k < KA ? s_x[((y1 - g.PTA - t.xa) * t.TXW + x1 + g.PLB) * g.C0 + koff] : 1.f;
+        const float2 d = *reinterpret_cast<const float2*>(s_dc1 + p * g.C1 + c1);
+        a0 = fmaf(xv2, d.x, a0);
+        a1 = fmaf(xv2, d.y, a1);
+      }
+      *reinterpret_cast<float2*>(s_part + (sl * rows + k) * g.C1 + c1) = make_float2(a0, a1);
+    }
+    __syncthreads();
+    for (int o = tid; o < rows * g.C1; o += CPV_T) {
+      float v = 0.f;
+      for (int q = 0; q < nsl; ++q) v += s_part[q * rows * g.C1 + o];
+      if (o < KA * g.C1) atomicAdd(&a.dwA[(long)sidx * KA * g.C1 + o], v);
+      else atomicAdd(&a.dbA[(long)sidx * g.C1 + o - KA * g.C1], v);
     }
   }
   CP_STAMP(13);
@@ -1275,10 +1373,11 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
 static bool cpv_ok(const CPGeom& g) {
   if (getenv("CSA_CP_MFMA")) return false;               // force the MFMA family (A/B)
   if (g.C0 > 4 || g.C1 > CPV_MAXC1 || g.C2 > CPV_MAXC2) return false;
-  if (g.KAh * g.KAw > CPV_MAXTAPS || g.KBh * g.KBw > CPV_MAXTAPS) return false;
+  if (g.KAh * g.KAw * g.C0 > CPV_MAXKA || g.C1 % 2 || g.C2 % 2) return false;
+  if (!((g.KBh == 2 && g.KBw == 2) || (g.KBh == 3 && g.KBw == 3))) return false;   // instantiated
   if (g.pool && (g.PH * 2 > g.H2 + 1 || g.PW * 2 > g.W2 + 1)) return false;
   const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
-  if (KA * g.C1 + KB * g.C2 > CPV_UW * CPV_T) return false;
+  if (((KA * g.C1 + 3) & ~3) + KB * g.C2 > CPV_UW * CPV_T) return false;
   const int rows = g.pool ? 2 * g.PR : g.PR;
   const int TXH = rows + g.KBh - 1 + g.KAh - 1;
   if (TXH * cpv_txw(g) * g.C0 > CPV_UX * CPV_T) return false;
@@ -1400,7 +1499,8 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
   a.nslab = nslab < 1 ? 1 : nslab;
   if (cpv_ok(a.g)) {
     CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab};
-    hipLaunchKernelGGL(cpv_fwd_kernel, dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
+    if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
+    else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
     return (int)hipGetLastError();
   }
   static bool attr = hipFuncSetAttribute((const void*)conv_pair_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1433,10 +1533,13 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
   if (!attr) return -3;
   const dim3 grid((unsigned)(a.g.B * a.g.nbands));
   if (cpv_bwd_ok(a)) {
-    static bool vattr = hipFuncSetAttribute((const void*)cpv_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    static bool vattr = hipFuncSetAttribute((const void*)cpv_bwd_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)CP_LDS_MAX) == hipSuccess &&
+                        hipFuncSetAttribute((const void*)cpv_bwd_kernel<3, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)CP_LDS_MAX) == hipSuccess;
     if (!vattr) return -3;
-    hipLaunchKernelGGL(cpv_bwd_kernel, grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
+    if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_bwd_kernel<2, 2>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
+    else hipLaunchKernelGGL((cpv_bwd_kernel<3, 3>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
     return (int)hipGetLastError();
   }
   if (cp_bwd_one_batch(a))

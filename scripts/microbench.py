@@ -147,8 +147,11 @@ def main() -> int:
                     eng.program.lib.csa_cp_debug(None)
                 t = dbg.tolist()
                 if name.endswith("fwd"):
-                    print(f"{i:2d} {name}: stage {t[1]-t[0]} (image {t[5]-t[0]} panels {t[6]-t[5]} tables {t[1]-t[6]}) "
-                          f"convA {t[2]-t[1]} convB+pool {t[3]-t[2]} stats {t[4]-t[3]}")
+                    print(f"{i:2d} {name}: stage {t[1]-t[0]} convA {t[2]-t[1]} convB+pool {t[3]-t[2]} "
+                          f"stats {t[4]-t[3]} (s_memtime ticks)")
+                elif t[14] == 0:      # VALU backward (cpv_bwd_kernel)
+                    print(f"{i:2d} {name}: loads {t[9]-t[8]} bn+c1 {t[10]-t[9]} route {t[11]-t[10]} "
+                          f"dwB+dc1 {t[12]-t[11]} dwA {t[13]-t[12]} (s_memtime ticks)")
                 else:
                     print(f"{i:2d} {name}: stage+bn {t[9]-t[8]} (loads {t[16]-t[8]} tables {t[17]-t[16]} "
                           f"stores {t[18]-t[17]} bn {t[9]-t[19]}) route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} "
