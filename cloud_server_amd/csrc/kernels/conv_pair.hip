@@ -862,6 +862,10 @@ struct CPVFwdArgs {
   const float* wA; const float* bA; int actA; float alphaA;
   const float* wB; const float* bB; int actB; float alphaB;
   float* y; uint8_t* argmax; float* stat; int nslab;
+  // BatchNorm table of the output (tab != null): the LAST workgroup to finish folds the
+  // statistic rows into [mean | rstd | a | b][C2] (a = scale * rstd, b = offset - mean a),
+  // so the consumers (the next dense layer's forward / backward) read 4 C2 floats
+  float* tab; unsigned* cnt; const float* bn_scale; const float* bn_offset; float bn_count, bn_eps;
 };
 
 __host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 1 + g.KAw - 1; }
@@ -1029,8 +1033,38 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
         acc += sq ? v * v : v;
       }
       float* row = a.stat + (size_t)(blockIdx.x % a.nslab) * 2 * g.C2;
-      if (a.nslab >= (int)gridDim.x) row[tid] = acc;     // one row per workgroup: plain store
+      if (a.nslab >= (int)gridDim.x && !a.tab) row[tid] = acc;   // one row per workgroup
       else atomicAdd(&row[tid], acc);
+    }
+  }
+  if (a.stat && a.tab) {
+    // last-arriver fold: the row atomics are device-scope (performed beyond every L2) and
+    // complete before the ticket (vmcnt drained); the last workgroup reads the rows with
+    // L1-bypassing agent loads — no L2 of its XCD ever held them during this launch
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == gridDim.x - 1;
+      if (s_last) __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+    }
+    __syncthreads();
+    if (s_last && tid < g.C2) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: loads stay below
+      float s1 = 0.f, s2 = 0.f;
+      for (int r = 0; r < a.nslab; ++r) {                   // rows in fixed order
+        s1 += __hip_atomic_load(a.stat + (size_t)r * 2 * g.C2 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s2 += __hip_atomic_load(a.stat + (size_t)r * 2 * g.C2 + g.C2 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const float mean = s1 / a.bn_count;
+      const float var = fmaxf(s2 / a.bn_count - mean * mean, 0.f);
+      const float rstd = rsqrtf(var + a.bn_eps);
+      const float sa = a.bn_scale[tid] * rstd;
+      a.tab[tid] = mean;
+      a.tab[g.C2 + tid] = rstd;
+      a.tab[2 * g.C2 + tid] = sa;
+      a.tab[3 * g.C2 + tid] = a.bn_offset[tid] - mean * sa;
     }
   }
   CP_STAMP(4);
@@ -1488,17 +1522,41 @@ CSA_API int csa_conv_pair_ok(const int* geom) {
   return cp_lds(g, true) <= CP_LDS_MAX ? 1 : 0;
 }
 
+CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
+                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
+                               int nslab, float* tab, unsigned* cnt, const float* bn_scale, const float* bn_offset,
+                               float bn_count, float bn_eps, hipStream_t st);
+
+// Is the VALU pair family (cpv kernels, BN table by the last workgroup) in use for geom?
+CSA_API int csa_conv_pair_tab_ok(const int* geom) {
+  CPGeom g;
+  return cp_geom(geom, g) && cpv_ok(g) ? 1 : 0;
+}
+
 CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
                               int nslab, hipStream_t st) {
+  return csa_conv_pair_fwd2(geom, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, nslab,
+                            nullptr, nullptr, nullptr, nullptr, 1.f, 0.f, st);
+}
+
+// ... + (tab != null, VALU family only) the BatchNorm table of the output, see CPVFwdArgs.
+CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
+                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
+                               int nslab, float* tab, unsigned* cnt, const float* bn_scale, const float* bn_offset,
+                               float bn_count, float bn_eps, hipStream_t st) {
   CPFwdArgs a{};
   if (!cp_geom(geom, a.g) || cp_lds(a.g, false) > CP_LDS_MAX) return -1;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.bB = bB; a.actB = actB; a.alphaB = alphaB; a.y = y; a.argmax = argmax; a.stat = stat;
   a.nslab = nslab < 1 ? 1 : nslab;
+  if (tab && (!stat || !cnt || !bn_scale || !bn_offset || !cpv_ok(a.g))) return -2;
   if (cpv_ok(a.g)) {
-    CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab};
+    CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab,
+                 tab, cnt, bn_scale, bn_offset, bn_count, bn_eps};
     if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
     else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
     return (int)hipGetLastError();

@@ -108,6 +108,7 @@ struct DDFwd {
   int M, N, K, act; float alpha; int ksplit, kper;   // kper: K per workgroup (multiple of 8)
   BNRef bn;          // bn.slab != null: A = act(x * a[c] + b[c]), c = k % C (tables from the slab)
   float* xt;         // != null (with bn): the N-tile-0 workgroups store the transformed A
+  const float* tab;  // != null (with bn): precomputed [mean | rstd | a | b][C] instead of the slab
 };
 
 constexpr int DD_KEEP = 2;       // transformed-input blocks a lane holds until after the K loop
@@ -167,7 +168,14 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
   float4 kx[DD_KEEP], ky[DD_KEEP];
   int kk_[DD_KEEP], nkeep = 0;
   load(ka);                        // the first group's loads overlap the BN-table reduction
-  if (BN) bn_reduce_to_lds(a.bn, s_bn, s_bn + DD_MAXC, s_bn + 2 * DD_MAXC, s_bn + 3 * DD_MAXC, s_bn + 4 * DD_MAXC);
+  if (BN && a.tab) {
+    for (int c = threadIdx.x; c < a.bn.C; c += DD_THREADS) {
+      s_bn[2 * DD_MAXC + c] = a.tab[2 * a.bn.C + c];
+      s_bn[3 * DD_MAXC + c] = a.tab[3 * a.bn.C + c];
+    }
+  } else if (BN) {
+    bn_reduce_to_lds(a.bn, s_bn, s_bn + DD_MAXC, s_bn + 2 * DD_MAXC, s_bn + 3 * DD_MAXC, s_bn + 4 * DD_MAXC);
+  }
   if (BN) __syncthreads();
   dd_f32x16 acc0 = {}, acc1 = {};
   for (int k = ka; k < kb; k += 8 * DD_U) {
@@ -540,9 +548,24 @@ CSA_API int csa_dd_fwd(const float* X, const float* W, const float* bias, float*
 
 // ... with the forward input transform act(bn(x)) applied while loading (C <= 128, K % 4
 // == 0); xt (optional) receives the transformed input [M][K].
+CSA_API int csa_dd_fwd_bn2(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
+                           int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
+                           float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, const float* tab,
+                           hipStream_t st);
+
 CSA_API int csa_dd_fwd_bn(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
                           int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
                           float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, hipStream_t st) {
+  return csa_dd_fwd_bn2(X, W, bias, Y, M, N, K, act, alpha, bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale,
+                        bn_offset, xt, nullptr, st);
+}
+
+// ... tab != null: the BatchNorm table [mean | rstd | a | b][C] was precomputed by the
+// producer (the conv pair's last workgroup): no slab reduction in any workgroup.
+CSA_API int csa_dd_fwd_bn2(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
+                           int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
+                           float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, const float* tab,
+                           hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (bn_slab && (bn_C <= 0 || bn_C > DD_MAXC || K % 4)) return -1;
   const int nt = (N + 31) / 32, mb = (M + 63) / 64;
@@ -550,7 +573,7 @@ CSA_API int csa_dd_fwd_bn(const float* X, const float* W, const float* bias, flo
   const int kper = dd_kper(K, ks);
   ks = (K + kper - 1) / kper;
   DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper,
-          BNRef{bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset}, xt};
+          BNRef{bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset}, xt, bn_slab ? tab : nullptr};
   if (bn_slab) hipLaunchKernelGGL((dd_fwd_kernel<true, true>), dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
   else if (K % 4 == 0) hipLaunchKernelGGL((dd_fwd_kernel<true, false>), dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
   else hipLaunchKernelGGL((dd_fwd_kernel<false, false>), dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);

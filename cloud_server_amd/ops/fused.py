@@ -69,6 +69,8 @@ _SIGS = {
     "csa_cp_debug": (I, [P]),
     "csa_head_debug": (I, [P]),
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P]),
+    "csa_conv_pair_fwd2": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P, P, P, P, F, F, P]),
+    "csa_conv_pair_tab_ok": (I, [P]),
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
                               P, P, P, P, I, P]),
     "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),
@@ -83,6 +85,7 @@ _SIGS = {
     "csa_dd_fwd_splits": (I, [I, I, I]),
     "csa_dd_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
     "csa_dd_fwd_bn": (I, [P, P, P, P, I, I, I, I, F, P, I, I, F, F, P, P, P, P]),
+    "csa_dd_fwd_bn2": (I, [P, P, P, P, I, I, I, I, F, P, I, I, F, F, P, P, P, P, P]),
     "csa_dd_dgrad_splits": (I, [I, I, I]),
     "csa_dd_dgrad_slabs": (I, []),
     "csa_dd_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P]),

@@ -576,6 +576,16 @@ class HipProgram:
             u.in_tf.bn_tab = (torch.zeros(4, u.in_tf.slab.shape[2], **f32)
                               if u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") != "1"
                               else None)
+        # the conv pair's last workgroup folds the following BatchNorm's statistics into the
+        # consumer's [mean | rstd | a | b] table (VALU pair family; csa_conv_pair_fwd2), and
+        # a register-direct dense consumer applies it while loading: no bn_act_apply launch
+        self.pair_cnt = None
+        if (self.pair is not None and len(self.units) > 2 and self.units[2].in_tf.has_bn
+                and getattr(self.units[2].in_tf, "bn_tab", None) is not None and not self.sync_bn
+                and os.environ.get("CSA_PAIR_BN_TAB", "1") == "1" and self.lib.csa_conv_pair_tab_ok(K.ints(self.pair))):
+            nt = self.units[2].in_tf
+            nt.pair_tab = nt.bn_tab
+            self.pair_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         self.dlast = self.units[-1].dy     # head input grad (None: forward only)
         if getattr(self, "head_row", False):
             self.hdl = torch.zeros(B, 10, **f32)                            # dlogits rows
@@ -996,13 +1006,18 @@ class HipProgram:
             nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
             oslab = nt.slab if nt.has_bn and not self._eval_bn else None
             simg, srows, scur = self._batch_src()
-            self._rc(lib.csa_conv_pair_fwd(
+            # the pair's last workgroup folds the BN statistics into the consumer's table
+            tab = getattr(nt, "pair_tab", None) if oslab is not None and not self.sync_bn else None
+            bn = (K.ptr(self.views[f"{nt.norm.name}.scale"]), K.ptr(self.views[f"{nt.norm.name}.offset"]),
+                  float(nt.count), float(nt.norm.spec.epsilon)) if tab is not None else (None, None, 1.0, 0.0)
+            self._rc(lib.csa_conv_pair_fwd2(
                 K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
                 K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
                 _act_id(ua.act), _alpha(ua.act),
                 K.ptr(V[f"{ub.layer.name}.weight"]), K.ptr(V.get(f"{ub.layer.name}.bias")) if ub.layer.spec.bias else None,
                 _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
-                self.lib.csa_conv_fwd_nslab(None, None), st), "conv_pair_fwd")
+                self.lib.csa_conv_fwd_nslab(None, None), K.ptr(tab), K.ptr(self.pair_cnt) if tab is not None else None,
+                *bn, st), "conv_pair_fwd")
             if oslab is not None and self.sync_bn:
                 e.sync.allreduce_tensors([oslab], tag="bnf1")
         for k, u in enumerate(self.units):
@@ -1037,6 +1052,15 @@ class HipProgram:
                         K.ptr(u.x.view(B, -1)), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
                         K.ptr(u.y), B, fout, fin, in_act, in_alpha, *self._bn_args_c(tf), K.ptr(u.xt), st),
                         "dd_fwd_bn")
+                    continue
+                if (u.direct and u.xt is not None and getattr(tf, "pair_tab", None) is not None
+                        and not self._eval_bn and not self.sync_bn):
+                    # BN + act applied while the GEMM loads its input, from the table the conv
+                    # pair's last workgroup wrote; the N tiles write xt (the backward's operand)
+                    self._rc(lib.csa_dd_fwd_bn2(
+                        K.ptr(u.x.view(B, -1)), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
+                        K.ptr(u.y), B, fout, fin, in_act, in_alpha, *self._bn_args_c(tf), K.ptr(u.xt),
+                        K.ptr(tf.pair_tab), st), "dd_fwd_bn(tab)")
                     continue
                 if u.xt is not None:
                     self._rc(lib.csa_bn_act_apply(
