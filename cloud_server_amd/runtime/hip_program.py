@@ -42,6 +42,7 @@ import torch
 
 from ..models.dsl import ActSpec, ConvSpec, DenseSpec, LayerPlan, NormSpec, PoolSpec
 from ..ops import fused as K
+from ..ops import fused as _FK      # (K is shadowed by feature counts inside _alloc)
 from ..ops import optim_ref
 
 
@@ -582,7 +583,7 @@ class HipProgram:
         self.pair_cnt = None
         if (self.pair is not None and len(self.units) > 2 and self.units[2].in_tf.has_bn
                 and getattr(self.units[2].in_tf, "bn_tab", None) is not None and not self.sync_bn
-                and os.environ.get("CSA_PAIR_BN_TAB", "1") == "1" and self.lib.csa_conv_pair_tab_ok(K.ints(self.pair))):
+                and os.environ.get("CSA_PAIR_BN_TAB", "1") == "1" and self.lib.csa_conv_pair_tab_ok(_FK.ints(self.pair))):
             nt = self.units[2].in_tf
             nt.pair_tab = nt.bn_tab
             self.pair_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
