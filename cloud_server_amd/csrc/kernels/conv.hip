@@ -965,20 +965,6 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_bwd_pair_kernel(ConvDgradAr
   else conv_wgrad_body<false>(w, blockIdx.x - nd, smem, s_bn);
 }
 
-// The same pair with the unit's route backward (BN backward + act backward + pool
-// routing) fused into both bodies' dc staging — one launch fewer per conv unit.
-__global__ __launch_bounds__(CONV_THREADS) void conv_bwd_route_pair_kernel(ConvDgradArgs d, ConvWgradArgs w,
-                                                                           int nd, RouteArgs r) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float s_bn[4 * 128 + 2 * 128];
-  __shared__ float s_stat[2 * 128];
-  __shared__ float s_rbn[4 * 128];
-  __shared__ float s_rss[2 * 128];
-  const RouteTables t{s_rbn, s_rss};
-  route_prologue(r, t, blockIdx.x);
-  if ((int)blockIdx.x < nd) conv_dgrad_body<CB_T>(d, blockIdx.x, smem, s_bn, s_stat, &r, t);
-  else conv_wgrad_body<false>(w, blockIdx.x - nd, smem, s_bn, &r, t);
-}
 
 static void fwd_bands(const ConvGeom& g, const PoolGeom& p, int& nbands, int& rows, int& rows_in) {
   const int out_rows = p.on ? p.OH : g.OH, out_w = p.on ? p.OW : g.OW;
@@ -1255,46 +1241,6 @@ static RouteArgs route_args(const float* dz, const float* y, const uint8_t* argm
   a.bn_on = bn_slab != nullptr;
   a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab; a.dscale = dscale; a.doffset = doffset;
   return a;
-}
-
-// Conv unit backward in ONE launch with the unit's route fused (see
-// conv_bwd_route_pair_kernel).  Returns 1 when launched, 0 when the route shape is outside
-// the fused family (overlapping or padded pool: the caller runs csa_route_bwd +
-// csa_conv_bwd), < 0 on error.
-CSA_API int csa_conv_bwd_route(const float* w, float* dx, const int* geom, const float* x_fwd, int in_act,
-                               float in_alpha, const float* bn_slab, int bn_nslab, float bn_count, float bn_eps,
-                               const float* bn_scale, const float* bn_offset, float* bwd_slab, float* dW,
-                               float* db, int stripes, const float* dz, const float* y, const uint8_t* argmax,
-                               const int* rg, int out_act, float out_alpha, const float* r_bn_slab,
-                               int r_bn_nslab, float r_bn_count, float r_bn_eps, const float* r_bn_scale,
-                               const float* r_bn_offset, const float* r_bwd_slab, int r_bwd_nslab,
-                               float* dscale, float* doffset, float* run_mean, float* run_var, float momentum,
-                               hipStream_t st) {
-  RouteArgs r = route_args(dz, y, argmax, nullptr, rg, out_act, out_alpha, r_bn_slab, r_bn_nslab, r_bn_count,
-                           r_bn_eps, r_bn_scale, r_bn_offset, r_bwd_slab, r_bwd_nslab, dscale, doffset,
-                           run_mean, run_var, momentum);
-  if (r.C > 128) return -1;
-  if (r.pool_on && (r.overlap || r.PPT != 0 || r.PPL != 0)) return 0;
-  ConvDgradArgs d;
-  ConvWgradArgs wg;
-  size_t shm_d, shm_w;
-  int rc = dgrad_args(nullptr, w, dx, geom, x_fwd, in_act, in_alpha, bn_slab, bn_nslab, bn_count, bn_eps,
-                      bn_scale, bn_offset, bwd_slab, d, shm_d);
-  if (rc) return rc;
-  const ConvGeom& g = d.g;
-  if (g.Cout != r.C || g.OH != r.OH || g.OW != r.OW) return -4;
-  rc = wgrad_args(x_fwd, nullptr, nullptr, nullptr, dW, db, stripes, g.B, g.H, g.W, g.Cin, g.KH, g.KW, g.SH, g.SW,
-                  g.PT, g.PL, g.OH, g.OW, g.Cout, bn_slab, bn_nslab, bn_count, bn_eps, bn_scale, bn_offset,
-                  in_act, in_alpha, nullptr, wg, shm_w);
-  if (rc) return rc;
-  static bool attr = set_lds_attr((const void*)conv_bwd_route_pair_kernel);
-  (void)attr;
-  const int nd = g.B * d.nbands;
-  dim3 grid((unsigned)(nd + g.B * wg.nbands));
-  hipLaunchKernelGGL(conv_bwd_route_pair_kernel, grid, dim3(CONV_THREADS), std::max(shm_d, shm_w), st, d, wg,
-                     nd, r);
-  const int e = (int)hipGetLastError();
-  return e ? -e : 1;
 }
 
 // Conv unit backward in ONE launch: input gradient (as csa_conv_dgrad) + weight gradient

@@ -317,158 +317,6 @@ __global__ __launch_bounds__(RT) void head_rows_kernel(HeadArgs a, int* ws) {
 }
 
 // ---------------------------------------------------------------------------------
-// Column-slice head (opt-in, CSA_HEAD_COLS=1; M <= 64, K % 16 == 0): ceil(K/16) workgroups.
-// Each computes the FULL logits T(h)·Wh (50x512x10 for the sample: 0.5 MFLOP of MFMA,
-// redundant per workgroup but cheaper than any cross-workgroup hand-off), the loss /
-// dlogits / #correct of every row, and then only ITS 16-column slice of
-// dWh = T(h)ᵀ·dl and dh = dl·Whᵀ ⊙ T'(h).  Every output has exactly one writer: plain
-// stores, no atomics, no arrival counter (the row-group kernel below spent most of its
-// 14.5 µs in ~20k same-line dWh atomics and its last-arriver hand-off).  Workgroup 0
-// writes dbh, the metric ring and the step counter.
-// T(h) reaches the MFMA straight from global memory: the K reduction is re-ordered so
-// that lane (r, q) of the 16x16x4 A operand owns k in [q*K/4, (q+1)*K/4) — contiguous
-// float4 loads — and the B operand (Wh, staged in LDS) follows the same order.
-// ---------------------------------------------------------------------------------
-constexpr int HCS = 16;           // K columns per workgroup
-
-__global__ __launch_bounds__(RT) void head_cols_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int M = a.M, K = a.K, KQ = K >> 2;
-  float* s_w = smem;                       // [K][10]
-  float* s_log = s_w + K * NCLS;           // [64][16] logits -> dlogits (rows >= M: 0)
-  float* s_hs = s_log + 64 * 16;           // [64][HCS] T(h) of this block's columns
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t* idx = a.cursor ? a.idx + a.cursor[0] * M : a.idx;
-  const int c0 = blockIdx.x * HCS;
-  const int act = a.in_act;
-  const float alpha = a.in_alpha;
-  const int my_label = tid < M ? (int)a.labels[idx[tid]] : 0;
-  // this lane's whole K quarter of its T(h) row (<= 128 floats) is loaded up front, so
-  // its round trip overlaps the Wh staging below (one wave per SIMD: VGPRs are free)
-  const int r = lane & 15, q = lane >> 4;
-  const int m_a = wave * 16 + r;
-  const bool okm = m_a < M;
-  const float* hrow = a.h + (long)(okm ? m_a : 0) * K + q * KQ;
-  float4 hv[32];
-#pragma unroll
-  for (int u = 0; u < 32; ++u) hv[u] = *reinterpret_cast<const float4*>(hrow + min(4 * u, KQ - 4));
-  {  // stage Wh and this block's T(h) columns
-    const int nw4 = (K * NCLS) >> 2;
-    const float4* w4 = reinterpret_cast<const float4*>(a.w);
-    for (int i = tid; i < nw4; i += RT) reinterpret_cast<float4*>(s_w)[i] = w4[i];
-    for (int e = tid; e < 64 * HCS; e += RT) {
-      const int m = e / HCS, k = c0 + (e % HCS);
-      const bool ok = m < M && k < K;
-      const float v = a.h[ok ? (long)m * K + k : 0];
-      s_hs[e] = ok ? act_fwd(v, act, alpha) : 0.f;
-    }
-  }
-  __syncthreads();
-  {  // logits: wave w owns rows 16w..16w+15; lane (r, q): row r, K quarter q
-    const float* wq = s_w + (long)q * KQ * NCLS + (r < NCLS ? r : 0);
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      if (4 * u >= KQ) break;                       // uniform: KQ % 4 == 0
-      const float e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int kk = 4 * u + t;
-        const float hvt = okm ? act_fwd(e4[t], act, alpha) : 0.f;
-        const float wv = r < NCLS ? wq[kk * NCLS] : 0.f;
-        if (t & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hvt, wv, acc1, 0, 0, 0);
-        else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hvt, wv, acc0, 0, 0, 0);
-      }
-    }
-    // D: lane (r, q) holds rows 4q..4q+3 (of the wave's 16) of column r
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s_log[(wave * 16 + 4 * q + i) * 16 + r] = acc0[i] + acc1[i];
-  }
-  __syncthreads();
-  // ---- loss / dlogits / #correct, one lane per row (all rows in wave 0) ----
-  float lsum = 0.f;
-  int cor = 0;
-  if (tid < 64) {
-    float* row = s_log + tid * 16;
-    if (tid < M) {
-      const int y = my_label;
-#pragma unroll
-      for (int j = 0; j < NCLS; ++j) row[j] += a.b[j];
-      float mx = row[0];
-      int am = 0;
-#pragma unroll
-      for (int j = 1; j < NCLS; ++j)
-        if (row[j] > mx) { mx = row[j]; am = j; }
-      cor = (am == y);
-      if (a.logits_out && blockIdx.x == 0) {
-#pragma unroll
-        for (int j = 0; j < NCLS; ++j) a.logits_out[(long)tid * NCLS + j] = row[j];
-      }
-      if (a.loss == 0) {
-        float se = 0.f;
-#pragma unroll
-        for (int j = 0; j < NCLS; ++j) se += __expf(row[j] - mx);
-        const float lse = mx + __logf(se);
-        lsum = lse - row[y];
-        const float inv = a.grad_scale / (float)M;
-#pragma unroll
-        for (int j = 0; j < NCLS; ++j) row[j] = (__expf(row[j] - lse) - (j == y ? 1.f : 0.f)) * inv;
-      } else {
-        const float inv = 2.f * a.grad_scale / (float)(M * NCLS);
-#pragma unroll
-        for (int j = 0; j < NCLS; ++j) {
-          const float d = row[j] - (j == y ? 1.f : 0.f);
-          lsum += d * d;
-          row[j] = d * inv;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NCLS; ++j) row[j] = 0.f;
-    }
-  }
-  if (wave == 0 && blockIdx.x == 0) {
-    lsum = wave_sum(lsum);
-    const unsigned long long ball = __ballot(cor != 0);
-    if (lane == 0) {
-      const int64_t st = *a.step;
-      const int pos = (int)(st % a.ring);
-      a.ring_loss[pos] = (a.loss == 0) ? lsum / M : lsum / (M * NCLS);
-      a.ring_correct[pos] = __popcll(ball);
-      *a.step = st + 1;
-    }
-  }
-  __syncthreads();
-  // ---- this block's slice of dWh and dh; dbh by block 0 ----
-  for (int e = tid; e < HCS * NCLS; e += RT) {
-    const int kk = e / NCLS, j = e - kk * NCLS, k = c0 + kk;
-    if (k >= K) continue;
-    float acc = 0.f;
-    for (int m = 0; m < M; ++m) acc = fmaf(s_hs[m * HCS + kk], s_log[m * 16 + j], acc);
-    a.dw[(long)k * NCLS + j] = acc;
-  }
-  if (a.dh) {
-    for (int e = tid; e < M * HCS; e += RT) {
-      const int m = e / HCS, kk = e - m * HCS, k = c0 + kk;
-      if (k >= K) continue;
-      float gv = 0.f;
-#pragma unroll
-      for (int j = 0; j < NCLS; ++j) gv = fmaf(s_log[m * 16 + j], s_w[k * NCLS + j], gv);
-      if (act) {   // post-activation value decides every supported derivative
-        const float y = s_hs[m * HCS + kk];
-        gv = act_bwd(gv, y, y, act, alpha);
-      }
-      a.dh[(long)m * K + k] = gv;
-    }
-  }
-  if (blockIdx.x == 0 && tid < NCLS) {
-    float acc = 0.f;
-    for (int m = 0; m < M; ++m) acc += s_log[m * 16 + tid];
-    a.db[tid] = acc;
-  }
-}
-
-// ---------------------------------------------------------------------------------
 // Row-group head with PARTIAL outputs (the fused-update step program): ceil(M / RG)
 // workgroups of 4 waves, RG <= 16 batch rows each; the waves split K (hidden features).
 // Every output has exactly one writer, so there are no atomics, no arrival counter and
@@ -925,20 +773,6 @@ CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, c
   if (M <= 0 || M > 4096) return -1;
   HeadArgs a{h, M, K, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dw, db, dh,
              logits_out, step, ring_loss, ring_correct, ring};
-  // measured on MI355X (sample config): 19.3 us vs 14.5 us for the row-group kernel — the
-  // per-MFMA LDS read of the Wh operand serialises its 128-step chain — so it is opt-in
-  static const bool cols_on = [] { const char* e = getenv("CSA_HEAD_COLS"); return e && atoi(e) != 0; }();
-  const size_t cols_lds = ((size_t)K * NCLS + 64 * 16 + 64 * HCS) * sizeof(float);
-  if (cols_on && M <= 64 && K >= 16 && K <= 512 && K % 16 == 0 && cols_lds <= HEAD_LDS_MAX) {
-    if (cols_lds > 64 * 1024) {
-      static bool attr = hipFuncSetAttribute((const void*)head_cols_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)HEAD_LDS_MAX) == hipSuccess;
-      if (!attr) return -3;
-    }
-    hipLaunchKernelGGL(head_cols_kernel, dim3((K + HCS - 1) / HCS), dim3(RT), cols_lds, st, a);
-    return (int)hipGetLastError();
-  }
   // dW/db are ACCUMULATED (the caller zeroes them every step); ws = int[4] zeroed once
   const size_t rows_lds =
       ((size_t)RG * NCLS + 4 * 256 + 8 + (size_t)K * NCLS + (size_t)RG * (K + 1)) * sizeof(float);

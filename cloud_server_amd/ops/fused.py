@@ -44,8 +44,6 @@ _SIGS = {
     "csa_conv_dgrad_nslab": (I, [P]),
     "csa_conv_dgrad": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, P]),
     "csa_conv_bwd": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, P, P, I, P]),
-    "csa_conv_bwd_route": (I, [P, P, P, P, I, F, P, I, F, F, P, P, P, P, P, I,
-                               P, P, P, P, I, F, P, I, F, F, P, P, P, I, P, P, P, P, F, P]),
     "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P, P]),
     "csa_optimizer": (I, [I, P, P, P, P, L, I, F, P, P, P, I, P, P, P, P, P, I, P, P, I, P, L, P]),
     "csa_optimizer2": (I, [I, P, P, P, P, L, P, P, I, I, F, P, P, P, I, P, P, P, P, P, P, I, P, P, I,

@@ -151,11 +151,6 @@ class HipProgram:
         sample config that is one ~1 MB bucket (head+fc2) launched after fc2, the 8 MB
         fc1 bucket launched right after fc1's weight gradient, and a small tail."""
         e = self.e
-        # measured on MI355X: the forked stream costs more in cross-queue sync than it
-        # overlaps (207 -> 233 us/step, profiles/r1_ab_wgrad_stream.txt), so it is opt-in
-        self.wsplit = os.environ.get("CSA_WGRAD_STREAM", "0") == "1"
-        if self.wsplit:
-            self.wstream = torch.cuda.Stream(e.device)
         self.overlap = (e.ctx.enabled and e.sync.strategy == "allreduce" and
                         os.environ.get("CSA_DP_OVERLAP", "1") == "1")
         self.bucket_at: Dict[object, tuple] = {}
@@ -265,24 +260,12 @@ class HipProgram:
                     W * B, fin, fout, None, 0, 0, 0.0, 0.0, None, None, u.lr_act[0], u.lr_act[1], 1.0, ss),
                     "dense_wgrad(lowrank)")
 
-    def _fork_wgrad(self, st):
-        """Weight gradients are off the critical path (nothing in this step reads them
-        before the optimizer), so they go to a second stream forked from the main one
-        and overlap the next dgrad/route kernels; the main stream joins before the
-        optimizer.  Returns the stream handle to launch on."""
-        if not self.wsplit:
-            return st
-        self.wstream.wait_stream(torch.cuda.current_stream(self.e.device))
-        return self.wstream.cuda_stream
-
     def _grad_ready(self, key) -> None:
         b = self.bucket_at.get(key)
         if b is None:
             return
         cur = torch.cuda.current_stream(self.e.device)
         self.side.wait_stream(cur)
-        if self.wsplit:
-            self.side.wait_stream(self.wstream)
         with torch.cuda.stream(self.side):
             self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
 
@@ -574,9 +557,7 @@ class HipProgram:
                 self.lib.csa_dense_bwd_update_ws(u.layer.in_shape.numel, u.layer.spec.hidden, ws)
                 u.du_part = torch.zeros(max(int(ws[0]), 1), **f32)
                 u.du_cnt = torch.zeros(max(int(ws[1]), 1), dtype=torch.int32, device=dev)
-            u.in_tf.bn_tab = (torch.zeros(4, u.in_tf.slab.shape[2], **f32)
-                              if u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") != "1"
-                              else None)
+            u.in_tf.bn_tab = torch.zeros(4, u.in_tf.slab.shape[2], **f32) if u.xt is not None else None
         # the conv pair's last workgroup folds the following BatchNorm's statistics into the
         # consumer's [mean | rstd | a | b] table (VALU pair family; csa_conv_pair_fwd2), and
         # a register-direct dense consumer applies it while loading: no bn_act_apply launch
@@ -891,7 +872,7 @@ class HipProgram:
                     self._dense_bwd_direct(u, prev, st)
                     self._grad_ready(k)
                     continue
-                if (prev is not None and u not in self.lr_units and not self.wsplit
+                if (prev is not None and u not in self.lr_units
                         and self._dense_bwd_fused(u, prev, st)):
                     self._grad_ready(k)          # dgrad + wgrad in one launch
                     continue
@@ -906,7 +887,7 @@ class HipProgram:
                         self._lowrank_wgrads()
                     self._grad_ready(k)
                     continue
-                ws = self._fork_wgrad(st)
+                ws = st
                 if u.xt is not None:
                     self._rc(lib.csa_dense_wgrad(
                         K.ptr(u.xt), K.ptr(u.dy), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
@@ -919,10 +900,6 @@ class HipProgram:
                 # output side: (BN backward of the NEXT transform) + act backward + pool routing
                 next_tf = self.units[k + 1].in_tf if k + 1 < len(self.units) else self.head_tf
                 need_route = next_tf.has_bn or u.act is not None or u.pool is not None
-                if need_route and prev is not None and self._conv_bwd_route_fused(u, prev, next_tf, st):
-                    self._sync_bn_param_grads(next_tf)
-                    self._grad_ready(k)          # route + input gradient + weight gradient: one launch
-                    continue
                 if need_route:
                     oh, ow = lp.out_shape.hw
                     g = [B, u.y.shape[1], u.y.shape[2], u.y.shape[3], oh, ow,
@@ -954,7 +931,7 @@ class HipProgram:
                 sp = lp.spec
                 h, w = lp.in_shape.hw
                 oh, ow = lp.out_shape.hw
-                if prev is not None and not self.wsplit and os.environ.get("CSA_CONV_PAIR", "1") == "1":
+                if prev is not None and os.environ.get("CSA_CONV_PAIR", "1") == "1":
                     # input gradient + weight gradient in one launch
                     self._rc(lib.csa_conv_bwd(
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
@@ -962,7 +939,7 @@ class HipProgram:
                         K.ptr(u.dw_acc), K.ptr(u.db_acc) if sp.bias else None, u.wg_stripes, st), "conv_bwd")
                     self._grad_ready(k)
                     continue
-                ws = self._fork_wgrad(st)
+                ws = st
                 self._rc(lib.csa_conv_wgrad(
                     None if raw else K.ptr(u.x), K.ptr(img) if raw else None, K.ptr(rows) if raw else None,
                     K.ptr(dc), K.ptr(u.dw_acc), K.ptr(u.db_acc) if sp.bias else None, u.wg_stripes,
@@ -977,8 +954,6 @@ class HipProgram:
 
         # ---------------- gradient sync + optimizer ----------------
         main = torch.cuda.current_stream(e.device)
-        if self.wsplit:
-            main.wait_stream(self.wstream)
         if self.overlap:
             main.wait_stream(self.side)
         elif e.ctx.enabled and e.sync.strategy == "lowrank":
@@ -1047,13 +1022,6 @@ class HipProgram:
                     e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
             else:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
-                if u.direct and u.xt is not None and os.environ.get("CSA_FWD_BN_FUSE", "0") == "1":
-                    # BN + act applied while the GEMM loads its input; N-tile 0 writes xt
-                    self._rc(lib.csa_dd_fwd_bn(
-                        K.ptr(u.x.view(B, -1)), K.ptr(V[f"{lp.name}.weight"]), K.ptr(V[f"{lp.name}.bias"]),
-                        K.ptr(u.y), B, fout, fin, in_act, in_alpha, *self._bn_args_c(tf), K.ptr(u.xt), st),
-                        "dd_fwd_bn")
-                    continue
                 if (u.direct and u.xt is not None and getattr(tf, "pair_tab", None) is not None
                         and not self._eval_bn and not self.sync_bn):
                     # BN + act applied while the GEMM loads its input, from the table the conv
@@ -1259,35 +1227,6 @@ class HipProgram:
         if self.sync_bn and tf.has_bn and self.W > 1:
             for p in ("scale", "offset"):
                 self.gviews[f"{tf.norm.name}.{p}"].mul_(1.0 / self.W)
-
-    def _conv_bwd_route_fused(self, u: Unit, prev: Unit, next_tf: Transform, st) -> bool:
-        """Route backward (BN + act backward + pool routing) fused into the conv unit's
-        input-gradient / weight-gradient pair (``csa_conv_bwd_route``).  False: outside
-        the fused family (overlapping / padded pool) or disabled."""
-        # opt-in: measured on MI355X (sample config) the fused launch took 30.4 us against
-        # 8.5 + 20.1 us for route + pair — every workgroup re-reduces both BN slabs before
-        # its first load — so the separate route launch stays the default
-        if self.wsplit or os.environ.get("CSA_CONV_PAIR", "1") != "1" or os.environ.get("CSA_ROUTE_FUSE", "0") != "1":
-            return False
-        lp, tf, sp = u.layer, u.in_tf, u.layer.spec
-        V, G = self.views, self.gviews
-        nbn = self._bn_args(next_tf)
-        dsc = G[f"{next_tf.norm.name}.scale"] if next_tf.has_bn else None
-        dof = G[f"{next_tf.norm.name}.offset"] if next_tf.has_bn else None
-        rm = rv = None
-        if next_tf.has_bn:
-            rm = getattr(self.model, f"bn{next_tf.norm.index}_mean")
-            rv = getattr(self.model, f"bn{next_tf.norm.index}_var")
-        rc = self.lib.csa_conv_bwd_route(
-            K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), self._conv_geom(lp, self.B), K.ptr(u.x),
-            _act_id(tf.act), _alpha(tf.act), *self._bn_args(tf), K.ptr(tf.bwd_slab),
-            K.ptr(u.dw_acc), K.ptr(u.db_acc) if sp.bias else None, u.wg_stripes,
-            K.ptr(u.dy), K.ptr(u.y), K.ptr(u.argmax), K.ints(self._route_geom(u)), _act_id(u.act), _alpha(u.act),
-            *nbn, K.ptr(next_tf.bwd_slab), next_tf.bwd_nslab, K.ptr(dsc), K.ptr(dof), K.ptr(rm), K.ptr(rv),
-            float(self.model.bn_momentum), st)
-        if rc < 0:
-            raise RuntimeError(f"conv_bwd_route failed: {rc}")
-        return rc == 1
 
     def _dense_bwd_fused(self, u: Unit, prev: Unit, st) -> bool:
         """Input gradient + weight gradient of a dense unit as ONE launch
