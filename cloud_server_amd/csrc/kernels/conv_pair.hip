@@ -977,6 +977,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
     for (int q = 0; q < 4; ++q) { acc[q][0] = b0; acc[q][1] = b1; }
     const float* cb = s_c1 + ((y2b - r2a) * t.T1W + x2b) * g.C1;
     const bool wide = g.pool != 0;                           // window rows/cols beyond KBH x KBW
+#pragma unroll 2
     for (int c1 = 0; c1 < g.C1; ++c1) {
       float cv[WR][WC];
 #pragma unroll
@@ -1050,21 +1051,47 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
       if (s_last) __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
     }
     __syncthreads();
-    if (s_last && tid < g.C2) {
+    if (s_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: loads stay below
-      float s1 = 0.f, s2 = 0.f;
-      for (int r = 0; r < a.nslab; ++r) {                   // rows in fixed order
-        s1 += __hip_atomic_load(a.stat + (size_t)r * 2 * g.C2 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s2 += __hip_atomic_load(a.stat + (size_t)r * 2 * g.C2 + g.C2 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // every row value loaded by its own thread (all in flight), then a fixed-order
+      // two-level sum: 8 row slices per column, slices in order
+      float* s_rows = s_out;                                  // the outputs are stored already
+      const int C2x2 = 2 * g.C2, nv = a.nslab * C2x2;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = u * CPV_T + tid;
+        v[u] = e < nv ? __hip_atomic_load(a.stat + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
       }
-      const float mean = s1 / a.bn_count;
-      const float var = fmaxf(s2 / a.bn_count - mean * mean, 0.f);
-      const float rstd = rsqrtf(var + a.bn_eps);
-      const float sa = a.bn_scale[tid] * rstd;
-      a.tab[tid] = mean;
-      a.tab[g.C2 + tid] = rstd;
-      a.tab[2 * g.C2 + tid] = sa;
-      a.tab[3 * g.C2 + tid] = a.bn_offset[tid] - mean * sa;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = u * CPV_T + tid;
+        if (e < nv) s_rows[e] = v[u];
+      }
+      __syncthreads();
+      constexpr int NSL = 8;
+      const int rper = (a.nslab + NSL - 1) / NSL;
+      float* s_slice = s_rows + nv;                           // [NSL][2 C2]
+      if (tid < NSL * C2x2) {
+        const int col = tid % C2x2, sl = tid / C2x2;
+        float acc = 0.f;
+        for (int r = sl * rper; r < min(a.nslab, (sl + 1) * rper); ++r) acc += s_rows[r * C2x2 + col];
+        s_slice[sl * C2x2 + col] = acc;
+      }
+      __syncthreads();
+      if (tid < g.C2) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int sl = 0; sl < NSL; ++sl) { s1 += s_slice[sl * C2x2 + tid]; s2 += s_slice[sl * C2x2 + g.C2 + tid]; }
+        const float mean = s1 / a.bn_count;
+        const float var = fmaxf(s2 / a.bn_count - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + a.bn_eps);
+        const float sa = a.bn_scale[tid] * rstd;
+        a.tab[tid] = mean;
+        a.tab[g.C2 + tid] = rstd;
+        a.tab[2 * g.C2 + tid] = sa;
+        a.tab[3 * g.C2 + tid] = a.bn_offset[tid] - mean * sa;
+      }
     }
   }
   CP_STAMP(4);
@@ -1126,7 +1153,7 @@ __host__ __device__ inline CPVBwdLds cpv_bwd_lds(const CPGeom& g, const CPVBwdTi
   // slab rows (fwd | bwd) staged for the fold, later the weight-gradient slice partials
   const int KB = g.KBh * g.KBw * g.C1, combos = g.C1 * (g.C2 / 2), nsl = combos > 0 ? (CPV_T / combos > 0 ? CPV_T / combos : 1) : 1;
   const int partB = nsl * (KB * g.C2 + g.C2), partA = CPV_T * 2;
-  int red = (32 + 16) * 2 * CPV_MAXC2;
+  int red = (32 + 16) * 2 * CPV_MAXC2 + 4 * 4 * CPV_MAXC2;
   red = red > partB ? red : partB;
   red = red > partA ? red : partA;
   L.red = o; o += red;
@@ -1220,25 +1247,48 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
   __syncthreads();
   CP_STAMP(9);
   // ---- P1: BN tables (rows summed in fixed order) | c1 tile
-  if (a.bn_on && tid < g.C2) {
-    const int c = tid;
-    float s1 = 0.f, s2 = 0.f, b1 = 0.f, b2 = 0.f;
-    for (int r = 0; r < a.bn.nslab; ++r) { s1 += s_red[r * C2x2 + c]; s2 += s_red[r * C2x2 + g.C2 + c]; }
-    for (int r = 0; r < a.bwd_nslab; ++r) { b1 += s_red[nsf + r * C2x2 + c]; b2 += s_red[nsf + r * C2x2 + g.C2 + c]; }
-    const float mean = s1 / a.bn.count;
-    const float var = fmaxf(s2 / a.bn.count - mean * mean, 0.f);
-    const float rstd = rsqrtf(var + a.bn.eps);
-    s_bn[c] = mean;
-    s_bn[CPV_MAXC2 + c] = rstd;
-    s_bn[2 * CPV_MAXC2 + c] = sc * rstd;
-    s_bn[3 * CPV_MAXC2 + c] = b1;
-    s_bn[4 * CPV_MAXC2 + c] = b2;
-    if (blockIdx.x == 0) {
-      a.doffset[c] = b1;
-      a.dscale[c] = b2;
-      if (a.run_mean) {
-        a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
-        a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var;
+  if (a.bn_on) {
+    // fixed-order two-level fold of both slabs: column x row-slice partials, then slices
+    // in order (a one-thread-per-column chain of 48 dependent LDS reads took ~2 us)
+    constexpr int NSL = 4;
+    float* s_sl = s_red + nsf + nsb;                         // [NSL][4 C2]
+    const int cols = 2 * C2x2;                               // fwd S1 | fwd S2 | bwd S1 | bwd S2
+    if (tid < NSL * cols) {
+      const int col = tid % cols, sl = tid / cols;
+      const bool fw = col < C2x2;
+      const int nr = fw ? a.bn.nslab : a.bwd_nslab, c = fw ? col : col - C2x2;
+      const float* base = s_red + (fw ? 0 : nsf);
+      const int rper = (nr + NSL - 1) / NSL;
+      float acc = 0.f;
+      for (int r = sl * rper; r < min(nr, (sl + 1) * rper); ++r) acc += base[r * C2x2 + c];
+      s_sl[sl * cols + col] = acc;
+    }
+    __syncthreads();
+    if (tid < g.C2) {
+      const int c = tid;
+      float s1 = 0.f, s2 = 0.f, b1 = 0.f, b2 = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl) {
+        s1 += s_sl[sl * cols + c];
+        s2 += s_sl[sl * cols + g.C2 + c];
+        b1 += s_sl[sl * cols + C2x2 + c];
+        b2 += s_sl[sl * cols + C2x2 + g.C2 + c];
+      }
+      const float mean = s1 / a.bn.count;
+      const float var = fmaxf(s2 / a.bn.count - mean * mean, 0.f);
+      const float rstd = rsqrtf(var + a.bn.eps);
+      s_bn[c] = mean;
+      s_bn[CPV_MAXC2 + c] = rstd;
+      s_bn[2 * CPV_MAXC2 + c] = sc * rstd;
+      s_bn[3 * CPV_MAXC2 + c] = b1;
+      s_bn[4 * CPV_MAXC2 + c] = b2;
+      if (blockIdx.x == 0) {
+        a.doffset[c] = b1;
+        a.dscale[c] = b2;
+        if (a.run_mean) {
+          a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
+          a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var;
+        }
       }
     }
   }
@@ -1298,6 +1348,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
       float acc[KBH * KBW][2], ab[2] = {0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < KBH * KBW; ++k) { acc[k][0] = 0.f; acc[k][1] = 0.f; }
+#pragma unroll 4
       for (int p = sl; p < npx2; p += nsl) {
         const int y2 = t.o2a + p / g.W2, x2 = p % g.W2;
         const float2 d = *reinterpret_cast<const float2*>(s_dc2 + ((y2 - t.d2a) * g.W2 + x2) * g.C2 + c2);
@@ -1351,8 +1402,9 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
           const float* dr = s_dc2 + ((y2 - t.d2a) * g.W2 + x2) * g.C2;
           const float* w0 = wB + ((i * KBW + j) * g.C1 + c1) * g.C2;
           const float* w1 = w0 + g.C2;
-#pragma unroll 2
-          for (int c2 = 0; c2 < g.C2; c2 += 4) {
+#pragma unroll
+          for (int c2 = 0; c2 < CPV_MAXC2; c2 += 4) {
+            if (c2 >= g.C2) break;                           // uniform
             const float4 d = *reinterpret_cast<const float4*>(dr + c2);
             const float4 u0 = *reinterpret_cast<const float4*>(w0 + c2);
             const float4 u1 = *reinterpret_cast<const float4*>(w1 + c2);
@@ -1384,6 +1436,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
         koff = (i * t.TXW + j) * g.C0 + c0;
       }
       float a0 = 0.f, a1 = 0.f;
+#pragma unroll 4
       for (int p = sl; p < npx; p += nsl) {
         const int y1 = t.o1a + p / g.W1, x1 = p % g.W1;
         const float xv2 = k < KA ? s_x[((y1 - g.PTA - t.xa) * t.TXW + x1 + g.PLB) * g.C0 + koff] : 1.f;
@@ -1443,7 +1496,8 @@ static size_t cpv_fwd_lds(const CPGeom& g) {
   const int rows = g.pool ? 2 * g.PR : g.PR;
   const int T1H = rows + g.KBh - 1, T1W = g.W2 + g.KBw - 1;
   const int units = (g.pool ? g.PR * g.PW : g.PR * g.W2);
-  return (size_t)(((T1H * T1W * g.C1 + 3) & ~3) + units * g.C2) * sizeof(float);
+  const int outs = std::max(units * g.C2, 8 * CPV_T + 8 * 2 * CPV_MAXC2);   // (later the slab fold)
+  return (size_t)(((T1H * T1W * g.C1 + 3) & ~3) + outs) * sizeof(float);
 }
 
 static bool cp_geom(const int* v, CPGeom& g) {
@@ -1553,7 +1607,8 @@ CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.bB = bB; a.actB = actB; a.alphaB = alphaB; a.y = y; a.argmax = argmax; a.stat = stat;
   a.nslab = nslab < 1 ? 1 : nslab;
-  if (tab && (!stat || !cnt || !bn_scale || !bn_offset || !cpv_ok(a.g))) return -2;
+  if (tab && (!stat || !cnt || !bn_scale || !bn_offset || !cpv_ok(a.g) || a.nslab * 2 * a.g.C2 > 8 * CPV_T))
+    return -2;
   if (cpv_ok(a.g)) {
     CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab,
                  tab, cnt, bn_scale, bn_offset, bn_count, bn_eps};

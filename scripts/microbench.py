@@ -146,7 +146,7 @@ def main() -> int:
                     torch.cuda.synchronize()
                     eng.program.lib.csa_cp_debug(None)
                 t = dbg.tolist()
-                if name.endswith("fwd"):
+                if "fwd" in name:
                     print(f"{i:2d} {name}: stage {t[1]-t[0]} convA {t[2]-t[1]} convB+pool {t[3]-t[2]} "
                           f"stats {t[4]-t[3]} (s_memtime ticks)")
                 elif t[14] == 0:      # VALU backward (cpv_bwd_kernel)
