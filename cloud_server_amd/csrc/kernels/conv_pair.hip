@@ -1072,8 +1072,8 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
       constexpr int NSL = 8;
       const int rper = (a.nslab + NSL - 1) / NSL;
       float* s_slice = s_rows + nv;                           // [NSL][2 C2]
-      if (tid < NSL * C2x2) {
-        const int col = tid % C2x2, sl = tid / C2x2;
+      for (int e = tid; e < NSL * C2x2; e += CPV_T) {
+        const int col = e % C2x2, sl = e / C2x2;
         float acc = 0.f;
         for (int r = sl * rper; r < min(a.nslab, (sl + 1) * rper); ++r) acc += s_rows[r * C2x2 + col];
         s_slice[sl * C2x2 + col] = acc;
@@ -1253,8 +1253,8 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
     constexpr int NSL = 4;
     float* s_sl = s_red + nsf + nsb;                         // [NSL][4 C2]
     const int cols = 2 * C2x2;                               // fwd S1 | fwd S2 | bwd S1 | bwd S2
-    if (tid < NSL * cols) {
-      const int col = tid % cols, sl = tid / cols;
+    for (int e = tid; e < NSL * cols; e += CPV_T) {
+      const int col = e % cols, sl = e / cols;
       const bool fw = col < C2x2;
       const int nr = fw ? a.bn.nslab : a.bwd_nslab, c = fw ? col : col - C2x2;
       const float* base = s_red + (fw ? 0 : nsf);
