@@ -17,6 +17,10 @@ namespace csa {
 
 enum Act : int { ACT_NONE = 0, ACT_SIGMOID = 1, ACT_RELU = 2, ACT_LEAKY = 3 };
 
+// Deterministic mode (det.hip, host state): launch helpers choose exclusive destinations
+// and no split-K, so no float atomic has more than one contributor per slot.
+extern int g_csa_det;
+
 __device__ __forceinline__ float act_fwd(float x, int act, float alpha) {
   switch (act) {
     case ACT_SIGMOID: return __builtin_amdgcn_rcpf(1.0f + __expf(-x));   // v_exp + v_rcp

@@ -1582,6 +1582,13 @@ CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_
                                int nslab, float* tab, unsigned* cnt, const float* bn_scale, const float* bn_offset,
                                float bn_count, float bn_eps, hipStream_t st);
 
+// Workgroups of the pair launches (one per (image, band)): deterministic mode gives every
+// workgroup its own statistic row and weight-gradient stripe.
+CSA_API int csa_conv_pair_grid(const int* geom) {
+  CPGeom g;
+  return cp_geom(geom, g) ? g.B * g.nbands : 0;
+}
+
 // Is the VALU pair family (cpv kernels, BN table by the last workgroup) in use for geom?
 CSA_API int csa_conv_pair_tab_ok(const int* geom) {
   CPGeom g;

@@ -65,6 +65,8 @@ struct DUArgs {
   BNRef bn; int bn_on;      // forward BatchNorm of the input, channel = f % C
   const float* bn_tab;      // [4][C] mean | rstd | a | b (null: reduce bn.slab here)
   float* bwd_slab;          // [DU_SLAB][2][C]: {sum dz, sum dz*xhat}, atomically folded
+  int det;                  // deterministic mode: bwd_slab has one EXCLUSIVE row per row
+                            // group (plain stores, folded in fixed order by csa_rows_fold)
   const float* Xw;          // [M][K] weight-gradient operand (transform applied)
   int opt; float lr; const int64_t* step;
   float* s0w; float* s1w;   // optimizer slots of W (same [K][N] layout) ...
@@ -508,7 +510,19 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
       }
     }
     __syncthreads();
-    if (tid < 32 && (tid & 15) < nf) {
+    if (a.det) {
+      // the group's whole row [2][C], features of one channel summed in feature order
+      if (tid < 2 * C) {
+        const int st = tid / C, c = tid - st * C;
+        float acc = 0.f;
+        for (int ff = 0; ff < nf; ++ff)
+          if ((f0 + ff) % C == c) {
+            const int e = 16 * st + ff;
+            acc += sred[e] + sred[32 + e] + sred[64 + e] + sred[96 + e];
+          }
+        a.bwd_slab[(size_t)grp * 2 * C + tid] = acc;
+      }
+    } else if (tid < 32 && (tid & 15) < nf) {
       const float acc = sred[tid] + sred[32 + tid] + sred[64 + tid] + sred[96 + tid];
       const int st = tid >> 4, c = (f0 + (tid & 15)) % C;
       atomicAdd(a.bwd_slab + (size_t)(grp % DU_SLAB) * 2 * C + st * C + c, acc);
@@ -536,7 +550,11 @@ CSA_API int csa_dense_bwd_update_ok(int M, int K, int N, int bn_C) {
 }
 
 // BN-backward slab rows the kernel accumulates into (atomically; the caller zeroes them).
-CSA_API int csa_dense_bwd_update_slabs(int K) { return (K + DU_FT - 1) / DU_FT < DU_SLAB ? (K + DU_FT - 1) / DU_FT : DU_SLAB; }
+// Deterministic mode: one exclusive row per row group.
+CSA_API int csa_dense_bwd_update_slabs(int K) {
+  const int groups = (K + DU_FT - 1) / DU_FT;
+  return g_csa_det || groups < DU_SLAB ? groups : DU_SLAB;
+}
 
 // Column blocks per row group the launcher picks: one 1024-thread block when the row groups
 // fill the chip (fc1: 245) and N <= 512, else 128-column blocks of 256 threads.
@@ -611,7 +629,7 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
   a.act = act; a.alpha = alpha;
   a.bn = BNRef{bn_slab, bn_nslab, bn_slab ? bn_C : 1, bn_count, bn_eps, bn_scale, bn_offset};
   a.bn_on = bn_slab != nullptr; a.bn_tab = bn_slab ? bn_tab : nullptr;
-  a.bwd_slab = bwd_slab; a.Xw = Xw;
+  a.bwd_slab = bwd_slab; a.Xw = Xw; a.det = g_csa_det;
   a.opt = opt; a.lr = lr; a.step = step; a.s0w = s0w; a.s1w = s1w; a.s0b = s0b; a.s1b = s1b; a.scale = scale;
   const int groups = (K + DU_FT - 1) / DU_FT;
   a.cs = du_cs(K, N);

@@ -69,6 +69,10 @@ _SIGS = {
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P]),
     "csa_conv_pair_fwd2": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P, P, P, P, F, F, P]),
     "csa_conv_pair_tab_ok": (I, [P]),
+    "csa_conv_pair_grid": (I, [P]),
+    "csa_set_deterministic": (None, [I]),
+    "csa_deterministic": (I, []),
+    "csa_rows_fold": (I, [P, L, I, L, P, I, P]),
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
                               P, P, P, P, I, P]),
     "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),

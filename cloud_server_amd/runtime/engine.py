@@ -107,19 +107,15 @@ class TrainEngine:
         self.ring_loss = torch.zeros(RING, dtype=torch.float32, device=self.device)
         self.host_step = 0
         # CSA_DETERMINISTIC=1: bitwise-reproducible steps for tests and
-        # debugging — the HIP program's split-K / statistics atomics make its fp32 sums
-        # order-dependent, so the step runs on the eager program with PyTorch's
-        # deterministic algorithms, atomics-free pooling and fixed-order collectives
-        # (RCCL ring / the xGMI kernels sum in rank order); still captured in a HIP graph
+        # debugging.  The HIP program keeps its kernels and swaps every cross-workgroup
+        # float atomic for exclusive rows + fixed-order folds (det.hip); a network outside
+        # that family runs on the eager program with PyTorch's deterministic algorithms and
+        # atomics-free pooling.  Either way still captured in a HIP graph
         self.deterministic = deterministic_mode()
-        if self.deterministic:
-            backend = "torch"
-            enable_deterministic_torch()
-            self.model.deterministic = True
         if backend == "auto":
             backend = "hip" if self.device.type == "cuda" else "torch"
         self.backend = backend
-        self.fallback_reason = "deterministic mode" if self.deterministic else ""
+        self.fallback_reason = ""
         if backend == "hip":
             from .hip_program import HipProgram, Unsupported
             try:
@@ -127,8 +123,11 @@ class TrainEngine:
             except Unsupported as exc:   # config outside the fused-kernel family
                 self.fallback_reason = str(exc)
                 self.backend = backend = "torch"
-                self.program = TorchProgram(self)
-        else:
+        if backend == "torch":
+            if self.deterministic:
+                # the eager program: PyTorch's deterministic algorithms + gather-form pooling
+                enable_deterministic_torch()
+                self.model.deterministic = True
             self.program = TorchProgram(self)
         # the program re-stages its batch whenever the host moves the cursor (seek/resume)
         self.stream.on_reset = (lambda: self.program.prime()) if hasattr(self.program, "prime") else None

@@ -72,6 +72,10 @@ class Transform:
     count: float = 0.0
     bwd_slab: Optional[torch.Tensor] = None  # filled by the consumer's dgrad
     bwd_nslab: int = 0
+    # deterministic mode: rows the producer writes (one per workgroup, folded to row 0 in
+    # fixed order by csa_rows_fold; consumers then read nslab = 1)
+    prod_rows: int = 0
+    bwd_prod_rows: int = 0
 
     @property
     def has_bn(self) -> bool:
@@ -110,6 +114,28 @@ class HipProgram:
         self.lib = K.load(required=True)
         if eng.device.type != "cuda":
             raise Unsupported("HIP program needs a GPU device")
+        # CSA_DETERMINISTIC=1: bitwise-reproducible steps on the same kernels (det.hip):
+        # exclusive slab rows / weight-gradient stripes per workgroup, fixed-order folds,
+        # no split-K.  The library flag is process state: set around every planning and
+        # launch sequence of this program, restored afterwards.
+        self.det = bool(getattr(eng, "deterministic", False)) and not forward_only
+        with self._det_scope():
+            self._init_plan(eng, forward_only)
+
+    def _det_scope(self):
+        prog = self
+
+        class _Scope:
+            def __enter__(self_):
+                self_.prev = int(prog.lib.csa_deterministic())
+                prog.lib.csa_set_deterministic(1 if prog.det else 0)
+
+            def __exit__(self_, *exc):
+                prog.lib.csa_set_deterministic(self_.prev)
+                return False
+        return _Scope()
+
+    def _init_plan(self, eng, forward_only: bool) -> None:
         self.B = eng.cfg.batch_size
         self.model = eng.model
         # SyncBN under DP: forward {sum, sumsq} slabs and backward {sum dz, sum dz*xhat}
@@ -123,6 +149,8 @@ class HipProgram:
         self._lower()
         self._plan_fused()
         self._plan_pair()
+        if self.det:
+            self._check_det()
         self._alloc()
         self._plan_splits()
         if forward_only:
@@ -374,6 +402,32 @@ class HipProgram:
             return
         self.pair = geom
 
+    # ------------------------------------------------------------------ deterministic mode
+    def _check_det(self) -> None:
+        """Deterministic mode covers the fused one-GPU family: the VALU conv pair (fixed-order
+        in-workgroup reductions; exclusive statistic rows and weight-gradient stripes), fused
+        dense backward + update units (exclusive BN-backward rows, fixed-order column-block
+        hand-off), register-direct dense forwards without split-K, and the row-per-workgroup
+        head (fixed-order batch reductions in the last dense layer's epilogue).  Any other
+        lowering raises Unsupported, and the engine runs the step on eager PyTorch with its
+        deterministic algorithms instead."""
+        e = self.e
+        if e.ctx.enabled:
+            raise Unsupported("deterministic mode: data parallel steps run on the eager program")
+        if self.pair is None or not self.lib.csa_conv_pair_tab_ok(K.ints(self.pair)):
+            raise Unsupported("deterministic mode: network does not start with a VALU conv pair")
+        for u in self.units[2:]:
+            if u.kind != "dense" or not u.fused or not u.direct:
+                raise Unsupported(f"deterministic mode: {u.kind} unit {u.layer.name} has no fixed-order variant")
+            if u.in_tf.has_bn and u is not self.units[2]:
+                raise Unsupported("deterministic mode: BatchNorm after a dense layer")
+        if not self.head_row:
+            raise Unsupported("deterministic mode: head outside the row-per-workgroup family")
+
+    def _det_fold(self, t: torch.Tensor, rows: int, width: int, dst: torch.Tensor, zero_src: int, st) -> None:
+        """dst[:width] = fixed-order sum of the first ``rows`` rows of ``t`` (row stride width)."""
+        self._rc(self.lib.csa_rows_fold(K.ptr(t), width, rows, width, K.ptr(dst), zero_src, st), "rows_fold")
+
     # ------------------------------------------------------------------ lowering
     def _lower(self) -> None:
         layers = self.e.model.plan.layers
@@ -524,8 +578,10 @@ class HipProgram:
                 src = self.units[k - 1]
                 ph, pw = src.y.shape[1], src.y.shape[2]
                 nslab = self.lib.csa_conv_fwd_nslab(self._conv_geom(src.layer, B), self._pool_geom(src))
+                if self.det:            # one row per pair workgroup, folded to row 0
+                    nslab = tf.prod_rows = int(self.lib.csa_conv_pair_grid(K.ints(self.pair)))
                 tf.slab = torch.zeros(nslab, 2, src.y.shape[3], **f32)
-                tf.nslab = nslab
+                tf.nslab = 1 if self.det else nslab
                 tf.count = float(B * ph * pw * self.W)
                 if fo:
                     continue
@@ -541,6 +597,8 @@ class HipProgram:
                     nb = self.lib.csa_conv_dgrad_nslab(self._conv_geom(u.layer, B))
                 tf.bwd_slab = torch.zeros(nb, 2, C, **f32)
                 tf.bwd_nslab = nb
+                if self.det:            # one row per row group (csa_dense_bwd_update_slabs)
+                    tf.bwd_prod_rows, tf.bwd_nslab = nb, 1
         # dense consumers of a BatchNorm'd tensor get it materialised once per step
         for u in self.units:
             u.xt = None
@@ -564,6 +622,7 @@ class HipProgram:
         self.pair_cnt = None
         if (self.pair is not None and len(self.units) > 2 and self.units[2].in_tf.has_bn
                 and getattr(self.units[2].in_tf, "bn_tab", None) is not None and not self.sync_bn
+                and not self.det
                 and os.environ.get("CSA_PAIR_BN_TAB", "1") == "1" and self.lib.csa_conv_pair_tab_ok(_FK.ints(self.pair))):
             nt = self.units[2].in_tf
             nt.pair_tab = nt.bn_tab
@@ -647,7 +706,10 @@ class HipProgram:
                 # straight into the flat gradient (data parallelism, or beyond that budget)
                 nf = 1 + (1 if lp.spec.bias else 0)
                 S = 1 if self.e.ctx.enabled or fold_budget < nf else self.WGRAD_STRIPES
-                if S > 1:
+                u.det_fold = self.det and self.pair is not None and k < 2
+                if u.det_fold:          # one stripe per pair workgroup, folded after the pair
+                    S = int(self.lib.csa_conv_pair_grid(K.ints(self.pair)))
+                elif S > 1:
                     fold_budget -= nf
                 u.wg_stripes = S
                 nw = self.gviews[f"{lp.name}.weight"].numel()
@@ -791,6 +853,10 @@ class HipProgram:
 
     # ------------------------------------------------------------------ the step
     def run(self) -> None:
+        with self._det_scope():
+            self._run()
+
+    def _run(self) -> None:
         e, lib, B = self.e, self.lib, self.B
         st = K.stream()
         # this step's dataset rows = stream.rows[cursor]; the kernels resolve the cursor on
@@ -992,8 +1058,10 @@ class HipProgram:
                 _act_id(ua.act), _alpha(ua.act),
                 K.ptr(V[f"{ub.layer.name}.weight"]), K.ptr(V.get(f"{ub.layer.name}.bias")) if ub.layer.spec.bias else None,
                 _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
-                self.lib.csa_conv_fwd_nslab(None, None), K.ptr(tab), K.ptr(self.pair_cnt) if tab is not None else None,
-                *bn, st), "conv_pair_fwd")
+                nt.prod_rows if self.det else self.lib.csa_conv_fwd_nslab(None, None), K.ptr(tab),
+                K.ptr(self.pair_cnt) if tab is not None else None, *bn, st), "conv_pair_fwd")
+            if oslab is not None and self.det:
+                self._det_fold(oslab, nt.prod_rows, oslab.shape[1] * oslab.shape[2], oslab, 0, st)
             if oslab is not None and self.sync_bn:
                 e.sync.allreduce_tensors([oslab], tag="bnf1")
         for k, u in enumerate(self.units):
@@ -1144,6 +1212,10 @@ class HipProgram:
                                           K.ptr(u.bn_k), act, alpha, st), "bn_bwd_apply")
 
     def predict_logits_into(self, logits: torch.Tensor) -> None:
+        with self._det_scope():
+            self._predict_logits_into(logits)
+
+    def _predict_logits_into(self, logits: torch.Tensor) -> None:
         """Forward-only pass over this program's input rows -> ``logits`` [B, 10] (graph
         capturable; ``serve.hip_infer`` captures it per batch bucket).  BatchNorm uses the
         running statistics unless the model normalises with batch statistics in eval
@@ -1211,6 +1283,12 @@ class HipProgram:
             K.ptr(ub.dw_acc), K.ptr(ub.db_acc) if ub.layer.spec.bias else None,
             min(ua.wg_stripes, ub.wg_stripes), st), "conv_pair_bwd")
         self._sync_bn_param_grads(nt)
+        if self.det:
+            for u in (ua, ub):
+                lp = u.layer
+                self._det_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
+                if u.db_acc is not None:
+                    self._det_fold(u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"], 1, st)
 
     def _route_geom(self, u: Unit):
         lp, B = u.layer, self.B
@@ -1320,6 +1398,9 @@ class HipProgram:
             K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
             1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), *head, st),
             "dense_bwd_update")
+        if self.det and tf.has_bn:
+            self._det_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],
+                           tf.bwd_slab, 0, st)
 
     def _opt_segments(self):
         """Flat [lo, hi) spans the optimizer launch updates: everything except the
@@ -1362,7 +1443,7 @@ class HipProgram:
         folds = []          # striped conv weight gradients / head partials -> summed inside the update
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind == "conv" and u.wg_stripes > 1:
+            if u.kind == "conv" and u.wg_stripes > 1 and not getattr(u, "det_fold", False):
                 lp = u.layer
                 folds.append((offs[f"{lp.name}.weight"], u.dw_acc.shape[1], u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], 1))
                 if u.db_acc is not None:

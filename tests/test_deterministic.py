@@ -62,3 +62,67 @@ def test_deterministic_mode_bitwise_gpu(monkeypatch):
         assert torch.equal(a.flat, b.flat) and torch.equal(a.slots, b.slots)
     finally:
         torch.use_deterministic_algorithms(False)
+
+
+def _sample_engine(device, use_graph=True, opt="AdagradOptimizer", lr=0.01, n=600, seed=7):
+    c = copy.deepcopy(SAMPLE_CONFIG)
+    c.update(optimizer_name=opt, learning_rate=lr)
+    c["options"] = dict(batch_size=50)
+    return TrainEngine(parse_train_config(c), synthetic_mnist(n, seed=seed), device=device,
+                       backend="hip", use_graph=use_graph)
+
+
+@pytest.mark.gpu
+def test_deterministic_hip_kernels_bitwise_gpu(monkeypatch):
+    """The sample config keeps the HIP program in deterministic mode (exclusive statistic
+    rows / weight-gradient stripes per workgroup, fixed-order folds, no split-K): two
+    graph runs of 20 steps, an eager run, and a run of 8-step graphs are bitwise equal."""
+    monkeypatch.setenv("CSA_DETERMINISTIC", "1")
+    runs = []
+    for mode in ("graph", "graph", "eager", "group"):
+        eng = _sample_engine("cuda:0", use_graph=mode != "eager")
+        assert eng.backend == "hip" and eng.program.det, eng.fallback_reason
+        if mode == "group":
+            eng.step()
+            eng.run_steps(19)
+        else:
+            for _ in range(20):
+                eng.step()
+        eng.sync_device()
+        assert int(eng.dstep.item()) == 20
+        runs.append((eng.flat.clone(), eng.slots.clone(), eng.metrics_since(0)["loss"]))
+    for i in range(1, len(runs)):
+        assert torch.equal(runs[0][0], runs[i][0]), f"run {i}: params differ"
+        assert torch.equal(runs[0][1], runs[i][1]), f"run {i}: optimizer slots differ"
+        assert runs[0][2] == runs[i][2]
+
+
+@pytest.mark.gpu
+def test_deterministic_hip_matches_torch_and_fast_path(monkeypatch):
+    """Deterministic-mode gradients (one SGD step) agree with the fp32 eager reference and
+    with the atomic fast path to fp32 reassociation noise."""
+    def grads(det, backend):
+        monkeypatch.setenv("CSA_DETERMINISTIC", "1" if det else "0")
+        c = copy.deepcopy(SAMPLE_CONFIG)
+        c.update(optimizer_name="GradientDescentOptimizer", learning_rate=0.5)
+        c["options"] = dict(batch_size=50)
+        cfg = parse_train_config(c)
+        eng = TrainEngine(cfg, synthetic_mnist(300, seed=13), device="cuda:0", backend=backend, use_graph=False)
+        if backend == "hip":
+            assert eng.backend == "hip" and eng.program.det == det
+        w0 = eng.flat.clone()
+        eng.step()
+        eng.sync_device()
+        return eng, (w0 - eng.flat) / cfg.effective_lr
+    try:
+        e_det, g_det = grads(True, "hip")
+        _, g_fast = grads(False, "hip")
+        _, g_ref = grads(False, "torch")
+    finally:
+        torch.use_deterministic_algorithms(False)
+    for k in e_det.model.state.shapes:
+        a = e_det.model.state.view(k, g_det)
+        for other, tol in ((g_ref, 3e-3), (g_fast, 3e-3)):
+            b = e_det.model.state.view(k, other)
+            scale = b.abs().max().item() + 1e-6
+            assert (a - b).abs().max().item() <= tol * scale + 1e-6, k
