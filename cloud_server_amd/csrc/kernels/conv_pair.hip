@@ -24,6 +24,7 @@
 // (uint8 dataset rows gathered through the batch index stream).  Everything else uses the
 // per-layer kernels (conv.hip).
 #include "common.h"
+#include "optim_common.h"
 #include <cstdlib>
 #include <algorithm>
 
@@ -437,6 +438,25 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a) 
 
 // --------------------------------------------------------------------------------------
 // Backward.
+// The step's tail inside the pair backward (VALU family, one-GPU program without an
+// optimizer launch).  Every workgroup zeroes a slice of the ``zs`` regions (accumulators
+// nobody reads after the pair); the LAST workgroup to finish (arrival ticket) folds the
+// weight-gradient stripes in fixed order and applies the optimizer update to the pair's
+// parameters and the BatchNorm scale / offset (whose gradients every workgroup already
+// holds in LDS), zeroes the stripes and the ``zl`` regions (statistic slabs every
+// workgroup read in its prologue) and advances the batch cursor.
+constexpr int CPT_MAXZ = 4;
+constexpr int CPT_MAXS = 16;
+struct CPTail {
+  int on, opt; float lr; const int64_t* step;
+  float* w; float* s0; float* s1;                 // flat parameters and optimizer slots
+  long offA, offbA, offB, offbB, offS, offO;       // flat offsets (-1: absent)
+  float* zs[CPT_MAXZ]; long zsn[CPT_MAXZ]; int nzs;
+  float* zl[CPT_MAXZ]; long zln[CPT_MAXZ]; int nzl;
+  int64_t* cursor; long wrap;
+  unsigned* cnt;
+};
+
 struct CPBwdArgs {
   CPGeom g;
   const uint8_t* img; const int64_t* idx; const int64_t* cursor;
@@ -448,6 +468,7 @@ struct CPBwdArgs {
   BNRef bn; int bn_on; const float* bwd_slab; int bwd_nslab;
   float* dscale; float* doffset; float* run_mean; float* run_var; float momentum;
   float* dwA; float* dbA; float* dwB; float* dbB; int stripes;
+  CPTail tail;
 };
 
 // LDS carve of the backward (float offsets), shared by the kernel and the host size check.
@@ -862,10 +883,6 @@ struct CPVFwdArgs {
   const float* wA; const float* bA; int actA; float alphaA;
   const float* wB; const float* bB; int actB; float alphaB;
   float* y; uint8_t* argmax; float* stat; int nslab;
-  // BatchNorm table of the output (tab != null): the LAST workgroup to finish folds the
-  // statistic rows into [mean | rstd | a | b][C2] (a = scale * rstd, b = offset - mean a),
-  // so the consumers (the next dense layer's forward / backward) read 4 C2 floats
-  float* tab; unsigned* cnt; const float* bn_scale; const float* bn_offset; float bn_count, bn_eps;
 };
 
 __host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 1 + g.KAw - 1; }
@@ -1034,64 +1051,8 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
         acc += sq ? v * v : v;
       }
       float* row = a.stat + (size_t)(blockIdx.x % a.nslab) * 2 * g.C2;
-      if (a.nslab >= (int)gridDim.x && !a.tab) row[tid] = acc;   // one row per workgroup
+      if (a.nslab >= (int)gridDim.x) row[tid] = acc;           // one row per workgroup
       else atomicAdd(&row[tid], acc);
-    }
-  }
-  if (a.stat && a.tab) {
-    // last-arriver fold: the row atomics are device-scope (performed beyond every L2) and
-    // complete before the ticket (vmcnt drained); the last workgroup reads the rows with
-    // L1-bypassing agent loads — no L2 of its XCD ever held them during this launch
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == gridDim.x - 1;
-      if (s_last) __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-    }
-    __syncthreads();
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: loads stay below
-      // every row value loaded by its own thread (all in flight), then a fixed-order
-      // two-level sum: 8 row slices per column, slices in order
-      float* s_rows = s_out;                                  // the outputs are stored already
-      const int C2x2 = 2 * g.C2, nv = a.nslab * C2x2;
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = u * CPV_T + tid;
-        v[u] = e < nv ? __hip_atomic_load(a.stat + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = u * CPV_T + tid;
-        if (e < nv) s_rows[e] = v[u];
-      }
-      __syncthreads();
-      constexpr int NSL = 8;
-      const int rper = (a.nslab + NSL - 1) / NSL;
-      float* s_slice = s_rows + nv;                           // [NSL][2 C2]
-      for (int e = tid; e < NSL * C2x2; e += CPV_T) {
-        const int col = e % C2x2, sl = e / C2x2;
-        float acc = 0.f;
-        for (int r = sl * rper; r < min(a.nslab, (sl + 1) * rper); ++r) acc += s_rows[r * C2x2 + col];
-        s_slice[sl * C2x2 + col] = acc;
-      }
-      __syncthreads();
-      if (tid < g.C2) {
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int sl = 0; sl < NSL; ++sl) { s1 += s_slice[sl * C2x2 + tid]; s2 += s_slice[sl * C2x2 + g.C2 + tid]; }
-        const float mean = s1 / a.bn_count;
-        const float var = fmaxf(s2 / a.bn_count - mean * mean, 0.f);
-        const float rstd = rsqrtf(var + a.bn_eps);
-        const float sa = a.bn_scale[tid] * rstd;
-        a.tab[tid] = mean;
-        a.tab[g.C2 + tid] = rstd;
-        a.tab[2 * g.C2 + tid] = sa;
-        a.tab[3 * g.C2 + tid] = a.bn_offset[tid] - mean * sa;
-      }
     }
   }
   CP_STAMP(4);
@@ -1159,6 +1120,74 @@ __host__ __device__ inline CPVBwdLds cpv_bwd_lds(const CPGeom& g, const CPVBwdTi
   L.red = o; o += red;
   L.end = o;
   return L;
+}
+
+// The step's tail (see CPTail).  s_bn holds this workgroup's folded BatchNorm-backward
+// sums: [3 ld + c] = sum dz (offset gradient), [4 ld + c] = sum dz xhat (scale gradient).
+__device__ __forceinline__ void cpv_tail(const CPBwdArgs& a, const float* s_bn, int ld) {
+  const CPTail& T = a.tail;
+  const CPGeom& g = a.g;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // (1) this workgroup's slice of the shared zero regions
+  for (int z = 0; z < T.nzs; ++z) {
+    const long n = T.zsn[z], per = (n + gridDim.x - 1) / gridDim.x, lo = (long)blockIdx.x * per;
+    const long hi = lo + per < n ? lo + per : n;
+    for (long i = lo + tid; i < hi; i += nt) T.zs[z][i] = 0.f;
+  }
+  // (2) arrival ticket: every stripe atomic of this workgroup is performed (device scope,
+  // beyond every L2) before the ticket; the last workgroup reads the stripes with
+  // agent-scope loads
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(T.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == gridDim.x - 1;
+    if (s_last) __hip_atomic_store(T.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       // compiler-only: loads stay below
+  const float lr = opt_step_lr(T.opt, T.lr, T.step);
+  const int ns = opt_nslots(T.opt);
+  const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
+  const int nA = KA * g.C1, nbA = T.offbA >= 0 ? g.C1 : 0, nB = KB * g.C2, nbB = T.offbB >= 0 ? g.C2 : 0;
+  const int nS = T.offS >= 0 ? g.C2 : 0;
+  const int total = nA + nbA + nB + nbB + 2 * nS;
+  const int S = a.stripes;
+  for (int e = tid; e < total; e += nt) {
+    float* src = nullptr; long ld = 0, off; int i = e;
+    float gv = 0.f;
+    if (i < nA) { src = a.dwA; ld = nA; off = T.offA; }
+    else if ((i -= nA) < nbA) { src = a.dbA; ld = g.C1; off = T.offbA; }
+    else if ((i -= nbA) < nB) { src = a.dwB; ld = nB; off = T.offB; }
+    else if ((i -= nB) < nbB) { src = a.dbB; ld = g.C2; off = T.offbB; }
+    else if ((i -= nbB) < nS) { gv = s_bn[4 * ld + i]; off = T.offS; }
+    else { i -= nS; gv = s_bn[3 * ld + i]; off = T.offO; }
+    if (src) {                                                  // stripes in fixed order
+      float v[CPT_MAXS];
+#pragma unroll
+      for (int q = 0; q < CPT_MAXS; ++q)
+        v[q] = q < S ? __hip_atomic_load(src + (long)q * ld + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+#pragma unroll
+      for (int q = 0; q < CPT_MAXS; ++q) gv += v[q];
+#pragma unroll
+      for (int q = 0; q < CPT_MAXS; ++q)
+        if (q < S) src[(long)q * ld + i] = 0.f;                  // the next step accumulates again
+    }
+    const long p = off + i;
+    float w = T.w[p], s0 = ns >= 1 ? T.s0[p] : 0.f, s1 = ns >= 2 ? T.s1[p] : 0.f;
+    opt_update(T.opt, lr, w, gv, s0, s1);
+    T.w[p] = w;
+    if (ns >= 1) T.s0[p] = s0;
+    if (ns >= 2) T.s1[p] = s1;
+  }
+  for (int z = 0; z < T.nzl; ++z)
+    for (long j = tid; j < T.zln[z]; j += nt) T.zl[z][j] = 0.f;
+  if (tid == 0 && T.cursor) {
+    const int64_t c = *T.cursor + 1;
+    *T.cursor = (T.wrap > 0 && c >= T.wrap) ? 0 : c;
+  }
 }
 
 template <int KBH, int KBW>
@@ -1455,6 +1484,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
     }
   }
   CP_STAMP(13);
+  if (a.tail.on) cpv_tail(a, s_bn, CPV_MAXC2);
 }
 
 static bool cpv_ok(const CPGeom& g) {
@@ -1496,8 +1526,7 @@ static size_t cpv_fwd_lds(const CPGeom& g) {
   const int rows = g.pool ? 2 * g.PR : g.PR;
   const int T1H = rows + g.KBh - 1, T1W = g.W2 + g.KBw - 1;
   const int units = (g.pool ? g.PR * g.PW : g.PR * g.W2);
-  const int outs = std::max(units * g.C2, 8 * CPV_T + 8 * 2 * CPV_MAXC2);   // (later the slab fold)
-  return (size_t)(((T1H * T1W * g.C1 + 3) & ~3) + outs) * sizeof(float);
+  return (size_t)(((T1H * T1W * g.C1 + 3) & ~3) + units * g.C2) * sizeof(float);
 }
 
 static bool cp_geom(const int* v, CPGeom& g) {
@@ -1576,12 +1605,6 @@ CSA_API int csa_conv_pair_ok(const int* geom) {
   return cp_lds(g, true) <= CP_LDS_MAX ? 1 : 0;
 }
 
-CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
-                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
-                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
-                               int nslab, float* tab, unsigned* cnt, const float* bn_scale, const float* bn_offset,
-                               float bn_count, float bn_eps, hipStream_t st);
-
 // Workgroups of the pair launches (one per (image, band)): deterministic mode gives every
 // workgroup its own statistic row and weight-gradient stripe.
 CSA_API int csa_conv_pair_grid(const int* geom) {
@@ -1589,8 +1612,8 @@ CSA_API int csa_conv_pair_grid(const int* geom) {
   return cp_geom(geom, g) ? g.B * g.nbands : 0;
 }
 
-// Is the VALU pair family (cpv kernels, BN table by the last workgroup) in use for geom?
-CSA_API int csa_conv_pair_tab_ok(const int* geom) {
+// Is the VALU pair family (cpv kernels: fixed-order in-workgroup reductions) in use for geom?
+CSA_API int csa_conv_pair_valu_ok(const int* geom) {
   CPGeom g;
   return cp_geom(geom, g) && cpv_ok(g) ? 1 : 0;
 }
@@ -1599,26 +1622,13 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
                               int nslab, hipStream_t st) {
-  return csa_conv_pair_fwd2(geom, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, nslab,
-                            nullptr, nullptr, nullptr, nullptr, 1.f, 0.f, st);
-}
-
-// ... + (tab != null, VALU family only) the BatchNorm table of the output, see CPVFwdArgs.
-CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
-                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
-                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
-                               int nslab, float* tab, unsigned* cnt, const float* bn_scale, const float* bn_offset,
-                               float bn_count, float bn_eps, hipStream_t st) {
   CPFwdArgs a{};
   if (!cp_geom(geom, a.g) || cp_lds(a.g, false) > CP_LDS_MAX) return -1;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.bB = bB; a.actB = actB; a.alphaB = alphaB; a.y = y; a.argmax = argmax; a.stat = stat;
   a.nslab = nslab < 1 ? 1 : nslab;
-  if (tab && (!stat || !cnt || !bn_scale || !bn_offset || !cpv_ok(a.g) || a.nslab * 2 * a.g.C2 > 8 * CPV_T))
-    return -2;
   if (cpv_ok(a.g)) {
-    CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab,
-                 tab, cnt, bn_scale, bn_offset, bn_count, bn_eps};
+    CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab};
     if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
     else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
     return (int)hipGetLastError();
@@ -1631,6 +1641,14 @@ CSA_API int csa_conv_pair_fwd2(const int* geom, const uint8_t* img, const int64_
   return (int)hipGetLastError();
 }
 
+CSA_API int csa_conv_pair_bwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
+                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
+                               const float* bn_slab, int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                               const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
+                               float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
+                               float* dwB, float* dbB, int stripes, const CPTail* tail, hipStream_t st);
+
 CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
@@ -1638,7 +1656,34 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
                               const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
                               float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
                               float* dwB, float* dbB, int stripes, hipStream_t st) {
+  return csa_conv_pair_bwd2(geom, img, idx, cursor, wA, bA, actA, alphaA, wB, hasBiasB, actB, alphaB, dz, y, argmax,
+                            bn_slab, bn_nslab, bn_count, bn_eps, bn_scale, bn_offset, bwd_slab, bwd_nslab, dscale,
+                            doffset, run_mean, run_var, momentum, dwA, dbA, dwB, dbB, stripes, nullptr, st);
+}
+
+// Does the pair backward run the step's tail (optimizer of the pair + BN parameters,
+// zeroing, cursor) for geom?  Only the VALU family does.
+CSA_API int csa_conv_pair_tail_ok(const int* geom) {
+  CPGeom g;
+  return cp_geom(geom, g) && cpv_ok(g) ? 1 : 0;
+}
+
+// tail: the step's tail descriptor (null: none) — {on, opt, lr, step, w, s0, s1, 6 flat
+// offsets, shared zero regions, last-workgroup zero regions, cursor, wrap, ticket}
+CSA_API int csa_conv_pair_tail_size() { return (int)sizeof(CPTail); }
+
+CSA_API int csa_conv_pair_bwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
+                              const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
+                              int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
+                              const float* bn_slab, int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
+                              const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
+                              float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
+                              float* dwB, float* dbB, int stripes, const CPTail* tail, hipStream_t st) {
   CPBwdArgs a{};
+  if (tail && tail->on) {
+    a.tail = *tail;
+    if (!a.tail.cnt || !a.tail.w || a.tail.nzs > CPT_MAXZ || a.tail.nzl > CPT_MAXZ || stripes > CPT_MAXS) return -2;
+  }
   if (!cp_geom(geom, a.g) || cp_lds(a.g, true) > CP_LDS_MAX) return -1;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.actB = actB; a.alphaB = alphaB; a.hasBiasB = hasBiasB; a.dz = dz; a.y = y; a.argmax = argmax;
@@ -1652,6 +1697,7 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
   const dim3 grid((unsigned)(a.g.B * a.g.nbands));
+  if (a.tail.on && !cpv_bwd_ok(a)) return -2;                 // only the VALU family runs the tail
   if (cpv_bwd_ok(a)) {
     static bool vattr = hipFuncSetAttribute((const void*)cpv_bwd_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)CP_LDS_MAX) == hipSuccess &&

@@ -106,30 +106,18 @@ __device__ __forceinline__ void dd_wave_range(int k0, int k1, int& a, int& b) {
 struct DDFwd {
   const float* x; const float* w; const float* bias; float* y;
   int M, N, K, act; float alpha; int ksplit, kper;   // kper: K per workgroup (multiple of 8)
-  BNRef bn;          // bn.slab != null: A = act(x * a[c] + b[c]), c = k % C (tables from the slab)
-  float* xt;         // != null (with bn): the N-tile-0 workgroups store the transformed A
-  const float* tab;  // != null (with bn): precomputed [mean | rstd | a | b][C] instead of the slab
 };
 
-constexpr int DD_KEEP = 2;       // transformed-input blocks a lane holds until after the K loop
-
-__device__ __forceinline__ void dd_store_xt(const DDFwd& a, int m0, int i, int k, float4 va, float4 vb) {
-  if (m0 + i < a.M) *reinterpret_cast<float4*>(a.xt + (long)(m0 + i) * a.K + k) = va;
-  if (m0 + 32 + i < a.M) *reinterpret_cast<float4*>(a.xt + (long)(m0 + 32 + i) * a.K + k) = vb;
-}
-
-template <bool V4, bool BN>
+// (Applying a producer's BatchNorm while loading A — from its statistic slab, or from a
+// table the conv pair's last workgroup folded — was measured slower than the separate
+// bn_act_apply launch both times: profiles/r2_dense_direct.md, profiles/r3_notes.md.)
+template <bool V4>
 __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
   __shared__ float s_red[DD_WAVES * 32 * 64];
-  __shared__ float s_bn[BN ? 6 * DD_MAXC : 1];
   DD_STAMP(0);
   DD_SPAN_BEGIN();
-  // BatchNorm(+act) applied while loading A: the tables come from the producer's slab, and
-  // the workgroups of N-tile 0 write the transformed input once for the backward pass —
-  // the separate bn_act_apply launch (and its kernel boundary) disappears
   const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
   const int nt = blockIdx.x, mb = blockIdx.y, ks = blockIdx.z;
-  const FastDiv dC(BN ? a.bn.C : 1);
   const int n0 = nt * 32, m0 = mb * 64;
   const int kg0 = ks * a.kper, kg1 = min(a.K, kg0 + a.kper);
   int ka, kb;
@@ -165,18 +153,7 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
       for (int s = 0; s < 4; ++s) bw[u][s] = a.w[(long)min(kk + s, a.K - 1) * a.N + n];
     }
   };
-  float4 kx[DD_KEEP], ky[DD_KEEP];
-  int kk_[DD_KEEP], nkeep = 0;
-  load(ka);                        // the first group's loads overlap the BN-table reduction
-  if (BN && a.tab) {
-    for (int c = threadIdx.x; c < a.bn.C; c += DD_THREADS) {
-      s_bn[2 * DD_MAXC + c] = a.tab[2 * a.bn.C + c];
-      s_bn[3 * DD_MAXC + c] = a.tab[3 * a.bn.C + c];
-    }
-  } else if (BN) {
-    bn_reduce_to_lds(a.bn, s_bn, s_bn + DD_MAXC, s_bn + 2 * DD_MAXC, s_bn + 3 * DD_MAXC, s_bn + 4 * DD_MAXC);
-  }
-  if (BN) __syncthreads();
+  load(ka);
   dd_f32x16 acc0 = {}, acc1 = {};
   for (int k = ka; k < kb; k += 8 * DD_U) {
     if (k != ka) load(k);
@@ -187,28 +164,15 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) dd_pin(bw[u][s]);
     }
-    // the group's transform first (all table reads of the group issued together, then
-    // the activation), the MFMA chain after it: a table read -> MFMA pairing left every
-    // MFMA waiting on its own LDS round trip
+    // the group's activation first, the MFMA chain after it
     float ta_[DD_U][4], tb_[DD_U][4];
 #pragma unroll
-    for (int u = 0; u < DD_U; ++u) {
-      const int kk0 = k + 8 * u + 4 * h;
-      int q_, c = 0;
-      if (BN) dC.divmod(min(kk0, a.K - 1), q_, c);
+    for (int u = 0; u < DD_U; ++u)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        float xa_s = dd_c(pa[u], s), xb_s = dd_c(pb[u], s);
-        if (BN) {
-          const float sa = s_bn[2 * DD_MAXC + c], sb = s_bn[3 * DD_MAXC + c];
-          xa_s = xa_s * sa + sb;
-          xb_s = xb_s * sa + sb;
-          c = c + 1 == a.bn.C ? 0 : c + 1;
-        }
-        ta_[u][s] = xa_s;
-        tb_[u][s] = xb_s;
+        ta_[u][s] = dd_c(pa[u], s);
+        tb_[u][s] = dd_c(pb[u], s);
       }
-    }
     if (a.act != ACT_NONE) {
 #pragma unroll
       for (int u = 0; u < DD_U; ++u)
@@ -230,24 +194,8 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
         acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[s] * vA, b, acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(tb[s] * vB, b, acc1, 0, 0, 0);
       }
-      // xt: 8-k block j is written by the N-tile j % ntiles (writes spread over the
-      // workgroups that loaded it anyway); kept in registers and stored after the K loop,
-      // because a store issued between loads holds up every later load (vmcnt is in order)
-      const int blk = (k + 8 * u) >> 3;
-      if (BN && a.xt && blk % (int)gridDim.x == nt && kk0 + 3 < kb) {
-        if (nkeep < DD_KEEP) {
-          kx[nkeep] = make_float4(ta[0], ta[1], ta[2], ta[3]);
-          ky[nkeep] = make_float4(tb[0], tb[1], tb[2], tb[3]);
-          kk_[nkeep++] = kk0;
-        } else {
-          dd_store_xt(a, m0, i, kk0, make_float4(ta[0], ta[1], ta[2], ta[3]), make_float4(tb[0], tb[1], tb[2], tb[3]));
-        }
-      }
     }
   }
-#pragma unroll
-  for (int q = 0; q < DD_KEEP; ++q)
-    if (q < nkeep) dd_store_xt(a, m0, i, kk_[q], kx[q], ky[q]);
   DD_STAMP(1);
   const DDTile t = dd_reduce(s_red, acc0, acc1);
   DD_STAMP(2);
@@ -538,46 +486,16 @@ CSA_API int csa_dd_fwd_splits(int M, int N, int K) {
 }
 
 // Y[M][N] (+)= act(X)[M][K] . W[K][N] + bias.  Y must be zeroed when splits > 1.
-CSA_API int csa_dd_fwd_bn(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
-                          int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
-                          float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, hipStream_t st);
-
 CSA_API int csa_dd_fwd(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
                        int act, float alpha, hipStream_t st) {
-  return csa_dd_fwd_bn(X, W, bias, Y, M, N, K, act, alpha, nullptr, 0, 0, 0.f, 0.f, nullptr, nullptr, nullptr, st);
-}
-
-// ... with the forward input transform act(bn(x)) applied while loading (C <= 128, K % 4
-// == 0); xt (optional) receives the transformed input [M][K].
-CSA_API int csa_dd_fwd_bn2(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
-                           int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
-                           float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, const float* tab,
-                           hipStream_t st);
-
-CSA_API int csa_dd_fwd_bn(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
-                          int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
-                          float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, hipStream_t st) {
-  return csa_dd_fwd_bn2(X, W, bias, Y, M, N, K, act, alpha, bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale,
-                        bn_offset, xt, nullptr, st);
-}
-
-// ... tab != null: the BatchNorm table [mean | rstd | a | b][C] was precomputed by the
-// producer (the conv pair's last workgroup): no slab reduction in any workgroup.
-CSA_API int csa_dd_fwd_bn2(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
-                           int act, float alpha, const float* bn_slab, int bn_nslab, int bn_C, float bn_count,
-                           float bn_eps, const float* bn_scale, const float* bn_offset, float* xt, const float* tab,
-                           hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
-  if (bn_slab && (bn_C <= 0 || bn_C > DD_MAXC || K % 4)) return -1;
   const int nt = (N + 31) / 32, mb = (M + 63) / 64;
   int ks = dd_splits(nt * mb, K);
   const int kper = dd_kper(K, ks);
   ks = (K + kper - 1) / kper;
-  DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper,
-          BNRef{bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset}, xt, bn_slab ? tab : nullptr};
-  if (bn_slab) hipLaunchKernelGGL((dd_fwd_kernel<true, true>), dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
-  else if (K % 4 == 0) hipLaunchKernelGGL((dd_fwd_kernel<true, false>), dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
-  else hipLaunchKernelGGL((dd_fwd_kernel<false, false>), dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
+  DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper};
+  if (K % 4 == 0) hipLaunchKernelGGL(dd_fwd_kernel<true>, dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
+  else hipLaunchKernelGGL(dd_fwd_kernel<false>, dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
   return (int)hipGetLastError();
 }
 

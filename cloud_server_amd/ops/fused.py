@@ -67,9 +67,14 @@ _SIGS = {
     "csa_cp_debug": (I, [P]),
     "csa_head_debug": (I, [P]),
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P]),
-    "csa_conv_pair_fwd2": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P, P, P, P, F, F, P]),
-    "csa_conv_pair_tab_ok": (I, [P]),
+    "csa_conv_pair_valu_ok": (I, [P]),
     "csa_conv_pair_grid": (I, [P]),
+    "csa_conv_pair_tail_ok": (I, [P]),
+    "csa_conv_pair_tail_size": (I, []),
+    "csa_conv_pair_bwd2": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
+                               P, P, P, P, I, P, P]),
+    "csa_dense_bwd_update_head2": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
+                                       P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, I, F, P, P]),
     "csa_set_deterministic": (None, [I]),
     "csa_deterministic": (I, []),
     "csa_rows_fold": (I, [P, L, I, L, P, I, P]),
@@ -86,8 +91,6 @@ _SIGS = {
     "csa_dd_debug": (I, [P]),
     "csa_dd_fwd_splits": (I, [I, I, I]),
     "csa_dd_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
-    "csa_dd_fwd_bn": (I, [P, P, P, P, I, I, I, I, F, P, I, I, F, F, P, P, P, P]),
-    "csa_dd_fwd_bn2": (I, [P, P, P, P, I, I, I, I, F, P, I, I, F, F, P, P, P, P, P]),
     "csa_dd_dgrad_splits": (I, [I, I, I]),
     "csa_dd_dgrad_slabs": (I, []),
     "csa_dd_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P]),
