@@ -24,7 +24,6 @@
 // (uint8 dataset rows gathered through the batch index stream).  Everything else uses the
 // per-layer kernels (conv.hip).
 #include "common.h"
-#include "optim_common.h"
 #include <cstdlib>
 #include <algorithm>
 
@@ -438,25 +437,6 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a) 
 
 // --------------------------------------------------------------------------------------
 // Backward.
-// The step's tail inside the pair backward (VALU family, one-GPU program without an
-// optimizer launch).  Every workgroup zeroes a slice of the ``zs`` regions (accumulators
-// nobody reads after the pair); the LAST workgroup to finish (arrival ticket) folds the
-// weight-gradient stripes in fixed order and applies the optimizer update to the pair's
-// parameters and the BatchNorm scale / offset (whose gradients every workgroup already
-// holds in LDS), zeroes the stripes and the ``zl`` regions (statistic slabs every
-// workgroup read in its prologue) and advances the batch cursor.
-constexpr int CPT_MAXZ = 4;
-constexpr int CPT_MAXS = 16;
-struct CPTail {
-  int on, opt; float lr; const int64_t* step;
-  float* w; float* s0; float* s1;                 // flat parameters and optimizer slots
-  long offA, offbA, offB, offbB, offS, offO;       // flat offsets (-1: absent)
-  float* zs[CPT_MAXZ]; long zsn[CPT_MAXZ]; int nzs;
-  float* zl[CPT_MAXZ]; long zln[CPT_MAXZ]; int nzl;
-  int64_t* cursor; long wrap;
-  unsigned* cnt;
-};
-
 struct CPBwdArgs {
   CPGeom g;
   const uint8_t* img; const int64_t* idx; const int64_t* cursor;
@@ -468,7 +448,6 @@ struct CPBwdArgs {
   BNRef bn; int bn_on; const float* bwd_slab; int bwd_nslab;
   float* dscale; float* doffset; float* run_mean; float* run_var; float momentum;
   float* dwA; float* dbA; float* dwB; float* dbB; int stripes;
-  CPTail tail;
 };
 
 // LDS carve of the backward (float offsets), shared by the kernel and the host size check.
@@ -1122,74 +1101,6 @@ __host__ __device__ inline CPVBwdLds cpv_bwd_lds(const CPGeom& g, const CPVBwdTi
   return L;
 }
 
-// The step's tail (see CPTail).  s_bn holds this workgroup's folded BatchNorm-backward
-// sums: [3 ld + c] = sum dz (offset gradient), [4 ld + c] = sum dz xhat (scale gradient).
-__device__ __forceinline__ void cpv_tail(const CPBwdArgs& a, const float* s_bn, int ld) {
-  const CPTail& T = a.tail;
-  const CPGeom& g = a.g;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  // (1) this workgroup's slice of the shared zero regions
-  for (int z = 0; z < T.nzs; ++z) {
-    const long n = T.zsn[z], per = (n + gridDim.x - 1) / gridDim.x, lo = (long)blockIdx.x * per;
-    const long hi = lo + per < n ? lo + per : n;
-    for (long i = lo + tid; i < hi; i += nt) T.zs[z][i] = 0.f;
-  }
-  // (2) arrival ticket: every stripe atomic of this workgroup is performed (device scope,
-  // beyond every L2) before the ticket; the last workgroup reads the stripes with
-  // agent-scope loads
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(T.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == gridDim.x - 1;
-    if (s_last) __hip_atomic_store(T.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       // compiler-only: loads stay below
-  const float lr = opt_step_lr(T.opt, T.lr, T.step);
-  const int ns = opt_nslots(T.opt);
-  const int KA = g.KAh * g.KAw * g.C0, KB = g.KBh * g.KBw * g.C1;
-  const int nA = KA * g.C1, nbA = T.offbA >= 0 ? g.C1 : 0, nB = KB * g.C2, nbB = T.offbB >= 0 ? g.C2 : 0;
-  const int nS = T.offS >= 0 ? g.C2 : 0;
-  const int total = nA + nbA + nB + nbB + 2 * nS;
-  const int S = a.stripes;
-  for (int e = tid; e < total; e += nt) {
-    float* src = nullptr; long ld = 0, off; int i = e;
-    float gv = 0.f;
-    if (i < nA) { src = a.dwA; ld = nA; off = T.offA; }
-    else if ((i -= nA) < nbA) { src = a.dbA; ld = g.C1; off = T.offbA; }
-    else if ((i -= nbA) < nB) { src = a.dwB; ld = nB; off = T.offB; }
-    else if ((i -= nB) < nbB) { src = a.dbB; ld = g.C2; off = T.offbB; }
-    else if ((i -= nbB) < nS) { gv = s_bn[4 * ld + i]; off = T.offS; }
-    else { i -= nS; gv = s_bn[3 * ld + i]; off = T.offO; }
-    if (src) {                                                  // stripes in fixed order
-      float v[CPT_MAXS];
-#pragma unroll
-      for (int q = 0; q < CPT_MAXS; ++q)
-        v[q] = q < S ? __hip_atomic_load(src + (long)q * ld + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-#pragma unroll
-      for (int q = 0; q < CPT_MAXS; ++q) gv += v[q];
-#pragma unroll
-      for (int q = 0; q < CPT_MAXS; ++q)
-        if (q < S) src[(long)q * ld + i] = 0.f;                  // the next step accumulates again
-    }
-    const long p = off + i;
-    float w = T.w[p], s0 = ns >= 1 ? T.s0[p] : 0.f, s1 = ns >= 2 ? T.s1[p] : 0.f;
-    opt_update(T.opt, lr, w, gv, s0, s1);
-    T.w[p] = w;
-    if (ns >= 1) T.s0[p] = s0;
-    if (ns >= 2) T.s1[p] = s1;
-  }
-  for (int z = 0; z < T.nzl; ++z)
-    for (long j = tid; j < T.zln[z]; j += nt) T.zl[z][j] = 0.f;
-  if (tid == 0 && T.cursor) {
-    const int64_t c = *T.cursor + 1;
-    *T.cursor = (T.wrap > 0 && c >= T.wrap) ? 0 : c;
-  }
-}
-
 template <int KBH, int KBW>
 __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
   const CPGeom& g = a.g;
@@ -1484,7 +1395,6 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
     }
   }
   CP_STAMP(13);
-  if (a.tail.on) cpv_tail(a, s_bn, CPV_MAXC2);
 }
 
 static bool cpv_ok(const CPGeom& g) {
@@ -1641,14 +1551,6 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
   return (int)hipGetLastError();
 }
 
-CSA_API int csa_conv_pair_bwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
-                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
-                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
-                               const float* bn_slab, int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                               const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
-                               float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
-                               float* dwB, float* dbB, int stripes, const CPTail* tail, hipStream_t st);
-
 CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
@@ -1656,34 +1558,7 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
                               const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
                               float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
                               float* dwB, float* dbB, int stripes, hipStream_t st) {
-  return csa_conv_pair_bwd2(geom, img, idx, cursor, wA, bA, actA, alphaA, wB, hasBiasB, actB, alphaB, dz, y, argmax,
-                            bn_slab, bn_nslab, bn_count, bn_eps, bn_scale, bn_offset, bwd_slab, bwd_nslab, dscale,
-                            doffset, run_mean, run_var, momentum, dwA, dbA, dwB, dbB, stripes, nullptr, st);
-}
-
-// Does the pair backward run the step's tail (optimizer of the pair + BN parameters,
-// zeroing, cursor) for geom?  Only the VALU family does.
-CSA_API int csa_conv_pair_tail_ok(const int* geom) {
-  CPGeom g;
-  return cp_geom(geom, g) && cpv_ok(g) ? 1 : 0;
-}
-
-// tail: the step's tail descriptor (null: none) — {on, opt, lr, step, w, s0, s1, 6 flat
-// offsets, shared zero regions, last-workgroup zero regions, cursor, wrap, ticket}
-CSA_API int csa_conv_pair_tail_size() { return (int)sizeof(CPTail); }
-
-CSA_API int csa_conv_pair_bwd2(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
-                              const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
-                              int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
-                              const float* bn_slab, int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
-                              const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
-                              float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
-                              float* dwB, float* dbB, int stripes, const CPTail* tail, hipStream_t st) {
   CPBwdArgs a{};
-  if (tail && tail->on) {
-    a.tail = *tail;
-    if (!a.tail.cnt || !a.tail.w || a.tail.nzs > CPT_MAXZ || a.tail.nzl > CPT_MAXZ || stripes > CPT_MAXS) return -2;
-  }
   if (!cp_geom(geom, a.g) || cp_lds(a.g, true) > CP_LDS_MAX) return -1;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.actB = actB; a.alphaB = alphaB; a.hasBiasB = hasBiasB; a.dz = dz; a.y = y; a.argmax = argmax;
@@ -1697,7 +1572,6 @@ CSA_API int csa_conv_pair_bwd2(const int* geom, const uint8_t* img, const int64_
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
   const dim3 grid((unsigned)(a.g.B * a.g.nbands));
-  if (a.tail.on && !cpv_bwd_ok(a)) return -2;                 // only the VALU family runs the tail
   if (cpv_bwd_ok(a)) {
     static bool vattr = hipFuncSetAttribute((const void*)cpv_bwd_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)CP_LDS_MAX) == hipSuccess &&

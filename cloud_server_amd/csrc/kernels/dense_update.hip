@@ -80,10 +80,7 @@ struct DUArgs {
   // gradient for its share of the N features, one block the bias gradient and metrics
   const float* hy;          // [M][N] (null: no head epilogue)
   const float* hdl;         // [M][10] dlogits (scaled)
-  float* hgw; float* hgb;   // dWh [N][10], dbh [10] (plain stores into the flat gradient) ...
-  // ... or (hw != null: one-GPU program without an optimizer launch) the optimizer update of
-  // the head parameters in place, with their slots (same layout as hw / hb)
-  float* hw; float* hb; float* hs0w; float* hs1w; float* hs0b; float* hs1b;
+  float* hgw; float* hgb;   // dWh [N][10], dbh [10] (plain stores into the flat gradient)
   const float* hrl; const int* hrc;   // [M] per-row loss / correct
   float* ring_loss; int* ring_correct; int ring; float ldiv;
   int hact; float halpha;   // the head's input transform: the head reads act(hy)
@@ -163,20 +160,8 @@ __device__ __forceinline__ void du_head_prefetch(const DUArgs& a, int grp, int g
   for (int u = 0; u < 3; ++u) h.dl[u] = a.hdl[min(t + u * THREADS, n10 - 1)];
 }
 
-// dWh / dbh element idx: stored as a gradient, or applied to the head parameter in place
-__device__ __forceinline__ void du_head_out(const DUArgs& a, float lr, float* g, float* w, float* s0, float* s1,
-                                            long idx, float v) {
-  if (!a.hw) { g[idx] = v; return; }
-  const int ns = opt_nslots(a.opt);
-  float wv = w[idx], a0 = ns >= 1 ? s0[idx] : 0.f, a1 = ns >= 2 ? s1[idx] : 0.f;
-  opt_update(a.opt, lr, wv, v, a0, a1);
-  w[idx] = wv;
-  if (ns >= 1) s0[idx] = a0;
-  if (ns >= 2) s1[idx] = a1;
-}
-
 template <int THREADS>
-__device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float* s_hw, float lr) {
+__device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float* s_hw) {
   // s_hw: [64][DU_HMAXR] act(hy) | [64][10] dl
   const int t = threadIdx.x, M = a.M;
   float* s_y = s_hw;
@@ -197,7 +182,7 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
     } else {
       for (int m = 0; m < M; ++m) v = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), s_d[m * DU_HNC + j], v);
     }
-    du_head_out(a, lr, a.hgw, a.hw, a.hs0w, a.hs1w, (long)n * DU_HNC + j, v);
+    a.hgw[(long)n * DU_HNC + j] = v;
   }
   if (blockIdx.x == gridDim.x - 1) {                      // dbh and the step's metrics
     const int lane = t & 63, w = t >> 6;
@@ -205,7 +190,7 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
       if (lane < DU_HNC) {
         float v = 0.f;
         for (int m = 0; m < M; ++m) v += s_d[m * DU_HNC + lane];
-        du_head_out(a, lr, a.hgb, a.hb, a.hs0b, a.hs1b, lane, v);
+        a.hgb[lane] = v;
       }
     } else if (w == 1) {
       float l = lane < M ? a.hrl[lane] : 0.f;
@@ -421,7 +406,7 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
     }
   }
   DU_STAMP(3);
-  if (HEAD) du_head_finish<THREADS>(a, hd, s_hw, lr);
+  if (HEAD) du_head_finish<THREADS>(a, hd, s_hw);
   if (!dgrad) {                                            // uniform: first layer
     du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
     return;
@@ -613,16 +598,6 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
                                       const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
                                       int hact, float halpha, hipStream_t st);
 
-CSA_API int csa_dense_bwd_update_head2(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
-                                       const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
-                                       int bn_C, float bn_count, float bn_eps, const float* bn_scale,
-                                       const float* bn_offset, float* bwd_slab, const float* Xw, int opt, float lr,
-                                       const int64_t* step, float* s0w, float* s1w, float* s0b, float* s1b,
-                                       float scale, const float* bn_tab, float* part, unsigned* cnt,
-                                       const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
-                                       const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
-                                       int hact, float halpha, float* const* hupd, hipStream_t st);
-
 CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
                                  const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
                                  int bn_C, float bn_count, float bn_eps, const float* bn_scale,
@@ -646,23 +621,6 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
                                       const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
                                       const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
                                       int hact, float halpha, hipStream_t st) {
-  return csa_dense_bwd_update_head2(dY, W, bias, dX, M, K, N, x_fwd, act, alpha, bn_slab, bn_nslab, bn_C, bn_count,
-                                    bn_eps, bn_scale, bn_offset, bwd_slab, Xw, opt, lr, step, s0w, s1w, s0b, s1b,
-                                    scale, bn_tab, part, cnt, hy, hdl, hgw, hgb, hrl, hrc, ring_loss, ring_correct,
-                                    ring, ldiv, hact, halpha, nullptr, st);
-}
-
-// ... hupd != null: {hw, hb, hs0w, hs1w, hs0b, hs1b} — the head's optimizer update applied in
-// the epilogue (no head gradient in memory; the one-GPU program without an optimizer launch)
-CSA_API int csa_dense_bwd_update_head2(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
-                                 const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
-                                 int bn_C, float bn_count, float bn_eps, const float* bn_scale,
-                                 const float* bn_offset, float* bwd_slab, const float* Xw, int opt, float lr,
-                                 const int64_t* step, float* s0w, float* s1w, float* s0b, float* s1b,
-                                 float scale, const float* bn_tab, float* part, unsigned* cnt,
-                                      const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
-                                      const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
-                                      int hact, float halpha, float* const* hupd, hipStream_t st) {
   if (!csa_dense_bwd_update_ok(M, K, N, bn_slab ? bn_C : 0)) return -1;
   if (hy && (!hdl || !hgw || !hgb || !hrl || !hrc || !ring_loss || !ring_correct || ring < 1 || !step)) return -2;
   if (!Xw || !W || !dY) return -2;
@@ -679,11 +637,6 @@ CSA_API int csa_dense_bwd_update_head2(const float* dY, float* W, float* bias, f
   a.hy = hy; a.hdl = hdl; a.hgw = hgw; a.hgb = hgb; a.hrl = hrl; a.hrc = hrc;
   a.ring_loss = ring_loss; a.ring_correct = ring_correct; a.ring = ring; a.ldiv = ldiv;
   a.hact = hact; a.halpha = halpha;
-  if (hupd) {
-    a.hw = hupd[0]; a.hb = hupd[1]; a.hs0w = hupd[2]; a.hs1w = hupd[3]; a.hs0b = hupd[4]; a.hs1b = hupd[5];
-    const int ns = opt_nslots(opt);
-    if (!a.hw || !a.hb || (ns >= 1 && (!a.hs0w || !a.hs0b)) || (ns >= 2 && (!a.hs1w || !a.hs1b)) || !hy) return -2;
-  }
   if (a.cs > 1 && dX && (!part || !cnt)) return -2;
   const int blocks = groups * a.cs;
   const int ns = opt_nslots(opt);

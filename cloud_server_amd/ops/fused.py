@@ -69,12 +69,6 @@ _SIGS = {
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P]),
     "csa_conv_pair_valu_ok": (I, [P]),
     "csa_conv_pair_grid": (I, [P]),
-    "csa_conv_pair_tail_ok": (I, [P]),
-    "csa_conv_pair_tail_size": (I, []),
-    "csa_conv_pair_bwd2": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
-                               P, P, P, P, I, P, P]),
-    "csa_dense_bwd_update_head2": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
-                                       P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, I, F, P, P]),
     "csa_set_deterministic": (None, [I]),
     "csa_deterministic": (I, []),
     "csa_rows_fold": (I, [P, L, I, L, P, I, P]),

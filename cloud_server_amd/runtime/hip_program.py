@@ -102,20 +102,8 @@ class Unit:
     norm: Optional[LayerPlan] = None        # bn unit: the norm layer (None: activation only)
 
 
-class _CPTail(C.Structure):
-    """conv_pair.hip ``CPTail`` (the step's tail inside the pair backward)."""
-    _fields_ = [("on", C.c_int), ("opt", C.c_int), ("lr", C.c_float), ("step", C.c_void_p),
-                ("w", C.c_void_p), ("s0", C.c_void_p), ("s1", C.c_void_p),
-                ("offA", C.c_long), ("offbA", C.c_long), ("offB", C.c_long), ("offbB", C.c_long),
-                ("offS", C.c_long), ("offO", C.c_long),
-                ("zs", C.c_void_p * 4), ("zsn", C.c_long * 4), ("nzs", C.c_int),
-                ("zl", C.c_void_p * 4), ("zln", C.c_long * 4), ("nzl", C.c_int),
-                ("cursor", C.c_void_p), ("wrap", C.c_long), ("cnt", C.c_void_p)]
-
-
 class HipProgram:
     WGRAD_STRIPES = 16
-    tail = None               # _CPTail of the step tail (None: the optimizer launch runs)
 
     def __init__(self, eng, forward_only: bool = False):
         """``forward_only``: the serving program (``serve.hip_infer``) — the same forward
@@ -172,7 +160,6 @@ class HipProgram:
         self.zero_regions: List[torch.Tensor] = []
         self._collect_zero_regions()
         self._zero_now()
-        self._plan_tail()
         self._plan_stage()
         self._plan_grad_buckets()
         self.opt_segments = self._opt_segments()
@@ -769,69 +756,6 @@ class HipProgram:
             r.zero_()
         self.e.flat_grad.zero_()
 
-    # ------------------------------------------------------------------ step tail
-    def _plan_tail(self) -> None:
-        """One-GPU fused program without an optimizer launch.  Every parameter is then
-        updated by the kernel that completes its gradient: the dense layers by their fused
-        backward (dense_update.hip), the head by the last dense layer's head epilogue, and
-        the conv pair's weights / biases and the following BatchNorm's scale / offset by the
-        LAST workgroup of the pair backward (conv_pair.hip ``cpv_tail``: fixed-order stripe
-        fold + update), which also zeroes the step's accumulators and advances the batch
-        cursor.  The pair backward ends the step: one launch less on the critical path.
-        (The batch is then read through the cursor: no staging launch to host it.)"""
-        e = self.e
-        self.tail = None
-        if (not self.fused or self.det or e.ctx.enabled or self.pair is None or not self.head_row
-                or os.environ.get("CSA_STEP_TAIL", "1") != "1"
-                or not self.lib.csa_conv_pair_tail_ok(K.ints(self.pair))):
-            return
-        if any(u.kind != "dense" or not u.fused for u in self.units[2:]):
-            return
-        ua, ub = self.units[0], self.units[1]
-        if ua.wg_stripes > 16 or ub.wg_stripes > 16 or ua.wg_stripes != ub.wg_stripes:
-            return
-        nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
-        late = set()
-        if nt.has_bn:
-            late = {nt.slab.data_ptr(), nt.bwd_slab.data_ptr()}
-        zs = [r for r in self.zero_regions + self.zero_early if r.data_ptr() not in late]
-        zl = [r for r in self.zero_regions + self.zero_early if r.data_ptr() in late]
-        if len(zs) > 4 or len(zl) > 4:
-            return
-        offs = self.model.state.offsets
-        if C.sizeof(_CPTail) != self.lib.csa_conv_pair_tail_size():
-            raise RuntimeError("CPTail layout mismatch between hip_program.py and conv_pair.hip")
-        t = _CPTail()
-        t.on, t.opt, t.lr, t.step = 1, e.opt_id, float(e.lr), e.dstep.data_ptr()
-        t.w = e.flat.data_ptr()
-        t.s0 = e.slots[0].data_ptr() if e.slots.shape[0] > 0 else None
-        t.s1 = e.slots[1].data_ptr() if e.slots.shape[0] > 1 else None
-        t.offA, t.offB = offs[f"{ua.layer.name}.weight"], offs[f"{ub.layer.name}.weight"]
-        t.offbA = offs[f"{ua.layer.name}.bias"] if ua.layer.spec.bias else -1
-        t.offbB = offs[f"{ub.layer.name}.bias"] if ub.layer.spec.bias else -1
-        t.offS = offs[f"{nt.norm.name}.scale"] if nt.has_bn else -1
-        t.offO = offs[f"{nt.norm.name}.offset"] if nt.has_bn else -1
-        for i, r in enumerate(zs):
-            t.zs[i], t.zsn[i] = r.data_ptr(), r.numel()
-        t.nzs = len(zs)
-        for i, r in enumerate(zl):
-            t.zl[i], t.zln[i] = r.data_ptr(), r.numel()
-        t.nzl = len(zl)
-        t.cursor, t.wrap = e.stream.cursor.data_ptr(), e.stream.wrap
-        self.tail_cnt = torch.zeros(1, dtype=torch.int32, device=e.device)
-        t.cnt = self.tail_cnt.data_ptr()
-        self.tail = t
-        self.tail_regions = zs + zl          # keep the tensors alive with the descriptor
-        # the head's update runs in the last dense layer's head epilogue
-        V, sl = self.views, e.slots
-        ow, ob = offs["head.weight"], offs["head.bias"]
-        s0 = sl[0] if sl.shape[0] > 0 else None
-        s1 = sl[1] if sl.shape[0] > 1 else None
-        self.head_upd = (C.c_void_p * 6)(
-            V["head.weight"].data_ptr(), V["head.bias"].data_ptr(),
-            s0[ow:].data_ptr() if s0 is not None else None, s1[ow:].data_ptr() if s1 is not None else None,
-            s0[ob:].data_ptr() if s0 is not None else None, s1[ob:].data_ptr() if s1 is not None else None)
-
     # ------------------------------------------------------------------ batch staging
     def _plan_stage(self) -> None:
         """Stage each step's batch at fixed addresses (one-GPU fused program).  The head
@@ -849,7 +773,6 @@ class HipProgram:
         img = e.data.images
         imsz = img[0].numel() if img.dim() > 1 else 0
         self.staged = (self.pair is not None and bool(self.head_rg or self.head_row) and img.dtype == torch.uint8
-                       and self.tail is None
                        and imsz % 4 == 0 and os.environ.get("CSA_STAGE_BATCH", "1") == "1")
         self.stage_img = self.stage_lbl = None
         if self.staged:
@@ -1094,8 +1017,7 @@ class HipProgram:
                 main.wait_stream(self.lr_side)
         else:
             e.after_backward_sync()
-        if self.tail is None:          # otherwise every update ran inside its producer
-            self._optimizer(st)
+        self._optimizer(st)
 
     # ------------------------------------------------------------------ forward
     _eval_bn = False          # predict: BN with running statistics (no batch-stat slabs)
@@ -1325,7 +1247,7 @@ class HipProgram:
             rm = getattr(self.model, f"bn{nt.norm.index}_mean")
             rv = getattr(self.model, f"bn{nt.norm.index}_var")
         simg, srows, scur = self._batch_src()
-        self._rc(lib.csa_conv_pair_bwd2(
+        self._rc(lib.csa_conv_pair_bwd(
             K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
             K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
             _act_id(ua.act), _alpha(ua.act), K.ptr(V[f"{ub.layer.name}.weight"]), 1 if ub.layer.spec.bias else 0,
@@ -1334,8 +1256,7 @@ class HipProgram:
             K.ptr(dsc), K.ptr(dof), K.ptr(rm), K.ptr(rv), float(self.model.bn_momentum),
             K.ptr(ua.dw_acc), K.ptr(ua.db_acc) if ua.layer.spec.bias else None,
             K.ptr(ub.dw_acc), K.ptr(ub.db_acc) if ub.layer.spec.bias else None,
-            min(ua.wg_stripes, ub.wg_stripes), C.addressof(self.tail) if self.tail is not None else None, st),
-            "conv_pair_bwd")
+            min(ua.wg_stripes, ub.wg_stripes), st), "conv_pair_bwd")
         self._sync_bn_param_grads(nt)
         if self.det:
             for u in (ua, ub):
@@ -1443,15 +1364,14 @@ class HipProgram:
                     _act_id(self.head_tf.act), _alpha(self.head_tf.act))
         else:
             head = (None, None, None, None, None, None, None, None, 1, 1.0, 0, 0.0)
-        self._rc(lib.csa_dense_bwd_update_head2(
+        self._rc(lib.csa_dense_bwd_update_head(
             K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
             K.ptr(prev.dy) if prev is not None else None, B, fin, fout,
             K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
             K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
             K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
             K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
-            1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), *head,
-            self.head_upd if (self.tail is not None and head[0] is not None) else None, st),
+            1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), *head, st),
             "dense_bwd_update")
         if self.det and tf.has_bn:
             self._det_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],

@@ -290,7 +290,6 @@ def test_staged_batch_matches_cursor_path(monkeypatch):
     # so a near-zero gradient's rounding can flip a whole step)
     cfg = _cfg(CASES["sample"], optimizer="GradientDescentOptimizer", lr=0.001)
     outs = []
-    monkeypatch.setenv("CSA_STEP_TAIL", "0")      # staging lives in the optimizer launch
     for staged in ("0", "1"):
         monkeypatch.setenv("CSA_STAGE_BATCH", staged)
         eng = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True, stream_chunk=4)
@@ -328,38 +327,5 @@ def test_run_steps_groups_equal_single_steps(monkeypatch):
     assert int(a.dstep.item()) == int(b.dstep.item()) == 18
     assert int(a.stream.cursor.item()) == int(b.stream.cursor.item())
     assert (a.flat - b.flat).abs().max().item() < 1e-3
-    ma, mb = a.metrics_since(0), b.metrics_since(0)
-    assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
-
-
-@pytest.mark.parametrize("opt", ["AdagradOptimizer", "AdamOptimizer", "GradientDescentOptimizer", "AdadeltaOptimizer"])
-def test_step_tail_matches_optimizer_launch(monkeypatch, opt):
-    """One-GPU fused program without an optimizer launch (the pair backward's last
-    workgroup updates the pair + BatchNorm parameters, zeroes the accumulators and moves
-    the cursor; the head update rides in the last dense layer's epilogue) == the program
-    with the optimizer launch: parameters, slots, metrics, cursor and step counter."""
-    ds = synthetic_mnist(700, seed=31)
-    cfg = _cfg(CASES["sample"], optimizer=opt, lr=1e-3 if opt != "GradientDescentOptimizer" else 1e-2)
-    engs = []
-    for tail in ("1", "0"):
-        monkeypatch.setenv("CSA_STEP_TAIL", tail)
-        e = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True, stream_chunk=5)
-        assert (e.program.tail is not None) == (tail == "1")
-        engs.append(e)
-    for e in engs:
-        e.step()
-        e.run_steps(12)
-    torch.cuda.synchronize()
-    a, b = engs
-    assert a.host_step == b.host_step == 13
-    assert int(a.dstep.item()) == int(b.dstep.item()) == 13
-    assert int(a.stream.cursor.item()) == int(b.stream.cursor.item())
-    diff = (a.flat - b.flat).abs()
-    if opt in ("AdamOptimizer", "AdadeltaOptimizer"):
-        # per-element normalised steps: a ~0 gradient's rounding can move its weight by ~lr
-        assert diff.max().item() <= 2 * 1e-3 * 13 + 1e-6
-        assert torch.quantile(diff[:1 << 24].float(), 0.999).item() < 1e-5
-    else:
-        assert diff.max().item() < 1e-3, f"{opt}: params differ by {diff.max().item()}"
     ma, mb = a.metrics_since(0), b.metrics_since(0)
     assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
