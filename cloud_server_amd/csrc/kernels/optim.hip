@@ -183,21 +183,23 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   OPT_STAMP(2);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (a.met.parts > 0) {
-      // all partials' loads in flight together (a serial load -> add loop is one memory
-      // round trip per partial on the critical path of the whole step)
-      float lv[MAXS];
-      int cv[MAXS];
-#pragma unroll
-      for (int p = 0; p < MAXS; ++p) {
-        const int pp = p < a.met.parts ? p : 0;
-        lv[p] = a.met.loss[pp];
-        cv[p] = a.met.corr[pp];
-      }
+      // MAXS partials' loads in flight together per round (a serial load -> add loop is one
+      // memory round trip per partial on the critical path of the whole step)
       float ls = 0.f;
       int nc = 0;
+      for (int p0 = 0; p0 < a.met.parts; p0 += MAXS) {
+        float lv[MAXS];
+        int cv[MAXS];
 #pragma unroll
-      for (int p = 0; p < MAXS; ++p)
-        if (p < a.met.parts) { ls += lv[p]; nc += cv[p]; }
+        for (int p = 0; p < MAXS; ++p) {
+          const int pp = p0 + p < a.met.parts ? p0 + p : 0;
+          lv[p] = a.met.loss[pp];
+          cv[p] = a.met.corr[pp];
+        }
+#pragma unroll
+        for (int p = 0; p < MAXS; ++p)
+          if (p0 + p < a.met.parts) { ls += lv[p]; nc += cv[p]; }
+      }
       const int pos = (int)((*a.step - 1) % a.met.ring);
       a.met.ring_loss[pos] = ls / a.met.div;
       a.met.ring_correct[pos] = nc;
@@ -283,7 +285,7 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
                             const int64_t* st_cursor, int st_B, long st_imsz, uint8_t* st_out_img,
                             int64_t* st_out_lbl, hipStream_t st) {
   if (st_out_img && (st_imsz % 4 || st_B <= 0)) return -1;
-  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG || met_parts > MAXS) return -1;
+  if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG) return -1;
   OptArgs a{};
   a.keep.count = nkeep;
   for (int i = 0; i < nkeep; ++i) {

@@ -331,6 +331,16 @@ class HipProgram:
                        and groups >= int(os.environ.get("CSA_FUSED_DENSE_MIN_GROUPS", "1")))
         self.head_rg = 0
         self.head_row = False
+        self.head_sep = False
+        if not self.fused and not self.forward_only and self.head_tf.norm is None:
+            # data parallel (or the unfused program): the row-per-workgroup head, its weight
+            # gradient as a register-direct wgrad launch (dWh = act(h)^T dlogits) into the flat
+            # gradient before the all-reduce, its metrics folded by the optimizer launch
+            # (the atomic 4-workgroup head took 15.6 us per DP step)
+            last = self.units[-1]
+            if (last.kind == "dense" and self.lib.csa_head_row_ok(B, last.layer.spec.hidden)
+                    and os.environ.get("CSA_HEAD_ROW", "1") == "1"):
+                self.head_row = self.head_sep = True
         if self.fused and self.head_tf.norm is None:
             last = self.units[-1]
             K = last.layer.spec.hidden if last.kind == "dense" else last.layer.out_shape.numel
@@ -695,9 +705,15 @@ class HipProgram:
                 # straight into the flat gradient (data parallelism, or beyond that budget)
                 nf = 1 + (1 if lp.spec.bias else 0)
                 S = 1 if self.e.ctx.enabled or fold_budget < nf else self.WGRAD_STRIPES
-                u.det_fold = self.det and self.pair is not None and k < 2
-                if u.det_fold:          # one stripe per pair workgroup, folded after the pair
-                    S = int(self.lib.csa_conv_pair_grid(_FK.ints(self.pair)))
+                # the conv pair's stripes are folded right after the pair backward (fixed-order
+                # csa_rows_fold into the flat gradient) in deterministic mode — one stripe per
+                # workgroup — and under data parallelism, where the gradient must be complete
+                # before its all-reduce (700 workgroups adding into ONE copy contend: the pair
+                # backward took 37 us instead of 25)
+                u.row_fold = self.pair is not None and k < 2 and (self.det or self.e.ctx.enabled)
+                if u.row_fold:
+                    S = (int(self.lib.csa_conv_pair_grid(_FK.ints(self.pair))) if self.det
+                         else self.WGRAD_STRIPES)
                 elif S > 1:
                     fold_budget -= nf
                 u.wg_stripes = S
@@ -871,6 +887,12 @@ class HipProgram:
                 None if staged else K.ptr(cur), 0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
                 K.ptr(last.dy), K.ptr(self.hdl), K.ptr(self.hrl), K.ptr(self.hrc), K.ptr(e.dstep),
                 K.ptr(cur) if staged else None, e.stream.wrap if staged else 0, st), "head_row")
+            if self.head_sep:
+                # dWh = act(h)^T dlogits, dbh = colsum(dlogits) into the flat gradient
+                self._rc(lib.csa_dd_wgrad(
+                    K.ptr(hin), K.ptr(self.hdl), B, hin.shape[1], 10, _act_id(self.head_tf.act),
+                    _alpha(self.head_tf.act), 1.0, K.ptr(G["head.weight"]), K.ptr(G["head.bias"]),
+                    None, None, None, None, None, None, -1, 0.0, None, st), "dd_wgrad(head)")
         elif self.head_rg:
             staged = getattr(self, "staged", False)
             self._rc(lib.csa_head_part2(
@@ -1258,7 +1280,7 @@ class HipProgram:
             K.ptr(ub.dw_acc), K.ptr(ub.db_acc) if ub.layer.spec.bias else None,
             min(ua.wg_stripes, ub.wg_stripes), st), "conv_pair_bwd")
         self._sync_bn_param_grads(nt)
-        if self.det:
+        if ua.row_fold:
             for u in (ua, ub):
                 lp = u.layer
                 self._det_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
@@ -1418,7 +1440,7 @@ class HipProgram:
         folds = []          # striped conv weight gradients / head partials -> summed inside the update
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind == "conv" and u.wg_stripes > 1 and not getattr(u, "det_fold", False):
+            if u.kind == "conv" and u.wg_stripes > 1 and not getattr(u, "row_fold", False):
                 lp = u.layer
                 folds.append((offs[f"{lp.name}.weight"], u.dw_acc.shape[1], u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], 1))
                 if u.db_acc is not None:
@@ -1446,9 +1468,12 @@ class HipProgram:
         segs = self.opt_segments
         slo = (C.c_long * 16)(*[x[0] for x in segs])
         shi = (C.c_long * 16)(*[x[1] for x in segs])
+        div = float(self.B if e.cfg.loss_name == "entropy" else self.B * 10)
         if self.head_rg:
-            div = float(self.B if e.cfg.loss_name == "entropy" else self.B * 10)
             met = (K.ptr(self.head_mloss), K.ptr(self.head_mcorr), self.head_mloss.numel(), div,
+                   K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel())
+        elif self.head_sep:             # the row head's per-row loss / #correct
+            met = (K.ptr(self.hrl), K.ptr(self.hrc), self.B, div,
                    K.ptr(e.ring_loss), K.ptr(e.ring_correct), e.ring_correct.numel())
         else:
             met = (None, None, 0, 1.0, None, None, 1)
