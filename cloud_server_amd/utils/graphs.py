@@ -6,10 +6,15 @@ finalised by the cyclic garbage collector at whatever allocation happened to tri
 collection, which was sometimes INSIDE a later capture (the DP tuner's timing graphs).
 Destroying a graph executable while this thread is capturing aborts the process in the
 HIP runtime (SIGABRT, rc 134), with only an unrelated Python frame on the stack.
-PyTorch's ``torch.cuda.graph`` no longer collects before capturing by default, so every
-capture in this package goes through ``capture()``: collect first, keep the collector
-off until the capture has ended, and always use ``thread_local`` capture mode so the
-RCCL watchdog's event queries and other threads' GPU calls stay legal meanwhile.
+So every capture in this package goes through ``capture()``: the collector is off until
+the capture has ended (a pending cycle is collected later, outside any capture), and the
+capture always uses ``thread_local`` mode so the RCCL watchdog's event queries and other
+threads' GPU calls stay legal meanwhile.
+
+(An explicit ``gc.collect()`` before every capture was the first fix; it made each
+re-capture of the packed host cost ~40 ms of collection — 83-100 ms per admission /
+retirement instead of 7-10 ms, profiles/r3_multitenant.md — and is not needed for the
+invariant: with the collector disabled nothing finalises cyclic garbage mid-capture.)
 """
 from __future__ import annotations
 
@@ -24,7 +29,6 @@ import torch
 def capture(graph: "torch.cuda.CUDAGraph", stream: Optional["torch.cuda.Stream"] = None,
             pool=None) -> Iterator[None]:
     was = gc.isenabled()
-    gc.collect()
     gc.disable()
     try:
         kw = {} if stream is None else {"stream": stream}

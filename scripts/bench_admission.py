@@ -83,7 +83,9 @@ def main() -> int:
                          "steady_group_ms": round(t_steady, 3),
                          "stall_ms": round(t_first + t_group - t_steady, 2)})
             print(json.dumps(rows[-1]), flush=True)
-    print(json.dumps({"steady_group_ms_K": round(steady, 3), "jobs": a.jobs,
+    import gc
+    t0 = time.perf_counter(); gc.collect(); t_gc = (time.perf_counter() - t0) * 1e3
+    print(json.dumps({"gc_collect_ms": round(t_gc, 2), "steady_group_ms_K": round(steady, 3), "jobs": a.jobs,
                       "mean_stall_ms_admit": round(sum(r["stall_ms"] for r in rows if r["event"] == "admit") / a.reps, 2),
                       "mean_stall_ms_retire": round(sum(r["stall_ms"] for r in rows if r["event"] == "retire") / a.reps, 2)}))
     return 0

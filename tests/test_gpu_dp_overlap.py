@@ -114,10 +114,10 @@ def test_collective_autotune_records_both_paths(pg, monkeypatch):
                                    rtol=2e-3, atol=2e-5)
 
 
-def test_capture_finalizes_garbage_graphs_before_capturing():
+def test_capture_never_finalizes_garbage_graphs_while_capturing():
     """Regression test of the round-2 GPU-suite abort (profiles/r3_gpu_suite_abort.md): a
-    CUDAGraph left in a reference cycle by an earlier engine must be destroyed BEFORE a new
-    capture begins, never by a garbage collection triggered inside the capture."""
+    CUDAGraph left in a reference cycle by an earlier engine must never be destroyed by a
+    garbage collection triggered inside a capture — only outside it."""
     import gc
     import weakref
     from cloud_server_amd.utils.graphs import capture
@@ -133,15 +133,12 @@ def test_capture_finalizes_garbage_graphs_before_capturing():
     seen = []
     weakref.finalize(h, lambda: seen.append(torch.cuda.is_current_stream_capturing()))
     del h, old
-    gc.disable()                       # the cycle survives until someone collects
-    try:
-        g = torch.cuda.CUDAGraph()
-        with capture(g):
-            for _ in range(200):
-                [object() for _ in range(100)]   # allocations that would trigger a collection
-            x.add_(1)
-    finally:
-        gc.enable()
+    g = torch.cuda.CUDAGraph()
+    with capture(g):
+        for _ in range(200):
+            [object() for _ in range(100)]   # allocations that would trigger a collection
+        x.add_(1)
+    gc.collect()                      # (the collector is back on after the capture)
     assert seen == [False]            # finalised, and not while capturing
     g.replay()
     torch.cuda.synchronize()
