@@ -179,9 +179,11 @@ class TrainEngine:
         self.dstep.add_(1)
 
     # ---------------- host API ----------------
-    def _warm_up(self) -> None:
+    def _warm_up(self, device_sync: bool = True) -> None:
         """Run the program twice off-graph (allocator, autotuning, RCCL comms), then undo
-        the warm-up's effect on the model state so capture starts from step 0's state."""
+        the warm-up's effect on the model state so capture starts from step 0's state.
+        ``device_sync=False``: wait for this engine's streams only (a packed host builds a
+        job on a builder thread while the hosted jobs keep stepping)."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         saved = (self.flat.clone(), self.slots.clone(), self.dstep.clone(),
@@ -191,7 +193,10 @@ class TrainEngine:
             for _ in range(2):      # warm up allocator / autotuning / RCCL comms off-graph
                 self.program.run()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
+        if device_sync:
+            torch.cuda.synchronize(self.device)
+        else:
+            s.synchronize()
         # undo the warm-up's effect on the model state
         self.flat.copy_(saved[0]); self.slots.copy_(saved[1])
         self.dstep.copy_(saved[2]); self.stream.cursor.copy_(saved[3])

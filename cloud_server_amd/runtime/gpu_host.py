@@ -18,18 +18,24 @@ its in-flight steps):
   single-job worker uses (``runtime.trainer.JobRun``).
 
 Between packed steps the host admits new jobs and retires finished ones; the set of jobs
-changing re-captures the packed graph (every engine keeps its state).  A job whose step
+changing re-captures the packed graph (every engine keeps its state).  A new job is BUILT
+on a builder thread (data decode, HBM upload, HIP program planning, its 2 warm-up steps,
+on a stream of its own) while the hosted jobs keep stepping; only the re-capture stops
+them (~10 ms, profiles/r3_multitenant.md).  Captures and builds never overlap.  A job whose step
 raises fails alone; a fault that kills the process fails every job it hosted (the
 manager's auto-restart policy then resumes them from their checkpoints).
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
+import threading
 import time
 import traceback
+from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Dict, List
 
 POLL_S = 0.05
@@ -65,6 +71,24 @@ def _take_inbox(spool: str) -> List[dict]:
     return out
 
 
+def _build_job(req: dict, device: str, backend: str, lock: threading.Lock):
+    """Construct (and warm up) one job off the stepping thread, on its own stream."""
+    import torch
+    from .trainer import JobRun
+    with open(os.path.join(req["model_dir"], "model.json"), encoding="utf-8") as f:
+        config = json.load(f)
+    cuda = device.startswith("cuda") and torch.cuda.is_available()
+    with lock:                                   # never while the stepping thread captures
+        s = torch.cuda.Stream(torch.device(device)) if cuda else None
+        with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
+            job = JobRun(req["model_dir"], config, req.get("datatype", "file"), device=device, backend=backend)
+            if s is not None and job.eng.use_graph and job.pending():
+                job.eng._warm_up(device_sync=False)   # the pack captures it without re-warming
+            if s is not None:
+                s.synchronize()
+    return job
+
+
 def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0.0,
           parent_pid: int = 0) -> int:
     from .multijob import PackedJobs, prefer_packed_kernels
@@ -72,6 +96,9 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
     prefer_packed_kernels()
 
     jobs: Dict[int, JobRun] = {}
+    building: Dict[int, Future] = {}
+    builder = ThreadPoolExecutor(max_workers=1, thread_name_prefix="csa-job-build")
+    gpu_lock = threading.Lock()             # builds vs captures of the packed graph
     pack = None
     idle_since = time.time()
     parent = parent_pid or os.getppid()     # the manager's launcher; if it dies we are orphaned
@@ -84,11 +111,13 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
         changed = False
         for req in _take_inbox(spool):
             jid = int(req["jid"])
+            building[jid] = builder.submit(_build_job, req, device, backend, gpu_lock)
+        for jid, fut in list(building.items()):
+            if not fut.done():
+                continue
+            del building[jid]
             try:
-                with open(os.path.join(req["model_dir"], "model.json"), encoding="utf-8") as f:
-                    config = json.load(f)
-                jobs[jid] = JobRun(req["model_dir"], config, req.get("datatype", "file"),
-                                   device=device, backend=backend)
+                jobs[jid] = fut.result()
                 changed = True
             except Exception:
                 traceback.print_exc()
@@ -102,13 +131,20 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
         if os.getppid() != parent:
             # the manager is gone (killed without a clean shutdown): checkpoint and stop
             # every hosted job rather than keep a GPU context nobody can control
+            for jid, fut in list(building.items()):
+                try:
+                    jobs[jid] = fut.result()
+                except Exception:
+                    _post_done(spool, jid, 1)
             for jid, job in list(jobs.items()):
                 job.state = "stopped"
                 retire(jid, _finish(job))
+            builder.shutdown(wait=True)
             return 0
         if not jobs:
             pack = None
-            if idle_exit_s and time.time() - idle_since > idle_exit_s:
+            if idle_exit_s and not building and time.time() - idle_since > idle_exit_s:
+                builder.shutdown(wait=True)
                 return 0
             time.sleep(POLL_S)
             continue
@@ -129,10 +165,15 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
         # 8 steps of every job in one multi-step graph launch when no job has a hook inside
         # them (PackedJobs.run_steps; 2.4x a lone job's throughput at 4 jobs)
         k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
-        if pack.graph is not None and k > 1 and all(j.groupable(k) for j in jobs.values()):
-            pack.run_steps(k)
-        else:
-            pack.step()
+        group = pack.graph is not None and k > 1 and all(j.groupable(k) for j in jobs.values())
+        # a launch that may capture (new pack, first multi-step launch) waits for a build
+        # in flight; plain replays run alongside it
+        may_capture = pack.graph is None or (group and pack.graph_k is None)
+        with (gpu_lock if may_capture else contextlib.nullcontext()):
+            if group:
+                pack.run_steps(k)
+            else:
+                pack.step()
         for jid, job in list(jobs.items()):
             try:
                 end = job.after_step()
