@@ -150,10 +150,40 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     int k = 0;
     for (int j = 1; j < a.seg.count; ++j) k = t >= a.seg.start4[j] ? j : k;
     const long i = (a.seg.lo[k] >> 2) + (t - a.seg.start4[k]);   // float4 index in the flat buffer
+    // a float4 lying wholly inside one folded gradient: its S stripe loads are issued with
+    // the parameter / slot loads, one memory round trip for all of them (a fold after the
+    // w / g / slot loads cost block 0 — the conv weights — three dependent round trips)
+    int fk = -1;
+    for (int k2 = 0; k2 < a.fold.count; ++k2) {
+      const Fold& f = a.fold.f[k2];
+      const long i0 = i * 4 - f.off;
+      if (i0 >= 0 && i0 + 4 <= f.n && (f.ld & 3) == 0) fk = k2;
+    }
+    float4 sv[MAXS];
+    if (fk >= 0) {
+      const Fold& f = a.fold.f[fk];
+      const long i0 = i * 4 - f.off;
+#pragma unroll
+      for (int s2 = 0; s2 < MAXS; ++s2)
+        sv[s2] = *reinterpret_cast<const float4*>(f.src + (s2 < f.S ? s2 : 0) * f.ld + i0);
+    }
     float4 w = w4[i];
     float4 g = g4[i];
     float4 s0 = nslot >= 1 ? s04[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 s1 = nslot >= 2 ? s14[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fk >= 0) {
+      const Fold& f = a.fold.f[fk];
+      const long i0 = i * 4 - f.off;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int s2 = 0; s2 < MAXS; ++s2) {
+        if (s2 >= f.S) break;
+        acc.x += sv[s2].x; acc.y += sv[s2].y; acc.z += sv[s2].z; acc.w += sv[s2].w;
+      }
+      if (f.zero)
+        for (int s2 = 0; s2 < f.S; ++s2) *reinterpret_cast<float4*>(f.src + s2 * f.ld + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      g = acc;
+    }
     // Zeroing the accumulators the next step adds into must not race with this read:
     // a zero-list pass over flat-gradient ranges run by OTHER threads could clear an
     // element before its owner read it, so the owner clears what it read.
@@ -162,7 +192,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       for (int q = 0; q < a.keep.count; ++q) keep |= (i * 4 >= a.keep.lo[q]) & (i * 4 < a.keep.hi[q]);
       if (!keep) reinterpret_cast<float4*>(a.gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (i * 4 + 3 >= a.fold.lo && i * 4 < a.fold.hi) g = fold_grad(a.fold, i * 4, g);
+    if (fk < 0 && i * 4 + 3 >= a.fold.lo && i * 4 < a.fold.hi) g = fold_grad(a.fold, i * 4, g);   // edges
     float* wp = (float*)&w;
     const float* gp = (const float*)&g;
     float* sp0 = (float*)&s0;

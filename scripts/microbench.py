@@ -86,7 +86,7 @@ def main() -> int:
     if os.environ.get("MB_DU"):
         # per-block stamps (100 MHz realtime): start, loads landed, ticket drawn, finisher end
         for i, (name, fn, args) in enumerate(rec.calls):
-            if name == "csa_dense_bwd_update":
+            if name.startswith("csa_dense_bwd_update"):
                 grid = 4096
                 dbg = torch.zeros(grid * 8, dtype=torch.int64, device="cuda")
                 for _ in range(3):
