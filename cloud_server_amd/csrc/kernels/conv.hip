@@ -998,11 +998,9 @@ static bool set_lds_attr(const void* fn) {
 
 
 // Launch the MFMA conv forward when the shape is inside its family; false = use the VALU
-// kernel.  Bands: ~CSA_CONV_TARGET (700) workgroups over the batch.
+// kernel.  Bands: ~700 workgroups over the batch.
 static bool conv_fwd_mfma(const ConvFwdArgs& f, hipStream_t st) {
-  static const int enabled = [] { const char* e = getenv("CSA_CONV_MFMA"); return e ? atoi(e) : 1; }();
-  static const int target = [] { const char* e = getenv("CSA_CONV_TARGET"); return e ? std::max(1, atoi(e)) : 700; }();
-  if (!enabled) return false;
+  constexpr int target = 700;
   const ConvGeom& g = f.g;
   const PoolGeom& p = f.pool;
   const bool pool = p.on != 0;
@@ -1184,11 +1182,8 @@ static int wgrad_args(const float* x, const uint8_t* img, const int64_t* idx, co
   };
   // Bands: the batch is cut into ~`target` workgroups.  Each ends in one atomicAdd per
   // output and atomics to one 128-B line serialise, so fewer, larger bands win until
-  // the per-wave pixel loop dominates (CSA_WGRAD_TARGET overrides for tuning).
-  static const int target = [] {
-    const char* e = getenv("CSA_WGRAD_TARGET");
-    return e ? std::max(1, atoi(e)) : 700;
-  }();
+  // the per-wave pixel loop dominates (swept: profiles/r1_conv_wgrad_iterations.md).
+  constexpr int target = 700;
   const int per_img = std::max(1, (target + B - 1) / B);
   int rows = std::max(1, (OH + per_img - 1) / per_img);
   while (rows > 1 && lds(rows) > 150 * 1024) --rows;

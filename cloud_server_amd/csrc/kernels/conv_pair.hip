@@ -1398,7 +1398,6 @@ __global__ __launch_bounds__(CPV_T) void cpv_bwd_kernel(CPBwdArgs a) {
 }
 
 static bool cpv_ok(const CPGeom& g) {
-  if (getenv("CSA_CP_MFMA")) return false;               // force the MFMA family (A/B)
   if (g.C0 > 4 || g.C1 > CPV_MAXC1 || g.C2 > CPV_MAXC2) return false;
   if (g.KAh * g.KAw * g.C0 > CPV_MAXKA || g.C1 % 2 || g.C2 % 2) return false;
   if (!((g.KBh == 2 && g.KBw == 2) || (g.KBh == 3 && g.KBw == 3))) return false;   // instantiated
@@ -1445,7 +1444,10 @@ static bool cp_geom(const int* v, CPGeom& g) {
   if (g.C0 < 1 || g.C0 > 4 || g.C1 < 2 || g.C1 > CP_MAXC1 || g.C1 % 2 || g.C2 < 4 || g.C2 > CP_MAXC2 || g.C2 % 4) return false;
   if (g.KAh > 5 || g.KAw > 5 || g.KBh > 5 || g.KBw > 5 || g.H > 64 || g.W > 64) return false;
   if (g.W1 < 1 || g.H2 < 1 || g.W2 < 1) return false;
-  if (((g.KAh * g.KAw * g.C0 + 3) & ~3) > 32) return false;   // static conv-A offset tables
+  // conv A is ONE 16-column MFMA tile in this family: its forward (cp_conv_a) writes
+  // c1 channels < 16 and its weight gradient covers taps (i, j, c0) < 16 — a wider conv A
+  // lowers to separate conv units (tests/test_hip_step.py "wide_conv_a", "wide_c1")
+  if (g.KAh * g.KAw * g.C0 > 16 || g.C1 > 16) return false;
   const int rows = g.pool ? g.PH : g.H2;
   static const int pr_env = [] { const char* e = getenv("CSA_CP_PR"); return e ? atoi(e) : 0; }();
   // unit rows per workgroup: PR = 1 (pooled) measured 120.0 vs 124.8 (PR 2) vs 130.5 us (PR 3)
@@ -1457,7 +1459,6 @@ static bool cp_geom(const int* v, CPGeom& g) {
 
 // Does every band's backward prologue fit the one-batch register budget?
 static bool cp_bwd_one_batch(const CPBwdArgs& a) {
-  if (getenv("CSA_CP_BWD_STAGED")) return false;
   const CPGeom& g = a.g;
   const int C2x2 = 2 * g.C2, per = CP_THREADS / C2x2;
   if (a.bn_on && (per == 0 || a.bn.nslab > CPB_US * per || a.bwd_nslab > CPB_US * per)) return false;

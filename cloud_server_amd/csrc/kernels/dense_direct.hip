@@ -463,7 +463,7 @@ __global__ __launch_bounds__(DD_THREADS) void dd_wgrad_kernel(DDWgrad a) {
 static int dd_splits(int tiles, int K) {
   if (g_csa_det) return 1;                 // deterministic mode: whole-K outputs, plain stores
   // waves per launch: swept 512 / 1024 / 2048 / 4096 -> graph step 125.4 / 120.3 / 119.5 / 122.5 us
-  static const int target = [] { const char* e = getenv("CSA_DD_WAVES"); return e ? atoi(e) : 2048; }();
+  constexpr int target = 2048;
   int ks = (target / DD_WAVES + tiles - 1) / tiles;
   const int maxks = (K + 8 * DD_WAVES * 2 - 1) / (8 * DD_WAVES * 2);   // >= 16 k per wave
   ks = ks < 1 ? 1 : ks;

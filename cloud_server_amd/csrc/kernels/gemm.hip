@@ -437,7 +437,7 @@ static Plan plan_gemm(int M, int N, int K, bool allow_split) {
   const int wg = ((tm + p.wm - 1) / p.wm) * ((tn + p.wn - 1) / p.wn);
   // split K across workgroups until each wave owns <= one KC chunk (one memory round
   // trip per wave), keeping the launch under ~4096 waves and 512 slices
-  static const int maxw = [] { const char* e = getenv("CSA_GEMM_MAX_WAVES"); return e ? atoi(e) : 4096; }();
+  constexpr int maxw = 4096;
   int splits = 1;
   if (allow_split && !g_csa_det)           // deterministic mode: no cross-workgroup atomics
     while ((K + splits * p.wk - 1) / (splits * p.wk) > KC && wg * 4 * splits * 2 <= maxw && splits < 512)

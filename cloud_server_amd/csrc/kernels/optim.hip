@@ -354,7 +354,7 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
   // block cap: swept on MI355X for the 2.28 M-parameter sample (graph step, µs): 512 ->
   // 122.8, 1024 -> 121.0, 1536 -> 120.2, 2048 -> 120.3, 8192 (one float4 per thread) ->
   // 121.6 — more blocks cost more than the grid-stride second iteration saves
-  static const int cap = [] { const char* e = getenv("CSA_OPT_MAX_BLOCKS"); return e ? atoi(e) : 2048; }();
+  constexpr int cap = 2048;
   int blocks = (int)((work + 255) / 256);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;

@@ -53,9 +53,8 @@ class GradSync:
             raise ValueError("ps strategy needs the flat buffer padded to a multiple of world")
         self.shard = numel // ctx.world if ctx.enabled else numel
         self.bucket_elems = max(1, bucket_bytes // 4)
-        # grouped RCCL launches for the multi-tensor lowrank collectives (opt-in: a grouped
+        # (grouped RCCL launches for the multi-tensor collectives are not used: a grouped
         # collective inside HIP-graph capture crashed capture_end on ROCm 7 / torch 2.10)
-        self.coalesce = ctx.backend == "nccl" and os.environ.get("CSA_COALESCE", "0") == "1"
         self.xgmi: Optional[_xg.XgmiComm] = None
         self.xgmi_reason = "off"
         self.xgmi_mode = _xg.enabled_by_env()
@@ -271,9 +270,8 @@ class GradSync:
         dist.all_gather_into_tensor(out, local.contiguous())
 
     def all_gather_rows_many(self, pairs, tag: str = "gather") -> None:
-        """Several ``all_gather_rows`` issued as ONE launch: the xGMI peer-buffer kernel, or
-        a grouped RCCL launch where the backend supports coalescing (each separate
-        collective pays its own fixed latency).  ``tag`` names the call site (one
+        """Several ``all_gather_rows`` issued as ONE launch where the xGMI peer-buffer kernel
+        takes them (each separate RCCL collective pays its own fixed latency).  ``tag`` names the call site (one
         device-ordered sequence of calls per tag)."""
         if not self.ctx.enabled:
             for local, out in pairs:
@@ -284,28 +282,18 @@ class GradSync:
             if ch is not None:
                 ch.all_gather(pairs)
                 return
-            if self.coalesce and len(pairs) > 1:
-                with dist._coalescing_manager(async_ops=False):
-                    for local, out in pairs:
-                        dist.all_gather_into_tensor(out, local.contiguous())
-                return
             for local, out in pairs:
                 dist.all_gather_into_tensor(out, local.contiguous())
 
     def allreduce_ranges(self, flat: torch.Tensor, ranges, tag: str = "ranges") -> None:
-        """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one launch: xGMI kernel or a
-        grouped RCCL launch)."""
+        """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one launch on the xGMI
+        kernel, else one RCCL all-reduce per slice)."""
         if not self.ctx.enabled or not ranges:
             return
         ch = self._xg_channel(tag, [flat[lo:hi] for lo, hi in ranges]) if len(ranges) <= 8 else None
         with self._timed():
             if ch is not None:
                 ch.all_reduce([flat[lo:hi] for lo, hi in ranges])
-                return
-            if self.coalesce and len(ranges) > 1:
-                with dist._coalescing_manager(async_ops=False):
-                    for lo, hi in ranges:
-                        dist.all_reduce(flat[lo:hi])
                 return
             for lo, hi in ranges:
                 dist.all_reduce(flat[lo:hi])

@@ -33,7 +33,7 @@ OP_GATHER, OP_ALLREDUCE, OP_ALLREDUCE_2SHOT = 0, 1, 2
 # default protocol crossover (per-rank message bytes) until the start-up tuner measured
 # both on the real links: one-shot below (one flag round trip), two-shot above (2 (W-1)/W
 # of the message leaves each GPU instead of (W-1) x)
-TWO_SHOT_MIN_BYTES = int(os.environ.get("CSA_XGMI_TWOSHOT_KB", "256")) * 1024
+TWO_SHOT_MIN_BYTES = 256 * 1024
 
 
 def _aligned(t: torch.Tensor) -> bool:
@@ -100,10 +100,9 @@ class XgmiChannel:
         self._flags = (C.c_void_p * world)(*ptrs[1])
         self.state = torch.zeros(4, dtype=torch.int32, device=device)   # seq, done, err, pad
         # workgroups per call (0: one per ~8 KB of the per-rank message, at most 256)
-        kb = int(os.environ.get("CSA_XGMI_BLOCK_KB", "0"))
-        self.nblocks = 0 if kb <= 0 else max(1, min(nblk, -(-self.slot_bytes // (kb * 1024))))
+        self.nblocks = 0
         # all-reduce protocol: None = by size (TWO_SHOT_MIN_BYTES); the tuner pins it
-        self.protocol: Optional[str] = os.environ.get("CSA_XGMI_PROTOCOL") or None
+        self.protocol: Optional[str] = None
 
     # ---------------------------------------------------------------- calls
     def _run(self, op: int, srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:

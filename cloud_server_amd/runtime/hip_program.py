@@ -238,7 +238,7 @@ class HipProgram:
             # inside that weight-gradient launch (csa_dd_wgrad update mode: dW never exists)
             # where the variables live — as ApplyAdagrad on the PS did
             # (construct_distribute.py:355-357, 372-373)
-            u.lr_update = os.environ.get("CSA_LOWRANK_UPDATE", "1") == "1"
+            u.lr_update = True
             for p in ("weight", "bias"):
                 n = f"{u.layer.name}.{p}"
                 taken.append((offs[n], offs[n] + self.gviews[n].numel()))
@@ -327,8 +327,7 @@ class HipProgram:
             # (a narrow layer's row groups are split over 128-column blocks with a partial
             # hand-off, so fc2's 32 row groups still use 128 CUs: profiles/r2_dense_fused.md)
             groups = (fin + 15) // 16
-            u.fused = (bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C))
-                       and groups >= int(os.environ.get("CSA_FUSED_DENSE_MIN_GROUPS", "1")))
+            u.fused = bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C)) and groups >= 1
         self.head_rg = 0
         self.head_row = False
         self.head_sep = False
@@ -338,8 +337,7 @@ class HipProgram:
             # gradient before the all-reduce, its metrics folded by the optimizer launch
             # (the atomic 4-workgroup head took 15.6 us per DP step)
             last = self.units[-1]
-            if (last.kind == "dense" and self.lib.csa_head_row_ok(B, last.layer.spec.hidden)
-                    and os.environ.get("CSA_HEAD_ROW", "1") == "1"):
+            if last.kind == "dense" and self.lib.csa_head_row_ok(B, last.layer.spec.hidden):
                 self.head_row = self.head_sep = True
         if self.fused and self.head_tf.norm is None:
             last = self.units[-1]
@@ -349,8 +347,7 @@ class HipProgram:
             # one batch row per workgroup; the head's batch reductions (dWh, dbh, metrics)
             # ride in the last dense layer's fused backward (csa_head_row + the head epilogue
             # of csa_dense_bwd_update_head) — no partial rows for the optimizer to fold
-            self.head_row = (last.kind == "dense" and last.fused and bool(self.lib.csa_head_row_ok(B, K))
-                             and os.environ.get("CSA_HEAD_ROW", "1") == "1")
+            self.head_row = last.kind == "dense" and last.fused and bool(self.lib.csa_head_row_ok(B, K))
             if not self.head_row:
                 self.head_rg = int(self.lib.csa_head_part_rows(B, K))
         # register-direct MFMA dense kernels (dense_direct.hip): forward, input gradient and
@@ -382,7 +379,7 @@ class HipProgram:
         -> pool) runs as ONE forward and ONE backward launch (conv_pair.hip): c1 stays in
         LDS, the backward recomputes it and never writes dc2 / dc1."""
         self.pair = None
-        if os.environ.get("CSA_CONV_PAIR_FUSE", "1") != "1" or len(self.units) < 2:
+        if len(self.units) < 2:
             return
         ua, ub = self.units[0], self.units[1]
         if ua.kind != "conv" or ub.kind != "conv" or ua.pool is not None:
@@ -1008,7 +1005,7 @@ class HipProgram:
                 sp = lp.spec
                 h, w = lp.in_shape.hw
                 oh, ow = lp.out_shape.hw
-                if prev is not None and os.environ.get("CSA_CONV_PAIR", "1") == "1":
+                if prev is not None:
                     # input gradient + weight gradient in one launch
                     self._rc(lib.csa_conv_bwd(
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
@@ -1307,8 +1304,6 @@ class HipProgram:
         """Input gradient + weight gradient of a dense unit as ONE launch
         (``csa_dense_bwd``) when its weight-gradient operand needs no transform (a
         materialised BN/act input, or an identity transform).  False: not applicable."""
-        if os.environ.get("CSA_DENSE_PAIR", "1") != "1":
-            return False
         tf, lp, B = u.in_tf, u.layer, self.B
         if u.xt is None and (tf.has_bn or tf.act is not None):
             return False

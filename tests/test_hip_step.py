@@ -59,6 +59,39 @@ CASES = {
         {"layer": "norm"},
         {"layer": "connect", "hidden": 32},
     ],
+    # the MFMA conv-pair family (outside the VALU pair's family): a 4x4 conv B, and a
+    # 48-channel conv B whose backward takes the staged (multi-batch) prologue
+    "pair_mfma": [
+        {"layer": "conv", "filter": [3, 3, 8], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [4, 4, 16]},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "pool"},
+        {"layer": "norm"},
+        {"layer": "connect", "hidden": 32},
+    ],
+    "pair_mfma_wide": [
+        {"layer": "conv", "filter": [2, 2, 8]},
+        {"layer": "conv", "filter": [3, 3, 48], "isBias": "True"},
+        {"layer": "active", "active_func": "sigmoid"},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 16},
+    ],
+    # conv A beyond the pair kernels' 16-wide conv-A tile: separate conv units
+    "wide_conv_a": [
+        {"layer": "conv", "filter": [5, 5, 8], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [3, 3, 16]},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 32},
+    ],
+    "wide_c1": [
+        {"layer": "conv", "filter": [3, 3, 24]},
+        {"layer": "conv", "filter": [2, 2, 32], "isBias": "True"},
+        {"layer": "active", "active_func": "sigmoid"},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 16},
+    ],
     "pair_nopool": [
         {"layer": "conv", "filter": [2, 2, 4]},
         {"layer": "conv", "filter": [3, 3, 8]},
@@ -253,7 +286,6 @@ def test_fused_update_path_active_and_matches_unfused(monkeypatch):
         cfg = _cfg(CASES["sample"], optimizer=opt, lr=1e-3)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "1")
         monkeypatch.setenv("CSA_FUSED_DENSE", "1")
-        monkeypatch.setenv("CSA_FUSED_DENSE_MIN_GROUPS", "1")     # fc2 (32 row groups) too
         a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
         monkeypatch.setenv("CSA_FUSED_UPDATE", "0")
         b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
@@ -271,13 +303,26 @@ def test_fused_update_path_active_and_matches_unfused(monkeypatch):
         assert int(a.dstep.item()) == int(b.dstep.item()) == 5
 
 
-@pytest.mark.parametrize("name", ["sample", "pair_relu_valid", "pair_nopool"])
-def test_conv_pair_fused_active(name):
+@pytest.mark.parametrize("name,valu", [("sample", True), ("pair_relu_valid", True), ("pair_nopool", True),
+                                       ("pair_mfma", False), ("pair_mfma_wide", False)])
+def test_conv_pair_fused_active(name, valu):
     """The leading conv pair runs as the fused conv_pair kernels (one forward and one
-    backward launch) for these configs; numerics are pinned by test_step_matches_torch."""
+    backward launch) for these configs, in the VALU family or the MFMA family as expected;
+    numerics of every case are pinned by test_step_matches_torch."""
+    from cloud_server_amd.ops import fused as FK
     ds = synthetic_mnist(200, seed=3)
     eng = TrainEngine(_cfg(CASES[name]), ds, device="cuda", backend="hip", use_graph=False)
     assert eng.program.pair is not None
+    assert bool(eng.program.lib.csa_conv_pair_valu_ok(FK.ints(eng.program.pair))) == valu
+
+
+@pytest.mark.parametrize("name", ["wide_conv_a", "wide_c1"])
+def test_wide_conv_a_lowers_to_separate_units(name):
+    """A conv A wider than the pair kernels' conv-A tile (> 16 taps or > 16 channels) is
+    not fused into a pair; numerics are pinned by test_step_matches_torch."""
+    ds = synthetic_mnist(200, seed=3)
+    eng = TrainEngine(_cfg(CASES[name]), ds, device="cuda", backend="hip", use_graph=False)
+    assert eng.backend == "hip" and eng.program.pair is None
 
 
 def test_staged_batch_matches_cursor_path(monkeypatch):
