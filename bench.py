@@ -88,15 +88,14 @@ def bench_packed(args) -> int:
         import torch
         from cloud_server_amd.data.datasets import synthetic_mnist
         from cloud_server_amd.runtime.engine import TrainEngine
-        from cloud_server_amd.runtime.multijob import PackedJobs, prefer_packed_kernels
-        prefer_packed_kernels()
+        from cloud_server_amd.runtime.multijob import PackedJobs
         dev = "cuda:0" if torch.cuda.is_available() else "cpu"
         engs = []
         for r in range(K):
             cfg = _sample_cfg(args)
             cfg.seed = r
             engs.append(TrainEngine(cfg, synthetic_mnist(60000, seed=r), device=dev,
-                                    backend=args.backend, use_graph=not args.no_graph))
+                                    backend=args.backend, use_graph=not args.no_graph, packed=True))
         pack = PackedJobs(engs)
         pack.step()                       # capture + first step
         pack.run_steps(max(args.warmup - 1, 0))   # (captures the multi-step graph)

@@ -1449,7 +1449,9 @@ static bool cp_geom(const int* v, CPGeom& g) {
   // lowers to separate conv units (tests/test_hip_step.py "wide_conv_a", "wide_c1")
   if (g.KAh * g.KAw * g.C0 > 16 || g.C1 > 16) return false;
   const int rows = g.pool ? g.PH : g.H2;
-  static const int pr_env = [] { const char* e = getenv("CSA_CP_PR"); return e ? atoi(e) : 0; }();
+  // packed profile: two pooled rows per workgroup (350 instead of 700 for B = 50) — less
+  // per-band staging CU-time: K = 8 jobs 995.4k vs 930.5k samples/s (profiles/r2_multitenant.md)
+  const int pr_env = g_csa_packed ? 2 : 0;
   // unit rows per workgroup: PR = 1 (pooled) measured 120.0 vs 124.8 (PR 2) vs 130.5 us (PR 3)
   // per graph step — more workgroups (700 for B = 50) beat the per-band staging overhead
   g.PR = pr_env > 0 ? pr_env : (g.pool ? 1 : 2);

@@ -560,7 +560,9 @@ CSA_API int csa_dense_bwd_update_slabs(int K) {
 // fill the chip (fc1: 245) and N <= 512, else 128-column blocks of 256 threads.
 static int du_cs(int K, int N) {
   const int groups = (K + DU_FT - 1) / DU_FT;
-  static const int minb = [] { const char* e = getenv("CSA_DU_WIDE_MIN_GROUPS"); return e ? atoi(e) : 128; }();
+  // packed profile: always 128-column blocks (256 threads, 33 KB LDS: four per CU beside
+  // other jobs' kernels): K = 4 805.5k vs 743.0k samples/s (profiles/r2_multitenant.md)
+  const int minb = g_csa_packed ? (1 << 30) : 128;
   if (N <= 512 && groups >= minb) return 1;
   return (N + 127) / 128;
 }

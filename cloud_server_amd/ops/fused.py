@@ -71,6 +71,8 @@ _SIGS = {
     "csa_conv_pair_grid": (I, [P]),
     "csa_set_deterministic": (None, [I]),
     "csa_deterministic": (I, []),
+    "csa_set_packed": (None, [I]),
+    "csa_packed": (I, []),
     "csa_rows_fold": (I, [P, L, I, L, P, I, P]),
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
                               P, P, P, P, I, P]),

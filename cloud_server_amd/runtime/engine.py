@@ -80,8 +80,11 @@ class TrainEngine:
     def __init__(self, cfg: TrainConfig, train: ArrayDataset, device="cpu",
                  ctx: Optional[DistContext] = None, backend: str = "auto",
                  use_graph: Optional[bool] = None, strategy: str = "allreduce",
-                 stream_chunk: int = 512):
+                 stream_chunk: int = 512, packed: bool = False):
+        """``packed``: this engine will run as one branch of a multi-job graph
+        (``runtime.multijob``): its HIP program uses the packed launch profile."""
         self.cfg = cfg
+        self.packed = packed
         self.ctx = ctx or DistContext(device=torch.device(device))
         self.device = torch.device(device)
         self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world,

@@ -81,7 +81,8 @@ def _build_job(req: dict, device: str, backend: str, lock: threading.Lock):
     with lock:                                   # never while the stepping thread captures
         s = torch.cuda.Stream(torch.device(device)) if cuda else None
         with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
-            job = JobRun(req["model_dir"], config, req.get("datatype", "file"), device=device, backend=backend)
+            job = JobRun(req["model_dir"], config, req.get("datatype", "file"), device=device, backend=backend,
+                         packed=True)
             if s is not None and job.eng.use_graph and job.pending():
                 job.eng._warm_up(device_sync=False)   # the pack captures it without re-warming
             if s is not None:
@@ -91,9 +92,8 @@ def _build_job(req: dict, device: str, backend: str, lock: threading.Lock):
 
 def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0.0,
           parent_pid: int = 0) -> int:
-    from .multijob import PackedJobs, prefer_packed_kernels
+    from .multijob import PackedJobs
     from .trainer import JobRun
-    prefer_packed_kernels()
 
     jobs: Dict[int, JobRun] = {}
     building: Dict[int, Future] = {}

@@ -119,6 +119,9 @@ class HipProgram:
         # no split-K.  The library flag is process state: set around every planning and
         # launch sequence of this program, restored afterwards.
         self.det = bool(getattr(eng, "deterministic", False)) and not forward_only
+        # packed profile (engines built to run as branches of one multi-job graph): launch
+        # shapes with less CU-time per step (conv_pair.hip, dense_update.hip)
+        self.packed = bool(getattr(eng, "packed", False))
         with self._det_scope():
             self._init_plan(eng, forward_only)
 
@@ -127,11 +130,13 @@ class HipProgram:
 
         class _Scope:
             def __enter__(self_):
-                self_.prev = int(prog.lib.csa_deterministic())
+                self_.prev = (int(prog.lib.csa_deterministic()), int(prog.lib.csa_packed()))
                 prog.lib.csa_set_deterministic(1 if prog.det else 0)
+                prog.lib.csa_set_packed(1 if prog.packed else 0)
 
             def __exit__(self_, *exc):
-                prog.lib.csa_set_deterministic(self_.prev)
+                prog.lib.csa_set_deterministic(self_.prev[0])
+                prog.lib.csa_set_packed(self_.prev[1])
                 return False
         return _Scope()
 
@@ -350,28 +355,19 @@ class HipProgram:
             self.head_row = last.kind == "dense" and last.fused and bool(self.lib.csa_head_row_ok(B, K))
             if not self.head_row:
                 self.head_rg = int(self.lib.csa_head_part_rows(B, K))
-        # register-direct MFMA dense kernels (dense_direct.hip): forward, input gradient and
-        # weight gradient; on one GPU the weight-gradient launch applies the optimizer update
-        # itself (the head advanced the step counter), so dW never exists in memory
-        # (lowrank data parallelism forms its dense weight gradients from gathered operands
-        # on a side stream: those layers keep the LDS-staged kernels)
-        # CSA_DENSE_DIRECT: "fwd" (default) = forward GEMMs only, "1" = forward + backward
-        # (+ in-kernel update), "0" = off — measured per launch in profiles/r2_dense_direct.md
-        mode = os.environ.get("CSA_DENSE_DIRECT", "fwd")
-        direct = mode in ("1", "fwd")
-        lowrank = e.ctx.enabled and e.sync.strategy == "lowrank"
+        # register-direct MFMA dense forward (dense_direct.hip); the backward of a dense layer
+        # is the fused backward + update (one GPU), the LDS-staged dgrad + wgrad pair (data
+        # parallel: the gradient is all-reduced), or under lowrank the gathered-operand
+        # weight gradient with the update in-kernel (profiles/r2_dense_direct.md measured
+        # the register-direct backward slower than the paired kernels)
         for u in self.units:
-            u.direct = u.direct_bwd = u.direct_update = u.lr_update = False
-            if u.kind != "dense" or not direct:
+            u.direct = u.lr_update = False
+            if u.kind != "dense":
                 continue
             fin = u.layer.in_shape.numel
             if u.in_tf.has_bn and fin % 4:
                 continue                         # BN'd input not materialised: LDS-staged GEMM
             u.direct = True
-            if u.fused:
-                continue                         # backward + update: csa_dense_bwd_update
-            u.direct_bwd = mode == "1" and not lowrank     # lowrank: wgrad from gathered operands
-            u.direct_update = bool(u.direct_bwd and self.fused and (self.head_rg or self.head_row))
 
     # ------------------------------------------------------------------ conv pair
     def _plan_pair(self) -> None:
@@ -596,8 +592,6 @@ class HipProgram:
                 C = src.y.shape[3]
                 if u.kind == "dense" and u.fused:
                     nb = self.lib.csa_dense_bwd_update_slabs(u.layer.in_shape.numel)
-                elif u.kind == "dense" and u.direct_bwd:
-                    nb = self.lib.csa_dd_dgrad_slabs()
                 elif u.kind == "dense":
                     nb = self.lib.csa_dense_dgrad_slabs(B, u.layer.in_shape.numel, u.layer.spec.hidden)
                 else:
@@ -672,10 +666,6 @@ class HipProgram:
                     regs.append(u.y)
                 if u.fused:
                     continue                     # plain stores; W never has a gradient buffer
-                if u.direct_bwd:
-                    if k > 0 and self.lib.csa_dd_dgrad_splits(B, fin, fout) > 1:
-                        regs.append(self.units[k - 1].dy)
-                    continue                     # wgrad: whole stores or the update itself
                 if k > 0:
                     tfm = u.in_tf.has_bn or u.in_tf.act is not None
                     if self.lib.csa_dense_dgrad_splits(B, fin, fout, int(tfm)) > 1:
@@ -744,11 +734,11 @@ class HipProgram:
         self.keep_ranges = []
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind != "dense" or u.fused or u.direct_update or u.lr_update:
+            if u.kind != "dense" or u.fused or u.lr_update:
                 continue
             fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
             m = B * (self.e.ctx.world if u in getattr(self, "lr_units", []) else 1)
-            if (u.direct_bwd and u not in getattr(self, "lr_units", [])) or self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
+            if self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
                 for p in ("weight", "bias"):
                     n = f"{u.layer.name}.{p}"
                     lo = offs[n]
@@ -941,10 +931,6 @@ class HipProgram:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
                 if u.fused:
                     self._dense_bwd_update(u, prev, st)
-                    continue
-                if u.direct_bwd and u not in self.lr_units:
-                    self._dense_bwd_direct(u, prev, st)
-                    self._grad_ready(k)
                     continue
                 if (prev is not None and u not in self.lr_units
                         and self._dense_bwd_fused(u, prev, st)):
@@ -1319,29 +1305,6 @@ class HipProgram:
             raise RuntimeError(f"dense_bwd failed: {rc}")
         return rc > 0
 
-    def _dense_bwd_direct(self, u: Unit, prev: Optional[Unit], st) -> None:
-        """Dense backward on the register-direct kernels: input gradient (through the
-        forward transform's backward) first — it reads the OLD weights — then the weight
-        gradient, or on one GPU the optimizer update of W / b in the same launch."""
-        e, lib, B = self.e, self.lib, self.B
-        lp, tf = u.layer, u.in_tf
-        fin, fout = lp.in_shape.numel, lp.spec.hidden
-        V, G = self.views, self.gviews
-        if prev is not None:
-            self._rc(lib.csa_dd_dgrad(
-                K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
-                K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
-                K.ptr(tf.bwd_slab) if tf.has_bn else None, st), "dd_dgrad")
-        xin = u.xt if u.xt is not None else u.x.view(B, -1)
-        act = (0, 0.0) if u.xt is not None else (_act_id(tf.act), _alpha(tf.act))
-        if u.direct_update:
-            self._dd_wgrad_update(u, xin, u.dy, B, act, st)
-        else:
-            self._rc(lib.csa_dd_wgrad(
-                K.ptr(xin), K.ptr(u.dy), B, fin, fout, act[0], act[1], 1.0,
-                K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
-                None, None, None, None, None, None, -1, 0.0, None, st), "dd_wgrad")
-
     def _dd_wgrad_update(self, u: Unit, x: torch.Tensor, dy: torch.Tensor, M: int, act, st) -> None:
         """Weight gradient X^T dY over ``M`` rows with the optimizer update of W / b applied
         in the same launch (csa_dd_wgrad update mode; the head advanced the step counter)."""
@@ -1404,7 +1367,7 @@ class HipProgram:
         ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
         skip = set()
         for u in self.units:
-            if u.kind == "dense" and (u.fused or u.direct_update or u.lr_update):
+            if u.kind == "dense" and (u.fused or u.lr_update):
                 skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
         if not skip:
             return []

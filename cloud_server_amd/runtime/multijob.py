@@ -19,10 +19,10 @@ Every job's numerics are exactly those of a lone run: branches share no buffers,
 branch is the same kernel sequence its own engine would capture.
 
 Packed, the chip is saturated, so what matters is CU-time per job-step rather than one
-job's latency: ``prefer_packed_kernels()`` selects the register-direct dense backward
-with the in-kernel optimizer update (no 8 MB gradient round trip, a smaller optimizer
-launch) — slower alone (139 vs 126 µs), faster packed (874k vs 817k samples/s at K=8,
-profiles/r2_multitenant.md).
+job's latency: engines built with ``packed=True`` run the packed launch profile (two
+pooled rows per conv-pair workgroup, 128-column fused dense blocks; profiles/
+r2_multitenant.md) — set per program around its own planning and launches, no process
+environment is touched.
 """
 from __future__ import annotations
 
@@ -33,19 +33,6 @@ import torch
 from .engine import TrainEngine
 from ..utils.tracing import trace_range
 from ..utils.graphs import capture
-
-
-def prefer_packed_kernels() -> None:
-    """Kernel choices for engines that will run packed (unless the user chose)."""
-    import os
-    os.environ.setdefault("CSA_DENSE_DIRECT", "1")
-    # wide dense backward as 128-column blocks (256 threads, 33 KB LDS: four per CU beside
-    # other jobs' kernels) instead of one 1024-thread, 106 KB row-group block per CU:
-    # K = 4 805.5k vs 743.0k, K = 8 917.8k vs 861.0k samples/s (profiles/r2_multitenant.md)
-    os.environ.setdefault("CSA_DU_WIDE_MIN_GROUPS", "100000")
-    # conv pair: two pooled rows per workgroup (350 instead of 700 for B = 50) — less
-    # per-band staging CU-time: K = 8 995.4k vs 930.5k samples/s (scripts/gpu_pack4.sh)
-    os.environ.setdefault("CSA_CP_PR", "2")
 
 
 class PackedJobs:

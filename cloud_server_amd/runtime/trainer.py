@@ -192,7 +192,7 @@ class JobRun:
 
     def __init__(self, model_dir: str, config: Dict[str, Any], datatype: str = "file",
                  device: Optional[str] = None, ctx: Optional[DistContext] = None,
-                 backend: str = "auto", data: Optional[tuple] = None):
+                 backend: str = "auto", data: Optional[tuple] = None, packed: bool = False):
         self.model_dir = model_dir
         self.ctx = ctx = ctx or DistContext()
         self.chief = chief = ctx.is_chief
@@ -208,7 +208,7 @@ class JobRun:
         self.mlog = None
         try:
             train, self.test = data if data is not None else load_job_data(model_dir, datatype, cfg.ratio)
-            self.eng = eng = TrainEngine(cfg, train, device=device, ctx=ctx, backend=backend,
+            self.eng = eng = TrainEngine(cfg, train, device=device, ctx=ctx, backend=backend, packed=packed,
                                          strategy=config.get("options", {}).get("strategy", "allreduce")
                                          if isinstance(config.get("options"), dict) else "allreduce")
             last = ckpt.latest(model_dir)

@@ -32,9 +32,8 @@ def main() -> int:
     from cloud_server_amd.data.datasets import synthetic_mnist
     from cloud_server_amd.models.dsl import SAMPLE_CONFIG, parse_train_config
     from cloud_server_amd.runtime.engine import TrainEngine
-    from cloud_server_amd.runtime.multijob import PackedJobs, prefer_packed_kernels
+    from cloud_server_amd.runtime.multijob import PackedJobs
 
-    prefer_packed_kernels()
     os.environ.setdefault("CSA_GRAPH_STEPS", "8")
     dev = "cuda:0"
 
@@ -47,7 +46,8 @@ def main() -> int:
 
     def build(seed):
         t0 = time.perf_counter()
-        e = TrainEngine(cfg(seed), synthetic_mnist(60000, seed=seed), device=dev, backend="hip", use_graph=True)
+        e = TrainEngine(cfg(seed), synthetic_mnist(60000, seed=seed), device=dev, backend="hip", use_graph=True,
+                        packed=True)
         torch.cuda.synchronize()
         return e, (time.perf_counter() - t0) * 1e3
 

@@ -106,17 +106,21 @@ def test_packed_hip_jobs_match_solo():
     from cloud_server_amd.runtime.engine import TrainEngine
     from cloud_server_amd.runtime.multijob import PackedJobs
 
-    def eng(seed):
+    def eng(seed, packed=False):
         c = _cfg(100, seed=seed)
         c.update(optimizer_name="AdagradOptimizer", learning_rate=1e-3)
-        return TrainEngine(parse_train_config(c), synthetic_mnist(2000, seed=seed), device="cuda:0", backend="hip")
+        return TrainEngine(parse_train_config(c), synthetic_mnist(2000, seed=seed), device="cuda:0", backend="hip",
+                           packed=packed)
 
     solo = [eng(s) for s in (1, 2, 3)]
     for e in solo:
         for _ in range(20):
             e.step()
-    packed = [eng(s) for s in (1, 2, 3)]
+    # the packed launch profile (two pooled rows per conv-pair workgroup, 128-column fused
+    # dense blocks) trains like the solo profile
+    packed = [eng(s, packed=True) for s in (1, 2, 3)]
     assert all(e.backend == "hip" for e in solo + packed)
+    assert all(e.program.packed for e in packed) and not any(e.program.packed for e in solo)
     pack = PackedJobs(packed)
     for _ in range(20):
         pack.step()
