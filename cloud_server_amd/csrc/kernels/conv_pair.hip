@@ -1410,6 +1410,9 @@ static bool cpv_ok(const CPGeom& g) {
   return true;
 }
 
+static size_t cp_lds(const CPGeom& g, bool bwd);
+static bool cp_lds_ok_bwd(const CPGeom& g) { return cp_lds(g, true) <= CP_LDS_MAX; }
+
 static bool cpv_bwd_ok(const CPBwdArgs& a) {
   const CPGeom& g = a.g;
   if (!cpv_ok(g)) return false;
@@ -1575,7 +1578,10 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
   const dim3 grid((unsigned)(a.g.B * a.g.nbands));
-  if (cpv_bwd_ok(a)) {
+  // VALU backward only in deterministic mode (its in-workgroup reductions are fixed-order);
+  // otherwise the MFMA backward: 20.9 vs 24.5 us per launch for the sample pair
+  // (profiles/r3_notes.md), while the VALU forward stays the faster forward
+  if (cpv_bwd_ok(a) && (g_csa_det || !cp_lds_ok_bwd(a.g))) {
     static bool vattr = hipFuncSetAttribute((const void*)cpv_bwd_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)CP_LDS_MAX) == hipSuccess &&
                         hipFuncSetAttribute((const void*)cpv_bwd_kernel<3, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
