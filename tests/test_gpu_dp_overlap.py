@@ -89,6 +89,32 @@ def test_lowrank_strategy_matches_single_gpu(pg, monkeypatch):
                                    rtol=2e-3, atol=2e-5)
 
 
+@pytest.mark.parametrize("strategy,xgmi", [("ps", "0"), ("ps", "1"), ("allreduce", "0")])
+def test_ps_and_rccl_programs_match_single_gpu(pg, monkeypatch, strategy, xgmi):
+    """The parameter-server capability (``ps``: reduce-scatter -> owner optimizer on its
+    shard -> all-gather, the reference's PS placement) and the all-reduce program on plain
+    RCCL, on the HIP program with the row-per-workgroup head and the striped pair
+    gradients; world 1 must reproduce the single-GPU step (20 steps, 8-step graphs)."""
+    monkeypatch.setenv("CSA_XGMI", xgmi)
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
+    assert a.backend == "hip", a.fallback_reason
+    assert a.program.head_row and a.program.head_sep
+    assert a.program.units[0].row_fold and a.program.units[0].wg_stripes == 16
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for _ in range(4):
+        a.step(); b.step()
+    a.run_steps(16); b.run_steps(16)
+    torch.cuda.synchronize()
+    assert a.host_step == b.host_step == 20 and int(a.dstep.item()) == 20
+    torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
+    ma, mb = a.metrics_since(0), b.metrics_since(0)
+    assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
+    assert abs(ma["accuracy"] - mb["accuracy"]) <= 3 / (20 * 50) + 1e-9
+
+
 def test_collective_autotune_records_both_paths(pg, monkeypatch):
     """CSA_XGMI=auto: each call site is timed on both paths (HIP graphs of 10 calls) at
     first use and the choice is recorded; training still matches the single-GPU step."""
