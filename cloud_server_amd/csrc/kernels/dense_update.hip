@@ -72,6 +72,9 @@ struct DUArgs {
   float* s0w; float* s1w;   // optimizer slots of W (same [K][N] layout) ...
   float* s0b; float* s1b;   // ... and of the bias
   float scale;
+  // gradient mode (gW != null, data parallel): the weight / bias GRADIENTS are stored whole
+  // into gW / gb (the flat gradient, all-reduced before the optimizer) instead of updating
+  float* gW; float* gb;
   int cs;                   // column blocks per row group (> 1: partial hand-off)
   float* part;              // [groups * cs][DU_PART] input-gradient partials (write-through)
   unsigned* cnt;            // [groups] arrival tickets (zero between launches)
@@ -115,14 +118,14 @@ __device__ __forceinline__ void du_store_w(const DUArgs& a, const float4 (&wv)[D
                                            const bool (&sok)[DU_SUB], int i, int nf, bool bown, int bn0, float bw,
                                            float bs0, float bs1) {
   if (bown && (threadIdx.x & 63) == 0) {
-    a.bias[bn0] = bw;
+    (a.gW ? a.gb : a.bias)[bn0] = bw;
     if (NSLOT >= 1) a.s0b[bn0] = bs0;
     if (NSLOT >= 2) a.s1b[bn0] = bs1;
   }
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
     if (!sok[j] || i >= nf) continue;
-    *reinterpret_cast<float4*>(a.W + wofs[j]) = wv[j];
+    *reinterpret_cast<float4*>((a.gW ? a.gW : a.W) + wofs[j]) = wv[j];
     if (NSLOT >= 1) *reinterpret_cast<float4*>(a.s0w + wofs[j]) = s0v[j];
     if (NSLOT >= 2) *reinterpret_cast<float4*>(a.s1w + wofs[j]) = s1v[j];
   }
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
   //     addresses: a load inside a branch is waited for right there, and vmcnt is in order)
   const int bper = (nb + groups - 1) / groups;
   const int bn0 = cb + grp * bper + wave;
-  const bool bown = a.bias && wave < bper && grp * bper + wave < nb;
+  const bool bown = (a.bias || a.gW) && wave < bper && grp * bper + wave < nb;
   const int bnc = bown ? bn0 : 0;
   float bw = (a.bias ? a.bias : a.dY)[bnc];
   float bs0 = (nslot >= 1 && a.bias ? a.s0b : a.dY)[bnc];
@@ -376,7 +379,10 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
     float s0[4] = {s0v[j].x, s0v[j].y, s0v[j].z, s0v[j].w};
     float s1[4] = {s1v[j].x, s1v[j].y, s1v[j].z, s1v[j].w};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) opt_update(a.opt, lr, w[r], (g0[r] + g1[r]) * a.scale, s0[r], s1[r]);
+    for (int r = 0; r < 4; ++r) {
+      if (a.gW) w[r] = (g0[r] + g1[r]) * a.scale;          // gradient mode: the store below writes dW
+      else opt_update(a.opt, lr, w[r], (g0[r] + g1[r]) * a.scale, s0[r], s1[r]);
+    }
     wv[j] = make_float4(w[0], w[1], w[2], w[3]);
     s0v[j] = make_float4(s0[0], s0[1], s0[2], s0[3]);
     s1v[j] = make_float4(s1[0], s1[1], s1[2], s1[3]);
@@ -391,14 +397,15 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
       float v = lane < M ? sdy[lane * SN + lcol] : 0.f;
       v = wave_sum(v);
       if (lane == 0) {
-        if (u != wave) {
+        if (u != wave && !a.gW) {
           bw = a.bias[n];
           if (nslot >= 1) bs0 = a.s0b[n];
           if (nslot >= 2) bs1 = a.s1b[n];
         }
-        opt_update(a.opt, lr, bw, v * a.scale, bs0, bs1);
+        if (a.gW) bw = v * a.scale;
+        else opt_update(a.opt, lr, bw, v * a.scale, bs0, bs1);
         if (u != wave) {                                   // the first column is stored late
-          a.bias[n] = bw;
+          (a.gW ? a.gb : a.bias)[n] = bw;
           if (nslot >= 1) a.s0b[n] = bs0;
           if (nslot >= 2) a.s1b[n] = bs1;
         }
@@ -535,6 +542,10 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
 
 using namespace csa;
 
+// gradient-mode outputs of the next launch (set by csa_dense_bwd_grad_head only)
+static float* g_du_grad_w = nullptr;
+static float* g_du_grad_b = nullptr;
+
 CSA_API int csa_du_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_du_dbg), &p, sizeof(p));
 }
@@ -612,6 +623,15 @@ CSA_API int csa_dense_bwd_update(const float* dY, float* W, float* bias, float* 
                                    nullptr, nullptr, 1, 1.f, 0, 0.f, st);
 }
 
+CSA_API int csa_dense_bwd_grad_head(const float* dY, const float* W, float* dX, int M, int K, int N,
+                                    const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
+                                    int bn_C, float bn_count, float bn_eps, const float* bn_scale,
+                                    const float* bn_offset, float* bwd_slab, const float* Xw, float scale,
+                                    const float* bn_tab, float* part, unsigned* cnt, float* gW, float* gb,
+                                    const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
+                                    const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
+                                    int hact, float halpha, const int64_t* step, hipStream_t st);
+
 // ... plus the head epilogue (hy != null): dWh / dbh of the row-per-workgroup head and the
 // step's metric ring entry are reduced by this launch (see DUArgs).
 CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, float* dX, int M, int K, int N,
@@ -639,9 +659,10 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
   a.hy = hy; a.hdl = hdl; a.hgw = hgw; a.hgb = hgb; a.hrl = hrl; a.hrc = hrc;
   a.ring_loss = ring_loss; a.ring_correct = ring_correct; a.ring = ring; a.ldiv = ldiv;
   a.hact = hact; a.halpha = halpha;
+  a.gW = g_du_grad_w; a.gb = g_du_grad_b;
   if (a.cs > 1 && dX && (!part || !cnt)) return -2;
   const int blocks = groups * a.cs;
-  const int ns = opt_nslots(opt);
+  const int ns = a.gW ? 0 : opt_nslots(opt);
   if (a.cs == 1) {
     if (ns == 0) du_launch<0, 16>(a, blocks, st);
     else if (ns == 1) du_launch<1, 16>(a, blocks, st);
@@ -652,4 +673,27 @@ CSA_API int csa_dense_bwd_update_head(const float* dY, float* W, float* bias, fl
     else du_launch<2, 4>(a, blocks, st);
   }
   return (int)hipGetLastError();
+}
+
+// Data-parallel form: the same fused launch (input gradient + transform backward + BN
+// statistics + the head epilogue) with the weight / bias GRADIENTS stored whole into
+// gW / gb instead of the in-kernel update — the gradient must be all-reduced first.
+CSA_API int csa_dense_bwd_grad_head(const float* dY, const float* W, float* dX, int M, int K, int N,
+                                    const float* x_fwd, int act, float alpha, const float* bn_slab, int bn_nslab,
+                                    int bn_C, float bn_count, float bn_eps, const float* bn_scale,
+                                    const float* bn_offset, float* bwd_slab, const float* Xw, float scale,
+                                    const float* bn_tab, float* part, unsigned* cnt, float* gW, float* gb,
+                                    const float* hy, const float* hdl, float* hgw, float* hgb, const float* hrl,
+                                    const int* hrc, float* ring_loss, int* ring_correct, int ring, float ldiv,
+                                    int hact, float halpha, const int64_t* step, hipStream_t st) {
+  if (!gW || !gb) return -2;
+  g_du_grad_w = gW;
+  g_du_grad_b = gb;
+  const int rc = csa_dense_bwd_update_head(dY, const_cast<float*>(W), nullptr, dX, M, K, N, x_fwd, act, alpha,
+                                           bn_slab, bn_nslab, bn_C, bn_count, bn_eps, bn_scale, bn_offset,
+                                           bwd_slab, Xw, OPT_SGD, 0.f, step, nullptr, nullptr, nullptr, nullptr,
+                                           scale, bn_tab, part, cnt, hy, hdl, hgw, hgb, hrl, hrc, ring_loss,
+                                           ring_correct, ring, ldiv, hact, halpha, st);
+  g_du_grad_w = g_du_grad_b = nullptr;
+  return rc;
 }

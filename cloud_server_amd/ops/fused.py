@@ -56,6 +56,8 @@ _SIGS = {
     "csa_dense_bwd_update": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
                                  P, P, P, P, F, P, P, P, P]),
     "csa_dense_bwd_update_ws": (I, [I, I, P]),
+    "csa_dense_bwd_grad_head": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, F, P, P, P, P, P,
+                                    P, P, P, P, P, P, P, P, I, F, I, F, P, P]),
     "csa_dense_bwd_update_head": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
                                       P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, I, F, P]),
     "csa_head_row_ok": (I, [I, I]),

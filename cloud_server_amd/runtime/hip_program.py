@@ -308,16 +308,19 @@ class HipProgram:
         layer's backward becomes ``csa_dense_bwd_update`` (dgrad + wgrad + the optimizer
         update of its W rows in one launch, dense_update.hip) and the head writes
         per-row-group partial gradients + metrics that the (now small) optimizer launch
-        folds (``csa_head_part``).  Data parallel keeps the materialised gradients: they
-        must be all-reduced before any update."""
+        folds (``csa_head_part``).  Data parallel (all-reduce / ps) runs the SAME fused
+        launch in gradient mode (``csa_dense_bwd_grad_head``): the dense weight / bias
+        gradients are stored whole into the flat gradient for the all-reduce and the flat
+        optimizer updates them (``fused_grad``); lowrank forms them from gathered operands."""
         e, B = self.e, self.B
-        self.fused = (not e.ctx.enabled and not self.forward_only
-                      and os.environ.get("CSA_FUSED_UPDATE", "1") == "1")
+        on = os.environ.get("CSA_FUSED_UPDATE", "1") == "1" and not self.forward_only
+        self.fused = on and not e.ctx.enabled
+        self.fused_grad = on and e.ctx.enabled and e.sync.strategy in ("allreduce", "ps")
         # measured on MI355X (profiles/r2_dense_fused.md): the row-group kernel (one
         # 1024-thread workgroup per 16 input features) replaces fc1's split-K pair + its
         # share of the flat optimizer (bench 0.1166 -> 0.1107 ms/step); CSA_FUSED_DENSE=0
         # restores the separate kernels
-        fuse_dense = self.fused and os.environ.get("CSA_FUSED_DENSE", "1") == "1"
+        fuse_dense = (self.fused or self.fused_grad) and os.environ.get("CSA_FUSED_DENSE", "1") == "1"
         for u in self.units:
             u.fused = False
             if not fuse_dense or u.kind != "dense":
@@ -336,15 +339,17 @@ class HipProgram:
         self.head_rg = 0
         self.head_row = False
         self.head_sep = False
-        if not self.fused and not self.forward_only and self.head_tf.norm is None:
-            # data parallel (or the unfused program): the row-per-workgroup head, its weight
-            # gradient as a register-direct wgrad launch (dWh = act(h)^T dlogits) into the flat
-            # gradient before the all-reduce, its metrics folded by the optimizer launch
-            # (the atomic 4-workgroup head took 15.6 us per DP step)
-            last = self.units[-1]
+        last = self.units[-1]
+        if (not self.fused and not self.forward_only and self.head_tf.norm is None
+                and not (self.fused_grad and last.kind == "dense" and last.fused)):
+            # data parallel without a fused last dense layer (lowrank, or the unfused
+            # program): the row-per-workgroup head, its weight gradient as a register-direct
+            # wgrad launch (dWh = act(h)^T dlogits) into the flat gradient before the
+            # all-reduce, its metrics folded by the optimizer launch (the atomic
+            # 4-workgroup head took 15.6 us per DP step)
             if last.kind == "dense" and self.lib.csa_head_row_ok(B, last.layer.spec.hidden):
                 self.head_row = self.head_sep = True
-        if self.fused and self.head_tf.norm is None:
+        if (self.fused or self.fused_grad) and self.head_tf.norm is None and not self.head_sep:
             last = self.units[-1]
             K = last.layer.spec.hidden if last.kind == "dense" else last.layer.out_shape.numel
             if last.kind == "conv" and last.pool is not None:
@@ -353,7 +358,7 @@ class HipProgram:
             # ride in the last dense layer's fused backward (csa_head_row + the head epilogue
             # of csa_dense_bwd_update_head) — no partial rows for the optimizer to fold
             self.head_row = last.kind == "dense" and last.fused and bool(self.lib.csa_head_row_ok(B, K))
-            if not self.head_row:
+            if not self.head_row and self.fused:
                 self.head_rg = int(self.lib.csa_head_part_rows(B, K))
         # register-direct MFMA dense forward (dense_direct.hip); the backward of a dense layer
         # is the fused backward + update (one GPU), the LDS-staged dgrad + wgrad pair (data
@@ -931,6 +936,8 @@ class HipProgram:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
                 if u.fused:
                     self._dense_bwd_update(u, prev, st)
+                    if self.fused_grad:
+                        self._grad_ready(k)
                     continue
                 if (prev is not None and u not in self.lr_units
                         and self._dense_bwd_fused(u, prev, st)):
@@ -1344,6 +1351,16 @@ class HipProgram:
                     _act_id(self.head_tf.act), _alpha(self.head_tf.act))
         else:
             head = (None, None, None, None, None, None, None, None, 1, 1.0, 0, 0.0)
+        if self.fused_grad:
+            # data parallel: the same launch stores dW / db whole into the flat gradient
+            G = self.gviews
+            self._rc(lib.csa_dense_bwd_grad_head(
+                K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(prev.dy) if prev is not None else None,
+                B, fin, fout, K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
+                K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), 1.0, K.ptr(getattr(tf, "bn_tab", None)),
+                K.ptr(u.du_part), K.ptr(u.du_cnt), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
+                *head, K.ptr(e.dstep), st), "dense_bwd_grad")
+            return
         self._rc(lib.csa_dense_bwd_update_head(
             K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
             K.ptr(prev.dy) if prev is not None else None, B, fin, fout,
@@ -1367,7 +1384,7 @@ class HipProgram:
         ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
         skip = set()
         for u in self.units:
-            if u.kind == "dense" and (u.fused or u.lr_update):
+            if u.kind == "dense" and ((u.fused and self.fused) or u.lr_update):
                 skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
         if not skip:
             return []

@@ -93,15 +93,19 @@ def test_lowrank_strategy_matches_single_gpu(pg, monkeypatch):
 def test_ps_and_rccl_programs_match_single_gpu(pg, monkeypatch, strategy, xgmi):
     """The parameter-server capability (``ps``: reduce-scatter -> owner optimizer on its
     shard -> all-gather, the reference's PS placement) and the all-reduce program on plain
-    RCCL, on the HIP program with the row-per-workgroup head and the striped pair
-    gradients; world 1 must reproduce the single-GPU step (20 steps, 8-step graphs)."""
+    RCCL, on the HIP program with the fused dense backward in gradient mode, the
+    row-per-workgroup head and the striped pair gradients; world 1 must reproduce the
+    single-GPU step (20 steps, 8-step graphs)."""
     monkeypatch.setenv("CSA_XGMI", xgmi)
     cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3))
     ds = synthetic_mnist(2000, seed=0)
     ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
     a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
     assert a.backend == "hip", a.fallback_reason
-    assert a.program.head_row and a.program.head_sep
+    # the fused dense backward in gradient mode (dW / db stored whole into the flat
+    # gradient for the exchange) with the row head's reductions in fc2's epilogue
+    assert a.program.fused_grad and all(u.fused for u in a.program.units[2:])
+    assert a.program.head_row and not a.program.head_sep
     assert a.program.units[0].row_fold and a.program.units[0].wg_stripes == 16
     b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
     for _ in range(4):
