@@ -31,7 +31,8 @@ class Recorder:
 
     def __getattr__(self, name):
         fn = getattr(self.lib, name)
-        if not name.startswith("csa_") or name.endswith(("_splits", "_slabs", "_nslab", "_ws", "_ok", "_rows")):
+        if (not name.startswith("csa_") or name.endswith(("_splits", "_slabs", "_nslab", "_ws", "_ok", "_rows", "_grid"))
+                or name.startswith("csa_set_") or name in ("csa_deterministic", "csa_packed")):
             return fn
 
         def wrapped(*args):

@@ -47,7 +47,9 @@ def main():
         m = re.match(r"\s*(\d+)\s+(csa_\w+)\s+([\d.]+) us", line)
         if m:
             times.append((int(m.group(1)), m.group(2), float(m.group(3))))
-    kmap = {"csa_conv_pair_fwd": "conv_pair_fwd_kernel", "csa_conv_pair_bwd": "conv_pair_bwd_kernel",
+    kmap = {"csa_conv_pair_fwd": "cpv_fwd_kernel", "csa_conv_pair_bwd": "conv_pair_bwd_kernel",
+            "csa_head_row": "head_row_kernel", "csa_dense_bwd_update_head": "dense_bwd_update_kernel",
+            "csa_dense_bwd_grad_head": "dense_bwd_update_kernel",
             "csa_bn_act_apply": "bn_act_apply_kernel", "csa_dense_fwd": "gemm_f32_kernel",
             "csa_head_part": "head_part_kernel", "csa_head_part2": "head_part_kernel", "csa_dense_bwd": "gemm_pair_kernel",
             "csa_optimizer2": "optim_kernel", "csa_optimizer2s": "optim_kernel", "csa_dd_fwd": "dd_fwd_kernel", "csa_dd_dgrad": "dd_dgrad_kernel",
