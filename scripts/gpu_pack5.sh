@@ -1,5 +1,5 @@
 #!/bin/bash
-# Packed curve with the packed-kernel defaults (prefer_packed_kernels).
+# Packed curve (bench.py --jobs K builds its engines with the packed launch profile).
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 for K in 2 4 8; do
   timeout -k 10 240 python bench.py --jobs $K --pack graph --steps 2000 --warmup 200 > gpurun_out/p5_$K.json 2> gpurun_out/pack_err.log || exit 7
