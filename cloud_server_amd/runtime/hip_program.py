@@ -432,7 +432,7 @@ class HipProgram:
         if not self.head_row:
             raise Unsupported("deterministic mode: head outside the row-per-workgroup family")
 
-    def _det_fold(self, t: torch.Tensor, rows: int, width: int, dst: torch.Tensor, zero_src: int, st) -> None:
+    def _row_fold(self, t: torch.Tensor, rows: int, width: int, dst: torch.Tensor, zero_src: int, st) -> None:
         """dst[:width] = fixed-order sum of the first ``rows`` rows of ``t`` (row stride width)."""
         self._rc(self.lib.csa_rows_fold(K.ptr(t), width, rows, width, K.ptr(dst), zero_src, st), "rows_fold")
 
@@ -1057,7 +1057,7 @@ class HipProgram:
                 _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
                 nt.prod_rows if self.det else self.lib.csa_conv_fwd_nslab(None, None), st), "conv_pair_fwd")
             if oslab is not None and self.det:
-                self._det_fold(oslab, nt.prod_rows, oslab.shape[1] * oslab.shape[2], oslab, 0, st)
+                self._row_fold(oslab, nt.prod_rows, oslab.shape[1] * oslab.shape[2], oslab, 0, st)
             if oslab is not None and self.sync_bn:
                 e.sync.allreduce_tensors([oslab], tag="bnf1")
         for k, u in enumerate(self.units):
@@ -1273,9 +1273,9 @@ class HipProgram:
         if ua.row_fold:
             for u in (ua, ub):
                 lp = u.layer
-                self._det_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
+                self._row_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
                 if u.db_acc is not None:
-                    self._det_fold(u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"], 1, st)
+                    self._row_fold(u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"], 1, st)
 
     def _route_geom(self, u: Unit):
         lp, B = u.layer, self.B
@@ -1371,7 +1371,7 @@ class HipProgram:
             1.0, K.ptr(getattr(tf, "bn_tab", None)), K.ptr(u.du_part), K.ptr(u.du_cnt), *head, st),
             "dense_bwd_update")
         if self.det and tf.has_bn:
-            self._det_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],
+            self._row_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],
                            tf.bwd_slab, 0, st)
 
     def _opt_segments(self):
