@@ -927,28 +927,31 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
   __syncthreads();
   CP_STAMP(1);
   // ---- conv A: the c1 tile [T1H][T1W][C1] (zero outside [0, H1) x [0, W1)): one thread
-  // per tile pixel, its KA input values in registers, channel pairs as float2 weight reads
+  // per (tile pixel, channel pair) — all 256 threads busy (one thread per pixel left 2/3 of
+  // them idle behind a C1/2-long chain) — tap offsets held in registers
   float* s_c1 = smem;
   const int npx1 = t.T1H * t.T1W;
-  for (int pix = tid; pix < npx1; pix += CPV_T) {
-    const int tx = pix % t.T1W, ty = pix / t.T1W;
-    const int yy = t.c1y0 + ty, xx = tx - g.PLB;
-    const bool in = yy >= 0 && yy < g.H1 && xx >= 0 && xx < g.W1;
-    const float* xb = s_x + (ty * t.TXW + tx) * g.C0;
-    float xk[CPV_MAXKA];
+  {
+    int koff[CPV_MAXKA];
 #pragma unroll
-    for (int k = 0; k < CPV_MAXKA; ++k) xk[k] = k < KA ? xb[s_koffA[k]] : 0.f;
-    float* out = s_c1 + pix * g.C1;
-    for (int c1 = 0; c1 < g.C1; c1 += 2) {
+    for (int k = 0; k < CPV_MAXKA; ++k) koff[k] = k < KA ? s_koffA[k] : 0;
+    const int nc1p = g.C1 >> 1;
+    for (int it = tid; it < npx1 * nc1p; it += CPV_T) {
+      const int cp = it % nc1p, pix = it / nc1p, c1 = 2 * cp;
+      const int tx = pix % t.T1W, ty = pix / t.T1W;
+      const int yy = t.c1y0 + ty, xx = tx - g.PLB;
+      const bool in = yy >= 0 && yy < g.H1 && xx >= 0 && xx < g.W1;
+      const float* xb = s_x + (ty * t.TXW + tx) * g.C0;
       float a0 = s_b[c1], a1 = s_b[c1 + 1];
 #pragma unroll
       for (int k = 0; k < CPV_MAXKA; ++k) {
-        if (k >= KA) break;                               // uniform
+        if (k >= KA) break;                                 // uniform
+        const float xv = xb[koff[k]];
         const float2 w = *reinterpret_cast<const float2*>(s_w + k * g.C1 + c1);
-        a0 = fmaf(xk[k], w.x, a0);
-        a1 = fmaf(xk[k], w.y, a1);
+        a0 = fmaf(xv, w.x, a0);
+        a1 = fmaf(xv, w.y, a1);
       }
-      *reinterpret_cast<float2*>(out + c1) =
+      *reinterpret_cast<float2*>(s_c1 + pix * g.C1 + c1) =
           in ? make_float2(act_fwd(a0, a.actA, a.alphaA), act_fwd(a1, a.actA, a.alphaA)) : make_float2(0.f, 0.f);
     }
   }
@@ -1021,14 +1024,23 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
   (void)nout;
   CP_STAMP(3);
   if (a.stat) {                                           // per-channel sums, fixed order
+    // (column, unit slice) per thread, slices combined in order
+    __shared__ float s_sp[CPV_T];
     __syncthreads();
-    if (tid < 2 * g.C2) {
-      const int c = tid % g.C2, sq = tid / g.C2;
+    const int cols = 2 * g.C2, nsl = max(1, CPV_T / cols), per = (nunit + nsl - 1) / nsl;
+    if (tid < cols * nsl) {
+      const int col = tid % cols, sl = tid / cols, c = col % g.C2, sq = col / g.C2;
       float acc = 0.f;
-      for (int u = 0; u < nunit; ++u) {
+      for (int u = sl * per; u < min(nunit, (sl + 1) * per); ++u) {
         const float v = s_out[u * g.C2 + c];
         acc += sq ? v * v : v;
       }
+      s_sp[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < cols) {
+      float acc = 0.f;
+      for (int sl = 0; sl < nsl; ++sl) acc += s_sp[sl * cols + tid];
       float* row = a.stat + (size_t)(blockIdx.x % a.nslab) * 2 * g.C2;
       if (a.nslab >= (int)gridDim.x) row[tid] = acc;           // one row per workgroup
       else atomicAdd(&row[tid], acc);
