@@ -739,11 +739,12 @@ class HipProgram:
         self.keep_ranges = []
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind != "dense" or u.fused or u.lr_update:
-                continue
+            if u.kind != "dense" or (u.fused and self.fused) or u.lr_update:
+                continue                         # (updated in-kernel: no gradient in memory)
             fin, fout = u.layer.in_shape.numel, u.layer.spec.hidden
             m = B * (self.e.ctx.world if u in getattr(self, "lr_units", []) else 1)
-            if self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
+            # the fused backward in gradient mode stores dW / db whole every step
+            if (u.fused and self.fused_grad) or self.lib.csa_dense_wgrad_splits(m, fin, fout) == 1:
                 for p in ("weight", "bias"):
                     n = f"{u.layer.name}.{p}"
                     lo = offs[n]
