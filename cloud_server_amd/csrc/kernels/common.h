@@ -17,12 +17,14 @@ namespace csa {
 
 enum Act : int { ACT_NONE = 0, ACT_SIGMOID = 1, ACT_RELU = 2, ACT_LEAKY = 3 };
 
-// Deterministic mode (det.hip, host state): launch helpers choose exclusive destinations
-// and no split-K, so no float atomic has more than one contributor per slot.
-extern int g_csa_det;
+// Deterministic mode (det.hip, host state of the CALLING thread: a job planned on a builder
+// thread never changes the launch shapes of a job stepping on another): launch helpers
+// choose exclusive destinations and no split-K, so no float atomic has more than one
+// contributor per slot.
+extern thread_local int g_csa_det;
 // Packed profile (det.hip, host state): a process that packs several jobs onto one GPU
 // prefers launch shapes with less CU-time per job-step over the lowest latency alone.
-extern int g_csa_packed;
+extern thread_local int g_csa_packed;
 
 __device__ __forceinline__ float act_fwd(float x, int act, float alpha) {
   switch (act) {

@@ -542,9 +542,9 @@ __global__ __launch_bounds__(64 * WAVES) void dense_bwd_update_kernel(DUArgs a) 
 
 using namespace csa;
 
-// gradient-mode outputs of the next launch (set by csa_dense_bwd_grad_head only)
-static float* g_du_grad_w = nullptr;
-static float* g_du_grad_b = nullptr;
+// gradient-mode outputs of the next launch on this thread (set by csa_dense_bwd_grad_head only)
+static thread_local float* g_du_grad_w = nullptr;
+static thread_local float* g_du_grad_b = nullptr;
 
 CSA_API int csa_du_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_du_dbg), &p, sizeof(p));

@@ -14,14 +14,14 @@
 //     then the slices in order) — the result depends only on the data, never on timing;
 //   * every reduction INSIDE a workgroup on those paths is already fixed-order.
 //
-// The flag is process state read by the launch-configuration helpers (split-K factors,
-// slab row counts); the step program sets it around its own planning and launches.
+// The flag is per-thread host state read by the launch-configuration helpers (split-K
+// factors, slab row counts); the step program sets it around its own planning and launches.
 #include "common.h"
 
 namespace csa {
 
-int g_csa_det = 0;
-int g_csa_packed = 0;
+thread_local int g_csa_det = 0;
+thread_local int g_csa_packed = 0;
 
 constexpr int RF_COLS = 64;      // columns per workgroup
 constexpr int RF_SL = 4;         // row slices per column (one per wave)

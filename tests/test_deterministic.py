@@ -126,3 +126,29 @@ def test_deterministic_hip_matches_torch_and_fast_path(monkeypatch):
             b = e_det.model.state.view(k, other)
             scale = b.abs().max().item() + 1e-6
             assert (a - b).abs().max().item() <= tol * scale + 1e-6, k
+
+
+def test_launch_profile_flags_are_per_thread():
+    """The deterministic / packed launch-profile flags are host state of the calling thread:
+    a job planned or warmed up on the packed host's builder thread never changes the launch
+    shapes of the jobs stepping on the main thread (runs on CPU: host-only library calls)."""
+    import threading
+    from cloud_server_amd.ops import fused as K
+
+    lib = K.load(required=False)
+    if lib is None:
+        pytest.skip("kernel library not built")
+    lib.csa_set_deterministic(0)
+    lib.csa_set_packed(0)
+    seen = {}
+
+    def other():
+        lib.csa_set_deterministic(1)
+        lib.csa_set_packed(1)
+        seen["other"] = (lib.csa_deterministic(), lib.csa_packed())
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen["other"] == (1, 1)
+    assert (lib.csa_deterministic(), lib.csa_packed()) == (0, 0)
