@@ -545,7 +545,7 @@ __global__ __launch_bounds__(256) void head_part_kernel(HeadPartArgs a) {
 // before any parameter update of the step reads it.
 // ---------------------------------------------------------------------------------
 constexpr int HR_T = 256;
-constexpr int HR_KPT = 4;               // k per thread: K <= 1024
+constexpr int HR_KPT = 4;               // k per thread at most: K <= 1024
 
 struct HeadRowArgs {
   const float* h; int M, K; int in_act; float in_alpha;
@@ -556,6 +556,8 @@ struct HeadRowArgs {
   int64_t* step; int64_t* adv_cursor; long wrap;
 };
 
+// KPT = k per thread, the smallest that covers K (no clamped duplicate loads of Wh rows)
+template <int KPT>
 __global__ __launch_bounds__(HR_T) void head_row_kernel(HeadRowArgs a) {
   __shared__ float s_part[HR_T / 64][NCLS];
   __shared__ float s_dl[NCLS];
@@ -570,9 +572,9 @@ __global__ __launch_bounds__(HR_T) void head_row_kernel(HeadRowArgs a) {
   }
   // every load first: this thread's h values and Wh rows (clamped addresses), the bias
   // and the row's label (the label chain runs under the h / Wh loads)
-  float hv[HR_KPT], wv[HR_KPT][NCLS];
+  float hv[KPT], wv[KPT][NCLS];
 #pragma unroll
-  for (int u = 0; u < HR_KPT; ++u) {
+  for (int u = 0; u < KPT; ++u) {
     const int k = min(u * HR_T + tid, K - 1);
     hv[u] = a.h[(long)m * K + k];
 #pragma unroll
@@ -591,7 +593,7 @@ __global__ __launch_bounds__(HR_T) void head_row_kernel(HeadRowArgs a) {
 #pragma unroll
   for (int j = 0; j < NCLS; ++j) acc[j] = 0.f;
 #pragma unroll
-  for (int u = 0; u < HR_KPT; ++u) {
+  for (int u = 0; u < KPT; ++u) {
     const bool ok = u * HR_T + tid < K;
     hv[u] = ok ? act_fwd(hv[u], a.in_act, a.in_alpha) : 0.f;     // post-activation value
 #pragma unroll
@@ -640,7 +642,7 @@ __global__ __launch_bounds__(HR_T) void head_row_kernel(HeadRowArgs a) {
 #pragma unroll
   for (int j = 0; j < NCLS; ++j) dl[j] = s_dl[j];
 #pragma unroll
-  for (int u = 0; u < HR_KPT; ++u) {
+  for (int u = 0; u < KPT; ++u) {
     const int k = u * HR_T + tid;
     if (k >= K) break;
     float g = 0.f;
@@ -733,7 +735,9 @@ CSA_API int csa_head_row(const float* h, int M, int K, int in_act, float in_alph
   if (!csa_head_row_ok(M, K) || !dh || !dl || !rloss || !rcorr) return -1;
   HeadRowArgs a{h, M, K, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, dl, rloss, rcorr,
                 step, adv_cursor, wrap};
-  hipLaunchKernelGGL(head_row_kernel, dim3((unsigned)M), dim3(HR_T), 0, st, a);
+  if (K <= HR_T) hipLaunchKernelGGL(head_row_kernel<1>, dim3((unsigned)M), dim3(HR_T), 0, st, a);
+  else if (K <= 2 * HR_T) hipLaunchKernelGGL(head_row_kernel<2>, dim3((unsigned)M), dim3(HR_T), 0, st, a);
+  else hipLaunchKernelGGL(head_row_kernel<HR_KPT>, dim3((unsigned)M), dim3(HR_T), 0, st, a);
   return (int)hipGetLastError();
 }
 
