@@ -142,20 +142,21 @@ __device__ __forceinline__ void slab_sum_to_lds(const float* slab, int nslab, in
   if (per > 0) {
     const int col = threadIdx.x % C2, lane_row = threadIdx.x / C2;
     if (lane_row < per) {
-      // batches of 8 loads in flight per thread (a load -> add chain is one memory round
-      // trip per row)
+      // batches of 16 loads in flight per thread (a load -> add chain is one memory round
+      // trip per row; a 32-row slab over 2 threads per column is then ONE round trip)
+      constexpr int U = 16;
       float acc = 0.f;
-      for (int r0 = lane_row; r0 < nslab; r0 += 8 * per) {
-        float v[8];
+      for (int r0 = lane_row; r0 < nslab; r0 += U * per) {
+        float v[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int r = r0 + u * per;
           v[u] = slab[(size_t)(r < nslab ? r : 0) * C2 + col];
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pin(v[u]);
+        for (int u = 0; u < U; ++u) pin(v[u]);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc += (r0 + u * per < nslab) ? v[u] : 0.f;
+        for (int u = 0; u < U; ++u) acc += (r0 + u * per < nslab) ? v[u] : 0.f;
       }
       atomicAdd(&s_out[col], acc);
     }
