@@ -21,7 +21,7 @@ from __future__ import annotations
 import math
 import os
 import time
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -139,6 +139,7 @@ class TrainEngine:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.graph = None
         self.graph_k = None      # CSA_GRAPH_STEPS steps captured in one graph (run_steps)
+        self.graphs_k: Dict[int, object] = {}   # every multi-step size (group_sizes)
         self.warmed = False      # _warm_up ran (a packed host re-captures without it)
 
     # ---------------- pieces used by the programs (device ops only) ----------------
@@ -188,10 +189,8 @@ class TrainEngine:
         ``device_sync=False``: wait for this engine's streams only (a packed host builds a
         job on a builder thread while the hosted jobs keep stepping)."""
         s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        saved = (self.flat.clone(), self.slots.clone(), self.dstep.clone(),
-                 self.stream.cursor.clone())
-        bufs = [(b, b.clone()) for b in self.model.buffers()]     # BN running statistics
+        snap = self._snapshot()     # parameters, slots, counters, BN running statistics
+        s.wait_stream(torch.cuda.current_stream(self.device))     # (after the clones)
         with torch.cuda.stream(s):
             for _ in range(2):      # warm up allocator / autotuning / RCCL comms off-graph
                 self.program.run()
@@ -201,11 +200,7 @@ class TrainEngine:
         else:
             s.synchronize()
         # undo the warm-up's effect on the model state
-        self.flat.copy_(saved[0]); self.slots.copy_(saved[1])
-        self.dstep.copy_(saved[2]); self.stream.cursor.copy_(saved[3])
-        for b, v in bufs:
-            b.copy_(v)
-        self.program.reset_after_warmup() if hasattr(self.program, "reset_after_warmup") else None
+        self._restore(snap)
         self.warmed = True
 
     def _capture(self) -> None:
@@ -241,32 +236,76 @@ class TrainEngine:
             return 1
         return k if (self.use_graph and k > 1) else 1
 
-    def prepare_group_graph(self) -> None:
-        """Capture the k-step graph now (capture does not execute; call after the first
-        step so a timed loop never includes a capture)."""
+    def group_sizes(self) -> List[int]:
+        """Multi-step graph sizes, largest first: k, k/2, ..., 2 (k = ``group_steps``), so
+        any ``n`` decomposes into at most one replay per size plus whole k-groups."""
         k = self.group_steps()
-        if k > 1 and self.graph is not None and self.graph_k is None:
+        sizes = []
+        while k > 1:
+            sizes.append(k)
+            k //= 2
+        return sizes
+
+    def _snapshot(self):
+        """Model / optimizer / stream state a throw-away replay must not change."""
+        return ((self.flat.clone(), self.slots.clone(), self.dstep.clone(), self.stream.cursor.clone()),
+                [(b, b.clone()) for b in self.model.buffers()])
+
+    def _restore(self, snap) -> None:
+        (flat, slots, dstep, cursor), bufs = snap
+        self.flat.copy_(flat); self.slots.copy_(slots)
+        self.dstep.copy_(dstep); self.stream.cursor.copy_(cursor)
+        for b, v in bufs:
+            b.copy_(v)
+        if hasattr(self.program, "reset_after_warmup"):
+            self.program.reset_after_warmup()
+
+    def prepare_group_graph(self) -> None:
+        """Capture every multi-step graph now (``group_sizes``: k, k/2, .., 2 steps each) and
+        replay each ONCE with the model state restored afterwards, so neither a capture nor
+        a graph's first launch (its upload to the device) ever lands in a timed loop.  Call
+        after the first step (the single-step graph is then captured and replayed)."""
+        if self.graph is None or self.graph_k is not None:
+            return
+        graphs = {}
+        for k in self.group_sizes():
             g = torch.cuda.CUDAGraph()
             with capture(g):
                 for _ in range(k):
                     self.program.run()
-            self.graph_k = g
+            graphs[k] = g
+        if not graphs:
+            return
+        self.graphs_k = graphs
+        self.graph_k = graphs[max(graphs)]
+        # warm replay: the device must not be reading the row table's halves the host
+        # refills meanwhile, so drain first; every rank replays the same graphs (collectives
+        # inside them stay matched)
+        self.sync_device()
+        snap = self._snapshot()
+        for k in sorted(graphs, reverse=True):
+            graphs[k].replay()
+        self.sync_device()
+        self._restore(snap)
+        self.sync_device()
 
     def run_steps(self, n: int) -> None:
         """``n`` training steps.  With a captured single-GPU program, groups of
         ``CSA_GRAPH_STEPS`` (default 8) steps replay ONE graph holding that many steps:
         one launch instead of k.  Bench on MI355X (scripts/gpu_sweep.sh): 0.108 ms/step
-        ungrouped, 0.1045 at k = 4, 0.1035 at k = 8, 0.1034 at k = 16.  Groups never straddle a half of the batch row
-        table (BatchStream.can_group); the remainder runs step by step, so exactly ``n``
-        steps execute."""
-        k = self.group_steps()
+        ungrouped, 0.1045 at k = 4, 0.1035 at k = 8, 0.1034 at k = 16.  The remainder
+        ``n mod k`` replays the k/2, k/4, .. 2-step graphs, so at most one step runs as a
+        single-step replay.  Groups never straddle a half of the batch row table
+        (BatchStream.can_group); exactly ``n`` steps execute."""
+        sizes = self.group_sizes() if self.graph is not None else []
         while n > 0:
-            if k > 1 and n >= k and self.graph is not None and self.stream.can_group(k):
+            k = next((s for s in sizes if s <= n and self.stream.can_group(s)), 1)
+            if k > 1:
                 self.prepare_group_graph()
                 with trace_range("csa.steps"):
                     for _ in range(k):
                         self.stream.before_step()
-                    self.graph_k.replay()
+                    self.graphs_k[k].replay()
                 self.host_step += k
                 n -= k
             else:

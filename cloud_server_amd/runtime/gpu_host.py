@@ -90,6 +90,17 @@ def _build_job(req: dict, device: str, backend: str, lock: threading.Lock):
     return job
 
 
+def _drain(device: str) -> None:
+    """Wait until the device is idle.  Called before the host drops its last reference to a
+    job's engine (retire / fail) or to the packed graph: the engine's blocks were allocated
+    on its builder stream, and the caching allocator hands a freed block to the next user
+    of that (pooled) stream without ordering it after the packed replay still reading it
+    on the branch streams."""
+    import torch
+    if device.startswith("cuda") and torch.cuda.is_available():
+        torch.cuda.synchronize(torch.device(device))
+
+
 def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0.0,
           parent_pid: int = 0) -> int:
     from .multijob import PackedJobs
@@ -104,6 +115,7 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
     parent = parent_pid or os.getppid()     # the manager's launcher; if it dies we are orphaned
 
     def retire(jid: int, rc: int) -> None:
+        _drain(device)                      # nothing in flight still uses its memory
         jobs.pop(jid, None)
         _post_done(spool, jid, rc)
 

@@ -67,6 +67,23 @@ class PackedJobs:
                 cap.wait_stream(s)
         self.graph_k = g
 
+    def prepare_group_graph(self, k: int = 0) -> None:
+        """Capture the k-step multi-job graph now and replay it once with every job's state
+        restored afterwards (see TrainEngine.prepare_group_graph): a timed loop then never
+        pays the capture or the graph's first launch."""
+        import os
+        k = k or int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        if not self.cuda or k <= 1 or self.graph is None or self.graph_k is not None:
+            return
+        self._capture_group(k)
+        self.sync_device()
+        snaps = [e._snapshot() for e in self.engines]
+        self.graph_k.replay()
+        self.sync_device()
+        for e, s in zip(self.engines, snaps):
+            e._restore(s)
+        self.sync_device()
+
     def run_steps(self, n: int) -> None:
         """``n`` steps of every job: groups of CSA_GRAPH_STEPS steps as one multi-step
         graph where every job's group stays inside one half of its row table (see

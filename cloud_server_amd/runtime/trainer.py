@@ -254,8 +254,11 @@ class JobRun:
         # k steps as one multi-step graph launch (TrainEngine.run_steps) when no per-step
         # hook falls inside them: the group's LAST step may be a log point (after_step
         # handles it), earlier ones may not; fault / hang injection steps run alone
-        k = eng.group_steps() if eng.graph is not None else 1
-        if k > 1 and self.groupable(k):
+        # (the largest captured size that fits: k, k/2, .., 2 — a log point 4 steps away
+        # runs as one 4-step replay instead of four single-step ones)
+        sizes = eng.group_sizes() if eng.graph is not None else []
+        k = next((s for s in sizes if self.groupable(s)), 1)
+        if k > 1:
             eng.run_steps(k)
         else:
             eng.step()

@@ -20,16 +20,43 @@ from __future__ import annotations
 
 import contextlib
 import gc
+import threading
 from typing import Iterator, Optional
 
 import torch
+
+# the collector's enable flag is process state: captures on different threads overlap, so
+# it is switched off by the first capture to start and back on by the LAST one to end
+_lock = threading.Lock()
+_active = 0
+_was_enabled = False
+
+
+def _enter() -> None:
+    global _active, _was_enabled
+    with _lock:
+        if _active == 0:
+            _was_enabled = gc.isenabled()
+            gc.disable()
+        _active += 1
+
+
+def _exit() -> None:
+    global _active
+    with _lock:
+        _active -= 1
+        if _active == 0 and _was_enabled:
+            gc.enable()
+
+
+def active_captures() -> int:
+    return _active
 
 
 @contextlib.contextmanager
 def capture(graph: "torch.cuda.CUDAGraph", stream: Optional["torch.cuda.Stream"] = None,
             pool=None) -> Iterator[None]:
-    was = gc.isenabled()
-    gc.disable()
+    _enter()
     try:
         kw = {} if stream is None else {"stream": stream}
         if pool is not None:
@@ -37,5 +64,4 @@ def capture(graph: "torch.cuda.CUDAGraph", stream: Optional["torch.cuda.Stream"]
         with torch.cuda.graph(graph, capture_error_mode="thread_local", **kw):
             yield
     finally:
-        if was:
-            gc.enable()
+        _exit()

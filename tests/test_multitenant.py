@@ -141,3 +141,47 @@ def test_gpu_host_exits_when_orphaned(tmp_path):
     else:
         os.kill(pid, 9)
         raise AssertionError("orphaned gpu_host kept running")
+
+
+def test_gpu_host_drains_before_dropping_a_failed_job(tmp_path, monkeypatch):
+    """a job failing in after_step is dropped only after the device is
+    idle — its engine memory came from a pooled builder stream, so freeing it while the
+    last packed replay still runs would let the next build reuse live memory."""
+    import gc
+    import weakref
+    from cloud_server_amd.runtime import gpu_host
+    from cloud_server_amd.runtime.trainer import JobRun
+    s = _settings(tmp_path)
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    spool = tmp_path / "spool"
+    (spool / "inbox").mkdir(parents=True)
+    mdirs = [_prep_model(s, uid, f"m{i}", n=40) for i in range(2)]
+    for i, m in enumerate(mdirs):
+        with open(os.path.join(m, "model.json"), "w") as f:
+            json.dump(dict(SMALL, iter=12), f)
+        with open(spool / "inbox" / f"{i}.json", "w") as f:
+            json.dump({"jid": i, "model_dir": m, "datatype": "file"}, f)
+    engines = {}
+    calls = {"n": 0}
+    orig = JobRun.after_step
+
+    def after_step(self):
+        engines.setdefault(self.model_dir, weakref.ref(self.eng))
+        if self.model_dir == mdirs[0] and self.eng.host_step >= 3:
+            raise RuntimeError("injected after_step failure")
+        return orig(self)
+
+    drains = []
+
+    def drain(device):
+        gc.collect()
+        ref = engines.get(mdirs[0])
+        drains.append(ref is not None and ref() is not None)   # the failed engine still alive
+
+    monkeypatch.setattr(JobRun, "after_step", after_step)
+    monkeypatch.setattr(gpu_host, "_drain", drain)
+    assert gpu_host.serve(str(spool), "cpu", "torch", idle_exit_s=0.3) == 0
+    done = {int(n.split(".")[0]): json.load(open(spool / "done" / n))["rc"] for n in os.listdir(spool / "done")}
+    assert done == {0: 1, 1: 0}
+    assert drains and drains[0] is True          # drained while the failed job was still referenced

@@ -553,3 +553,37 @@ def test_job_manager_reserves_serving_slot(tmp_path):
         assert jm.reserve_serving(0) == 0            # would take the GPU's last slot
     finally:
         jm.shutdown()
+
+
+def test_capture_gc_guard_holds_across_overlapping_threads(monkeypatch):
+    """two captures on different threads overlap — the collector stays off until
+    the LAST one ends (a per-call save/restore re-enabled it under the other capture)."""
+    import contextlib
+    import gc
+    import threading
+    from cloud_server_amd.utils import graphs
+    monkeypatch.setattr(torch.cuda, "graph", lambda *a, **k: contextlib.nullcontext())
+    assert gc.isenabled() and graphs.active_captures() == 0
+    a_in, b_in, a_out = threading.Event(), threading.Event(), threading.Event()
+    seen = {}
+
+    def first():
+        with graphs.capture(object()):
+            a_in.set()
+            b_in.wait(10)
+        a_out.set()
+
+    def second():
+        a_in.wait(10)
+        with graphs.capture(object()):
+            b_in.set()
+            a_out.wait(10)
+            seen["after_first_ended"] = gc.isenabled()
+
+    ts = [threading.Thread(target=first), threading.Thread(target=second)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(20)
+    assert seen["after_first_ended"] is False
+    assert gc.isenabled() and graphs.active_captures() == 0
