@@ -24,6 +24,7 @@
 // (uint8 dataset rows gathered through the batch index stream).  Everything else uses the
 // per-layer kernels (conv.hip).
 #include "common.h"
+#include "dense_update.h"
 #include <cstdlib>
 #include <algorithm>
 
@@ -495,12 +496,11 @@ __host__ __device__ inline CPBwdLayout cp_bwd_layout(const CPGeom& g, int band, 
 constexpr int CPB_UP = 8, CPB_UX = 2, CPB_US = 8;
 
 template <bool ONE>
-__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, float* smem) {
   __shared__ float s_bn[4 * CP_MAXC2];
   __shared__ float s_ss[2 * CP_MAXC2];
   const CPGeom& g = a.g;
-  const int b = blockIdx.x / g.nbands, band = blockIdx.x % g.nbands;
+  const int b = bid / g.nbands, band = bid % g.nbands;
   const int pr0 = band * g.PR;
   const CPBand t0 = cp_band(g, 0, 0);
   (void)t0;
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
       __syncthreads();
       slab_sum_to_lds(a.bwd_slab, a.bwd_nslab, 2 * g.C2, s_ss);
     }
-    if (blockIdx.x == 0)
+    if (bid == 0)
       for (int c = threadIdx.x; c < g.C2; c += CP_THREADS) {
         a.doffset[c] = s_ss[c];
         a.dscale[c] = s_ss[g.C2 + c];
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
   CP_STAMP(14);
   // ---- one atomic per (workgroup, weight) into stripe blockIdx % S, in memory order
   {
-    const int sidx = blockIdx.x % a.stripes;
+    const int sidx = bid % a.stripes;
     const int nB = L.KB * g.C2;
     for (int o = threadIdx.x; o < nB; o += CP_THREADS) {
       const int tap = o / g.C2, c2 = o - tap * g.C2;
@@ -835,6 +835,45 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
       for (int o = threadIdx.x; o < g.C1; o += CP_THREADS) atomicAdd(&a.dbA[(long)sidx * g.C1 + o], s_bias[g.C2 + o]);
   }
   CP_STAMP(15);
+}
+
+template <bool ONE>
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cp_bwd_body<ONE>(a, (int)blockIdx.x, smem);
+}
+
+// Horizontal fusion (round 4): the pair backward's workgroups [0, B * nbands) followed by
+// the deferred dense weight-gradient + update segments (csa_dense_update_defer; 128-column
+// 256-thread workgroups of du_body, dX = null).  The pair backward is a latency chain that
+// leaves most CU cycles and memory bandwidth idle (3 % HBM, 8 % MFMA: profiles/
+// r3_roofline.md); the dense updates only have to finish before the next step's forward
+// of their layer, so they run inside this launch instead of as serial links of the chain.
+// The pair's workgroups come first: the dispatcher deals blocks in index order, so the
+// critical pair blocks all start before any update block takes a slot.
+struct CPUpd {
+  DUArgs seg[DU_MAXDEF];
+  int start[DU_MAXDEF + 1];          // segment s = extra blocks [start[s], start[s + 1])
+  int nseg, head;
+};
+
+template <bool ONE, int NSLOT>
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, CPUpd u) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int npair = a.g.B * a.g.nbands;
+  const int bid = (int)blockIdx.x;
+  if (bid < npair) {
+    cp_bwd_body<ONE>(a, bid, smem);
+    return;
+  }
+  const int e = bid - npair;
+  int s = 0;
+#pragma unroll
+  for (int k = 1; k < DU_MAXDEF; ++k) s += (k < u.nseg && e >= u.start[k]) ? 1 : 0;
+  const DUArgs& d = u.seg[s];
+  const int lb = e - u.start[s], nb = u.start[s + 1] - u.start[s];
+  if (s == u.head) du_body<NSLOT, 4, true, false, true>(d, lb, nb, smem);
+  else du_body<NSLOT, 4, false, false, true>(d, lb, nb, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1569,6 +1608,40 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
   return (int)hipGetLastError();
 }
 
+template <bool ONE, int NSLOT>
+static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const CPUpd& u, size_t lds, hipStream_t st) {
+  static const bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_upd_kernel<ONE, NSLOT>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
+  if (!attr) return -3;
+  const unsigned blocks = (unsigned)(a.g.B * a.g.nbands + u.start[u.nseg]);
+  hipLaunchKernelGGL((conv_pair_bwd_upd_kernel<ONE, NSLOT>), dim3(blocks), dim3(CP_THREADS), lds, st, a, u);
+  return (int)hipGetLastError();
+}
+
+// The MFMA pair backward carrying the deferred dense update segments (consumes them).
+static int cp_launch_bwd_upd(const CPBwdArgs& a, hipStream_t st) {
+  CPUpd u{};
+  u.nseg = g_du_def.n;
+  u.head = g_du_def.head;
+  u.start[0] = 0;
+  for (int s = 0; s < DU_MAXDEF; ++s) {
+    if (s < u.nseg) u.seg[s] = g_du_def.seg[s];
+    u.start[s + 1] = u.start[s] + (s < u.nseg ? g_du_def.blocks[s] : 0);
+  }
+  g_du_def.n = 0;
+  g_du_def.head = -1;
+  size_t lds = cp_lds(a.g, true);
+  const size_t dl = du_lds_floats(u.seg[0].M, 4) * sizeof(float);
+  for (int s = 1; s < u.nseg; ++s)
+    if (du_lds_floats(u.seg[s].M, 4) * sizeof(float) > dl) return -5;
+  if (dl > lds) lds = dl;
+  const int ns = opt_nslots(u.seg[0].opt);
+  const bool one = cp_bwd_one_batch(a);
+  if (ns == 0) return one ? cp_launch_bwd_upd_t<true, 0>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 0>(a, u, lds, st);
+  if (ns == 1) return one ? cp_launch_bwd_upd_t<true, 1>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 1>(a, u, lds, st);
+  return one ? cp_launch_bwd_upd_t<true, 2>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 2>(a, u, lds, st);
+}
+
 CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
@@ -1601,8 +1674,10 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
     if (!vattr) return -3;
     if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_bwd_kernel<2, 2>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
     else hipLaunchKernelGGL((cpv_bwd_kernel<3, 3>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
+    if (g_du_def.n > 0) return csa_dense_update_flush(st);     // deferred updates on their own
     return (int)hipGetLastError();
   }
+  if (g_du_def.n > 0) return cp_launch_bwd_upd(a, st);
   if (cp_bwd_one_batch(a))
     hipLaunchKernelGGL(conv_pair_bwd_kernel<true>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
   else

@@ -653,6 +653,205 @@ __global__ __launch_bounds__(HR_T) void head_row_kernel(HeadRowArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Head + the LAST dense layer's input gradient in ONE launch (round 4, horizontal-fusion
+// program).  The head's outputs per batch row (dlogits, loss, #correct, the head input
+// gradient dh) need nothing but that row, and the last dense layer's input gradient
+//   dX[m][f] = act'( sum_n dh[m][n] W[f][n] )           (W = [K1][Kh], this layer)
+// needs nothing but row m's dh — so a workgroup owning R rows x FS input features
+// recomputes the (tiny) head for its R rows and finishes dX for its features, with no
+// batch-wide reduction anywhere.  The dense layer's weight gradient + update and the head's
+// batch reductions (dWh, dbh, the metric ring entry) are deferred into the pair backward
+// launch (dense_update.h, csa_dense_update_defer).  Replaces head_row_kernel + the fused
+// dense backward of that layer on the critical path (5.0 + 13.5 us in the round-3 trace).
+//
+// Per workgroup: ONE batch of loads (R rows of h, all of Wh, the FS x Kh slice of W as
+// float4s, the epilogue's forward inputs), R x 10 wave reductions for the logits, one wave
+// per row for the softmax, dh into LDS, then 16 lanes per feature dot their W float4s with
+// dh and reduce by DPP inside their 16-lane row.  Workgroups that share a W slice are
+// dealt to one XCD (blocks b and b + 8 share an XCD under round-robin dispatch: speed only).
+// ---------------------------------------------------------------------------------
+constexpr int HD_T = 256;
+constexpr int HD_R = 4;                  // batch rows per workgroup (one wave each for the softmax)
+constexpr int HD_FS = HD_T / 16;         // input features per workgroup (16 lanes each)
+
+struct HeadDgradArgs {
+  const float* h; int M, Kh; int in_act; float in_alpha;     // head input + its transform
+  const float* w; const float* b;                             // head [Kh][10], [10]
+  const int64_t* labels; const int64_t* idx; const int64_t* cursor;
+  int loss; float grad_scale;
+  float* dh; float* dl; float* rloss; int* rcorr;             // written by feature slice 0
+  int64_t* step; int64_t* adv_cursor; long wrap;
+  const float* W; int K1;                                     // last dense layer [K1][Kh]
+  const float* x_fwd; int act; float alpha;                   // its pre-transform input [M][K1]
+  float* dX;                                                  // [M][K1]
+};
+
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xf, 0xf, false));  // row_mirror
+  return v;
+}
+
+// KPT = head-input values per thread (Kh <= 256 KPT), KQ = W float4s per thread (Kh = 64 KQ)
+template <int KPT, int KQ>
+__global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
+  __shared__ float s_part[HD_T / 64][HD_R][NCLS];
+  __shared__ float s_dl[HD_R][NCLS];
+  __shared__ __attribute__((aligned(16))) float s_dh[HD_R][64 * KQ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = a.M, Kh = a.Kh, K1 = a.K1;
+  const int nrt = (M + HD_R - 1) / HD_R, nfs = (K1 + HD_FS - 1) / HD_FS;
+  const int bid = blockIdx.x;
+  int rt, fs;
+  if (nfs % 8 == 0) {                    // slices {x, x+8, ..} on XCD x
+    const int xcd = bid & 7, idx = bid >> 3;
+    fs = xcd + 8 * (idx / nrt);
+    rt = idx % nrt;
+  } else {
+    fs = bid / nrt;
+    rt = bid % nrt;
+  }
+  const int m0 = rt * HD_R, f0 = fs * HD_FS;
+  const int nr = min(HD_R, M - m0);
+  if (bid == 0 && tid == 0) {
+    *a.step += 1;
+    if (a.adv_cursor) {
+      const int64_t c = *a.adv_cursor + 1;
+      *a.adv_cursor = (a.wrap > 0 && c >= a.wrap) ? 0 : c;
+    }
+  }
+  // ---- every load first
+  const int f = tid >> 4, c = tid & 15;
+  const int frow = min(f0 + f, K1 - 1);
+  float4 wq[KQ];
+#pragma unroll
+  for (int u = 0; u < KQ; ++u)
+    wq[u] = reinterpret_cast<const float4*>(a.W + (long)frow * Kh)[u * 16 + c];
+  float hv[HD_R][KPT], wv[KPT][NCLS];
+#pragma unroll
+  for (int u = 0; u < KPT; ++u) {
+    const int k = min(u * HD_T + tid, Kh - 1);
+#pragma unroll
+    for (int r = 0; r < HD_R; ++r) hv[r][u] = a.h[(long)min(m0 + r, M - 1) * Kh + k];
+#pragma unroll
+    for (int j = 0; j < NCLS; j += 2) {
+      const float2 t = *reinterpret_cast<const float2*>(a.w + (long)k * NCLS + j);
+      wv[u][j] = t.x; wv[u][j + 1] = t.y;
+    }
+  }
+  const float bias = lane < NCLS ? a.b[lane] : 0.f;
+  int label = 0;
+  if (wave < nr) {
+    const int m = m0 + wave;
+    if (!a.idx) label = (int)a.labels[m];
+    else label = (int)a.labels[(a.cursor ? a.idx + a.cursor[0] * a.M : a.idx)[m]];
+  }
+  // epilogue operand: lane c < R of feature f stores row m0 + c
+  const float xe = (a.x_fwd && c < HD_R) ? a.x_fwd[(long)min(m0 + c, M - 1) * K1 + frow] : 0.f;
+  // ---- logits
+  float hx[HD_R][KPT];
+#pragma unroll
+  for (int u = 0; u < KPT; ++u) {
+    const bool ok = u * HD_T + tid < Kh;
+#pragma unroll
+    for (int r = 0; r < HD_R; ++r) hx[r][u] = ok ? act_fwd(hv[r][u], a.in_act, a.in_alpha) : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < HD_R; ++r) {
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < KPT; ++u) acc = fmaf(hx[r][u], wv[u][j], acc);
+      acc = wave_sum_dpp(acc);
+      if (lane == 0) s_part[wave][r][j] = acc;
+    }
+  }
+  __syncthreads();
+  if (wave < nr) {
+    // wave r: row m0 + r; lane j < 10: logit j (waves folded in fixed order)
+    const int r = wave, m = m0 + r;
+    float z = -INFINITY;
+    if (lane < NCLS) z = s_part[0][r][lane] + s_part[1][r][lane] + s_part[2][r][lane] + s_part[3][r][lane] + bias;
+    const float mx = wave_max(z);
+    const unsigned long long hit = __ballot(lane < NCLS && z == mx);
+    const int am = __builtin_ctzll(hit);       // lowest index attaining the max (tf.argmax)
+    float d = 0.f, lterm = 0.f;
+    if (a.loss == 0) {
+      const float e = lane < NCLS ? __expf(z - mx) : 0.f;
+      const float se = wave_sum(e);
+      const float lse = mx + __logf(se);
+      if (lane < NCLS) {
+        d = (__expf(z - lse) - (lane == label ? 1.f : 0.f)) * (a.grad_scale / (float)M);
+        lterm = lane == label ? lse - z : 0.f;
+      }
+    } else if (lane < NCLS) {
+      const float t = z - (lane == label ? 1.f : 0.f);
+      lterm = t * t;
+      d = t * (2.f * a.grad_scale / (float)(M * NCLS));
+    }
+    const float ls = wave_sum(lterm);
+    if (lane < NCLS) s_dl[r][lane] = d;
+    if (fs == 0) {
+      if (lane < NCLS) a.dl[(long)m * NCLS + lane] = d;
+      if (lane == 0) {
+        a.rloss[m] = ls;
+        a.rcorr[m] = am == label ? 1 : 0;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- dh = act'(dl . Wh^T) for the R rows -> LDS (slice 0 also stores it: the deferred
+  // weight gradient of the dense layer reads it as its dY)
+#pragma unroll
+  for (int r = 0; r < HD_R; ++r) {
+    float dl[NCLS];
+#pragma unroll
+    for (int j = 0; j < NCLS; ++j) dl[j] = s_dl[r][j];
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int k = u * HD_T + tid;
+      if (k >= Kh) break;
+      float g = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCLS; ++j) g = fmaf(dl[j], wv[u][j], g);
+      if (a.in_act) g = act_bwd(g, hv[r][u], hx[r][u], a.in_act, a.in_alpha);   // x-based: any alpha
+      g = r < nr ? g : 0.f;
+      s_dh[r][k] = g;
+      if (fs == 0 && r < nr) a.dh[(long)(m0 + r) * Kh + k] = g;
+    }
+  }
+  __syncthreads();
+  // ---- dX[m0 + r][f0 + f] = sum_k dh[r][k] W[f][k]: 16 lanes per feature, DPP row sums
+  float p[HD_R];
+#pragma unroll
+  for (int r = 0; r < HD_R; ++r) p[r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < KQ; ++u) {
+    const int k4 = u * 16 + c;
+#pragma unroll
+    for (int r = 0; r < HD_R; ++r) {
+      const float4 d4 = reinterpret_cast<const float4*>(&s_dh[r][0])[k4];
+      p[r] = fmaf(d4.x, wq[u].x, fmaf(d4.y, wq[u].y, fmaf(d4.z, wq[u].z, fmaf(d4.w, wq[u].w, p[r]))));
+    }
+  }
+  float mine = 0.f;
+#pragma unroll
+  for (int r = 0; r < HD_R; ++r) {
+    const float t = row16_sum(p[r]);
+    mine = c == r ? t : mine;
+  }
+  if (c < nr && f0 + f < K1) {
+    float g = mine;
+    if (a.act) g = act_bwd(g, xe, act_fwd(xe, a.act, a.alpha), a.act, a.alpha);
+    a.dX[(long)(m0 + c) * K1 + f0 + f] = g;
+  }
+}
+
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.
 __global__ __launch_bounds__(HT) void head_generic_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -792,5 +991,36 @@ CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, c
     const size_t base = ((size_t)M * NCLS + 32) * sizeof(float);
     hipLaunchKernelGGL(head_generic_kernel, dim3(1), dim3(HT), base, st, a);
   }
+  return (int)hipGetLastError();
+}
+
+// Head + last dense layer input gradient (see head_dgrad_kernel): 0 when outside its
+// family (Kh a multiple of 64 up to 1024; K1 any).
+CSA_API int csa_head_dgrad_ok(int M, int Kh, int K1) {
+  return M >= 1 && K1 >= 1 && Kh >= 64 && Kh <= 1024 && Kh % 64 == 0 ? 1 : 0;
+}
+
+CSA_API int csa_head_dgrad(const float* h, int M, int Kh, int in_act, float in_alpha, const float* w,
+                           const float* b, const int64_t* labels, const int64_t* idx, const int64_t* cursor,
+                           int loss, float grad_scale, float* dh, float* dl, float* rloss, int* rcorr,
+                           int64_t* step, int64_t* adv_cursor, long wrap, const float* W, int K1,
+                           const float* x_fwd, int act, float alpha, float* dX, hipStream_t st) {
+  if (!csa_head_dgrad_ok(M, Kh, K1) || !dh || !dl || !rloss || !rcorr || !W || !dX || !step) return -1;
+  if (act && !x_fwd) return -2;
+  HeadDgradArgs a{h, M, Kh, in_act, in_alpha, w, b, labels, idx, cursor, loss, grad_scale, dh, dl, rloss, rcorr,
+                  step, adv_cursor, wrap, W, K1, x_fwd, act, alpha, dX};
+  const int blocks = ((M + HD_R - 1) / HD_R) * ((K1 + HD_FS - 1) / HD_FS);
+  const dim3 grid((unsigned)blocks), blk(HD_T);
+  const int kq = Kh / 64;
+#define HD_CASE(KQ)                                                                         \
+  case KQ:                                                                                  \
+    hipLaunchKernelGGL((head_dgrad_kernel<(KQ * 64 + HD_T - 1) / HD_T, KQ>), grid, blk, 0, st, a); \
+    break;
+  switch (kq) {
+    HD_CASE(1) HD_CASE(2) HD_CASE(3) HD_CASE(4) HD_CASE(5) HD_CASE(6) HD_CASE(7) HD_CASE(8)
+    HD_CASE(9) HD_CASE(10) HD_CASE(11) HD_CASE(12) HD_CASE(13) HD_CASE(14) HD_CASE(15) HD_CASE(16)
+    default: return -1;
+  }
+#undef HD_CASE
   return (int)hipGetLastError();
 }

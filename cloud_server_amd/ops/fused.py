@@ -60,6 +60,15 @@ _SIGS = {
                                     P, P, P, P, P, P, P, P, I, F, I, F, P, P]),
     "csa_dense_bwd_update_head": (I, [P, P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, I, F, P,
                                       P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, I, F, I, F, P]),
+    # horizontal fusion (round 4): dgrad-only dense backward + deferred update segments
+    "csa_dense_bwd_dgrad": (I, [P, P, P, I, I, I, P, I, F, P, I, I, F, F, P, P, P, P, P, P, P]),
+    "csa_dense_update_defer": (I, [P, P, P, I, I, I, P, I, F, P, P, P, P, P, F, P, P, P, P, P, P, P, P, I, F,
+                                   I, F]),
+    "csa_dense_update_pending": (I, []),
+    "csa_head_dgrad_ok": (I, [I, I, I]),
+    "csa_head_dgrad": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, L, P, I, P, I, F, P, P]),
+    "csa_dense_update_flush": (I, [P]),
+    "csa_dense_update_clear": (None, []),
     "csa_head_row_ok": (I, [I, I]),
     "csa_head_row": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, L, P]),
     "csa_head_part_rows": (I, [I, I]),

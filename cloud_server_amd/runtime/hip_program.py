@@ -154,6 +154,7 @@ class HipProgram:
         self._lower()
         self._plan_fused()
         self._plan_pair()
+        self._plan_hfuse()
         if self.det:
             self._check_det()
         self._alloc()
@@ -409,6 +410,37 @@ class HipProgram:
         except Unsupported:
             return
         self.pair = geom
+
+    # ------------------------------------------------------------------ horizontal fusion
+    def _plan_hfuse(self) -> None:
+        """One-GPU fused program with a conv pair: split every fused dense backward into its
+        input gradient (``csa_dense_bwd_dgrad``, on the step's critical path) and its weight
+        gradient + optimizer update, which is DEFERRED (``csa_dense_update_defer``) and runs
+        as extra workgroups of the pair backward launch (conv_pair.hip,
+        ``conv_pair_bwd_upd_kernel``).  The update only has to land before the next step's
+        forward of its layer; inside the pair backward — a latency chain at 3 % of HBM and
+        8 % of MFMA (profiles/r3_roofline.md) — it uses idle CUs instead of adding 10-15 us
+        of serial work per dense layer.  The head's batch reductions ride in the last dense
+        layer's deferred segment exactly as they rode in its fused backward."""
+        self.hfuse = False
+        self.head_dgrad = False
+        if (self.forward_only or not self.fused or self.det or self.pair is None
+                or os.environ.get("CSA_HFUSE", "1") != "1"):
+            return
+        dense = [u for u in self.units if u.kind == "dense" and u.fused]
+        if not dense or len(dense) > 4:
+            return
+        if any(u.layer.spec.hidden % 128 for u in dense):
+            return
+        self.hfuse = True
+        # the last dense layer's input gradient rides in the head launch (csa_head_dgrad:
+        # every workgroup recomputes the head for its rows, no batch reduction), when that
+        # layer's input transform is at most an activation
+        last = self.units[-1]
+        self.head_dgrad = bool(
+            self.head_row and last.kind == "dense" and last.fused and len(self.units) > 2
+            and not last.in_tf.has_bn
+            and self.lib.csa_head_dgrad_ok(self.B, last.layer.spec.hidden, last.layer.in_shape.numel))
 
     # ------------------------------------------------------------------ deterministic mode
     def _check_det(self) -> None:
@@ -864,6 +896,8 @@ class HipProgram:
         V, G = self.views, self.gviews
         for r in self.zero_early:
             r.zero_()
+        if getattr(self, "hfuse", False):
+            lib.csa_dense_update_clear()        # no stale segment from an aborted step
         self._forward(st)
 
         self._lowrank_gather_inputs()
@@ -871,7 +905,19 @@ class HipProgram:
         # ---------------- head (loss, head grads, input grad, metrics) ----------------
         last = self.units[-1]
         hin = last.y.view(B, -1)
-        if self.head_row:
+        if getattr(self, "head_dgrad", False):
+            staged = getattr(self, "staged", False)
+            ltf = last.in_tf
+            self._rc(lib.csa_head_dgrad(
+                K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
+                K.ptr(V["head.weight"]), K.ptr(V["head.bias"]),
+                K.ptr(self.stage_lbl if staged else e.data.labels), None if staged else K.ptr(rows),
+                None if staged else K.ptr(cur), 0 if e.cfg.loss_name == "entropy" else 1, float(e.sync.grad_scale),
+                K.ptr(last.dy), K.ptr(self.hdl), K.ptr(self.hrl), K.ptr(self.hrc), K.ptr(e.dstep),
+                K.ptr(cur) if staged else None, e.stream.wrap if staged else 0,
+                K.ptr(V[f"{last.layer.name}.weight"]), last.layer.in_shape.numel, K.ptr(last.x.view(B, -1)),
+                _act_id(ltf.act), _alpha(ltf.act), K.ptr(self.units[-2].dy), st), "head_dgrad")
+        elif self.head_row:
             staged = getattr(self, "staged", False)
             self._rc(lib.csa_head_row(
                 K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
@@ -1270,6 +1316,8 @@ class HipProgram:
             K.ptr(ua.dw_acc), K.ptr(ua.db_acc) if ua.layer.spec.bias else None,
             K.ptr(ub.dw_acc), K.ptr(ub.db_acc) if ub.layer.spec.bias else None,
             min(ua.wg_stripes, ub.wg_stripes), st), "conv_pair_bwd")
+        if getattr(self, "hfuse", False) and lib.csa_dense_update_pending():
+            raise RuntimeError("deferred dense updates were not consumed by the pair backward")
         self._sync_bn_param_grads(nt)
         if ua.row_fold:
             for u in (ua, ub):
@@ -1352,6 +1400,24 @@ class HipProgram:
                     _act_id(self.head_tf.act), _alpha(self.head_tf.act))
         else:
             head = (None, None, None, None, None, None, None, None, 1, 1.0, 0, 0.0)
+        if self.hfuse:
+            # weight gradient + update deferred into the pair backward launch; the input
+            # gradient (+ transform backward + BN statistics) now
+            rc = lib.csa_dense_update_defer(
+                K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
+                B, fin, fout, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
+                K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
+                K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
+                1.0, *head)
+            if rc < 0:
+                raise RuntimeError(f"dense_update_defer failed: {rc}")
+            if prev is not None and not (self.head_dgrad and u is self.units[-1]):
+                self._rc(lib.csa_dense_bwd_dgrad(
+                    K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
+                    K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
+                    K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(getattr(tf, "bn_tab", None)),
+                    K.ptr(u.du_part), K.ptr(u.du_cnt), st), "dense_bwd_dgrad")
+            return
         if self.fused_grad:
             # data parallel: the same launch stores dW / db whole into the flat gradient
             G = self.gviews

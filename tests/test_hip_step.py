@@ -163,6 +163,22 @@ CASES = {
         {"layer": "active", "active_func": "relu"},
         {"layer": "connect", "hidden": 32},
     ],
+    # three dense layers with activations between them and before the head: the
+    # horizontal-fusion program (three deferred update segments, the head + last-dense
+    # input gradient launch with an activation epilogue)
+    "dense3_act": [
+        {"layer": "conv", "filter": [2, 2, 10]},
+        {"layer": "conv", "filter": [2, 2, 20]},
+        {"layer": "pool"},
+        {"layer": "norm"},
+        {"layer": "active"},
+        {"layer": "connect", "hidden": 256},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "connect", "hidden": 256},
+        {"layer": "active", "active_func": "sigmoid"},
+        {"layer": "connect", "hidden": 128},
+        {"layer": "active", "active_func": "leaky_relu", "param": [0.2]},
+    ],
     "wide_conv_chain": [
         {"layer": "conv", "filter": [3, 3, 8], "isBias": "True"},
         {"layer": "active", "active_func": "relu"},
@@ -374,3 +390,30 @@ def test_run_steps_groups_equal_single_steps(monkeypatch):
     assert (a.flat - b.flat).abs().max().item() < 1e-3
     ma, mb = a.metrics_since(0), b.metrics_since(0)
     assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
+
+
+@pytest.mark.parametrize("name", ["sample", "dense3_act"])
+def test_horizontal_fusion_matches_fused_program(monkeypatch, name):
+    """Round-4 program: every dense layer's weight gradient + update is deferred into the
+    pair backward launch (conv_pair_bwd_upd_kernel), the input gradients run alone, and the
+    last dense layer's input gradient rides in the head launch (csa_head_dgrad).  Several
+    Adam / Adagrad steps (graph-captured) match the round-3 fused program and the metric
+    ring agrees."""
+    ds = synthetic_mnist(600, seed=17)
+    for opt in ("AdamOptimizer", "AdagradOptimizer"):
+        cfg = _cfg(CASES[name], optimizer=opt, lr=1e-3)
+        monkeypatch.setenv("CSA_HFUSE", "1")
+        a = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
+        monkeypatch.setenv("CSA_HFUSE", "0")
+        b = TrainEngine(cfg, ds, device="cuda", backend="hip", use_graph=True)
+        assert a.program.hfuse and a.program.head_dgrad and not b.program.hfuse
+        for _ in range(5):
+            a.step()
+            b.step()
+        torch.cuda.synchronize()
+        d = (a.flat - b.flat).abs().max().item()
+        assert d < 2e-4, f"{name}/{opt}: horizontal-fusion vs fused params differ by {d}"
+        ma, mb = a.metrics_since(0), b.metrics_since(0)
+        assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
+        assert ma["accuracy"] == mb["accuracy"]
+        assert int(a.dstep.item()) == int(b.dstep.item()) == 5
