@@ -17,7 +17,7 @@ the PS push/pull of the whole gradient every step (construct_distribute.py:355-3
 from __future__ import annotations
 
 import time
-from typing import Dict, Sequence, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
@@ -49,11 +49,48 @@ def time_strategy(cfg, ds, ctx: DistContext, strategy: str, steps: int = 30, war
     return all_reduce_max(ctx, dt)
 
 
-def pick_strategy(cfg, ds, ctx: DistContext, candidates: Sequence[str] = ("lowrank", "allreduce"),
+# Rough MI355X rates for the start-up pruning below (measured in profiles/: the dense
+# weight-gradient kernels reach 27-35 TFLOP/s of f32 MFMA on these shapes; one xGMI link
+# moves ~153 GB/s and a fully connected node's peer-buffer collectives use all W - 1 links)
+F32_GEMM_FLOPS = 30e12
+XGMI_LINK_BPS = 153e9
+
+
+def lowrank_worth_trying(cfg, world: int) -> bool:
+    """False when lowrank's extra weight-gradient FLOPs — every rank forms the GLOBAL dense
+    gradient with K = world x B instead of B — already cost more than moving the dense
+    gradient bytes over the links would (2 (W-1)/W of it per rank, spread over W-1 links),
+    so a W-GPU job does not pay a 30-step trial for a strategy that cannot win.  At B = 50
+    on the sample CNN that keeps lowrank at W = 2 (7 us of extra GEMM vs 52 us on one
+    link) and drops it at W = 8 (47 us vs 13 us)."""
+    from ..models.cnn import build_model
+    if world <= 1:
+        return False
+    B = cfg.batch_size
+    plan = build_model(cfg).plan
+    dense = [lp for lp in plan.layers if type(lp.spec).__name__ == "DenseSpec"]
+    extra_flops = sum(2.0 * (world - 1) * B * lp.in_shape.numel * lp.spec.hidden for lp in dense)
+    grad_bytes = sum(4.0 * lp.in_shape.numel * lp.spec.hidden for lp in dense)
+    t_gemm = extra_flops / F32_GEMM_FLOPS
+    t_links = 2.0 * (world - 1) / world * grad_bytes / ((world - 1) * XGMI_LINK_BPS)
+    return t_gemm <= t_links
+
+
+def default_candidates(cfg, world: int) -> Tuple[str, ...]:
+    return ("lowrank", "allreduce") if lowrank_worth_trying(cfg, world) else ("allreduce",)
+
+
+def pick_strategy(cfg, ds, ctx: DistContext, candidates: Optional[Sequence[str]] = None,
                   steps: int = 30, backend: str = "auto") -> Tuple[str, Dict[str, float]]:
-    """(fastest strategy, {strategy: ms per step}) — identical on every rank."""
+    """(fastest strategy, {strategy: ms per step}) — identical on every rank.  Default
+    candidates: ``default_candidates`` (lowrank only where it can win)."""
     if not ctx.enabled:
         return "allreduce", {}
+    if candidates is None:
+        candidates = default_candidates(cfg, ctx.world)
+    candidates = tuple(candidates)
+    if len(candidates) == 1:
+        return candidates[0], {}
     times = {s: time_strategy(cfg, ds, ctx, s, steps=steps, backend=backend) * 1e3 for s in candidates}
     best = min(candidates, key=lambda s: (times[s], candidates.index(s)))
     return best, {k: round(v, 4) for k, v in times.items()}

@@ -153,14 +153,32 @@ class JobManager:
     def reserve_serving(self, gpu: int) -> int:
         """Take ``settings.serve_slots`` slots of GPU ``gpu`` for the API process (its
         resident inference graphs and GPU preprocessing share that GPU with training), so
-        least-loaded placement steers jobs elsewhere.  Never takes a GPU's last slot.
+        least-loaded placement steers jobs elsewhere.  Never takes a GPU's last slot, counting
+        the jobs already placed there: a reservation that would fill the GPU is undone.  Each
+        slot has its own owner id (``SERVE_JOB - i``), so ``release_serving`` frees them all.
         Returns the number of slots reserved."""
         n = int(getattr(self.settings, "serve_slots", 1) or 0)
-        if self.use_cpu or not 0 <= gpu < self.ngpu or n >= self.slots_per_gpu:
+        if self.use_cpu or not 0 <= gpu < self.ngpu:
             return 0
-        got = sum(1 for _ in range(n) if self.sched.reserve(self.SERVE_JOB, gpu))
-        self.serve_reserved = (gpu, got)
-        return got
+        got = []
+        with self._lock:
+            for i in range(n):
+                owner = self.SERVE_JOB - len(getattr(self, "serve_owners", [])) - i
+                if not self.sched.reserve(owner, gpu):
+                    break
+                if self.sched.load(gpu) >= self.slots_per_gpu:     # that was the last slot
+                    self.sched.release(owner)
+                    break
+                got.append(owner)
+            self.serve_owners = getattr(self, "serve_owners", []) + got
+        self.serve_reserved = (gpu, len(got))
+        return len(got)
+
+    def release_serving(self) -> int:
+        """Free every serving slot this manager reserved."""
+        with self._lock:
+            owners, self.serve_owners = getattr(self, "serve_owners", []), []
+        return sum(self.sched.release(o) for o in owners)
 
     # ------------------------------------------------------------------ public API
     def submit(self, owner: int, model: str, datatype: str, config: Dict[str, Any],
@@ -355,7 +373,7 @@ class JobManager:
         if n > 1:
             port = _free_port()             # a fixed 29500 + jid formula collided
             argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-                    "--master-addr", "127.0.0.1", "--master-port", str(port)] + mod[1:]
+                    "--master-addr", "127.0.0.1", "--master-port", str(port)] + mod   # -m: run as a module
         else:
             argv = [sys.executable] + mod + ["--device", "cpu" if self.use_cpu else "cuda:0"]
         env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")   # RCCL errors/timeouts abort the rank

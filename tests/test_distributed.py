@@ -38,6 +38,7 @@ def _port():
 
 
 def _init(rank, world, port):
+    torch.set_num_threads(1)            # world 8 on an 8-CPU box: no oversubscription
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from cloud_server_amd.parallel.dist import init_distributed
@@ -193,6 +194,10 @@ BN_CFG = {"iter": 4, "learning_rate": 0.01, "ratio": 0.8, "loss_name": "entropy"
 
 
 def _sync_bn(rank, world, port, out):
+    _sync_bn_w(rank, world, port, out)
+
+
+def _sync_bn_w(rank, world, port, out):
     """SyncBN: each rank normalises its half of the batch with the GLOBAL statistics; the
     forward equals the single-process full batch and the all-reduced mean gradient
     equals the full-batch gradient."""
@@ -202,8 +207,8 @@ def _sync_bn(rank, world, port, out):
     cfg = parse_train_config(BN_CFG)
     assert cfg.sync_bn
     g = torch.Generator().manual_seed(7)
-    X = torch.rand(12, 28, 28, 1, generator=g)
-    Y = torch.randint(0, 10, (12,), generator=g)
+    X = torch.rand(6 * world, 28, 28, 1, generator=g)
+    Y = torch.randint(0, 10, (6 * world,), generator=g)
     ref = build_model(cfg)
     ref.train()
     lr = ref(X)
@@ -265,3 +270,74 @@ def _agreed_error(rank, world, port, out):
 def test_xgmi_error_agreed_across_ranks():
     out = _spawn(_agreed_error, 2)
     assert out == {0: "raised", 1: "raised"}
+
+
+# ---------------------------------------------------------------------------------------
+# World-8 rehearsal of the 8-GPU node (VERDICT r3 "next" #4): every strategy and SyncBN at
+# the width the driver's scaling run uses, on gloo.  Reference: the PS/worker host lists
+# (construct_distribute.py:37-40, 344-345) — scaling by adding workers.
+W8_CFG = dict(CFG, options=dict(CFG["options"], batch_size=50))
+
+
+def _named(eng):
+    return {k: eng.model.state.view(k, eng.flat).detach().clone() for k in eng.model.state.shapes}
+
+
+def _train_strategies(rank, world, port, steps, out):
+    from cloud_server_amd.parallel.dist import shutdown
+    from cloud_server_amd.runtime.engine import TrainEngine
+    ctx = _init(rank, world, port)
+    cfg = parse_train_config(W8_CFG)
+    res = {}
+    for strategy in ("allreduce", "ps", "lowrank"):
+        eng = TrainEngine(cfg, synthetic_mnist(800, seed=1), device="cpu", ctx=ctx, strategy=strategy)
+        for _ in range(steps):
+            eng.step()
+        res[strategy] = _named(eng)
+    out[rank] = res
+    shutdown(ctx)
+
+
+def test_world8_strategies_equal_single_process_400_batch():
+    """8 ranks x B=50 with allreduce, ps (reduce-scatter -> owner Adagrad -> all-gather) and
+    lowrank each equal ONE process training on the 400-sample global batch (3 steps, across
+    an epoch boundary of the 800-sample set); replicas are identical."""
+    from cloud_server_amd.runtime.engine import TrainEngine
+    out = _spawn(_train_strategies, 8, 3)
+    cfg = parse_train_config(dict(W8_CFG, options=dict(W8_CFG["options"], batch_size=400)))
+    ref = TrainEngine(cfg, synthetic_mnist(800, seed=1), device="cpu")
+    for _ in range(3):
+        ref.step()
+    want = _named(ref)
+    for strategy in ("allreduce", "ps", "lowrank"):
+        for r in range(1, 8):
+            for k in want:
+                torch.testing.assert_close(out[r][strategy][k], out[0][strategy][k], rtol=0, atol=0)
+        for k, v in want.items():
+            torch.testing.assert_close(out[0][strategy][k], v, rtol=2e-4, atol=2e-5,
+                                       msg=lambda m, s=strategy, k=k: f"{s} {k}: {m}")
+
+
+def test_sync_bn_equals_full_batch_world8():
+    out = _spawn(_sync_bn_w, 8)
+    for r in range(8):
+        fwd_ok, gdiff, gmax, run_ok = out[r]
+        assert fwd_ok, r
+        assert gdiff <= 1e-5 * max(1.0, gmax), (r, gdiff, gmax)
+        assert run_ok, r
+
+
+def test_collectives_world8():
+    out = _spawn(_collectives, 8)
+    assert out == {r: True for r in range(8)}
+
+
+def test_lowrank_candidate_pruned_at_width():
+    """lowrank's K = W x B weight gradient outgrows the all-reduce's
+    link time on the sample CNN somewhere between 4 and 8 GPUs; an 8-GPU job does not time
+    it at start-up."""
+    from cloud_server_amd.models.dsl import SAMPLE_CONFIG
+    from cloud_server_amd.parallel.strategy import default_candidates
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, options={"batch_size": 50}))
+    assert default_candidates(cfg, 2) == ("lowrank", "allreduce")
+    assert default_candidates(cfg, 8) == ("allreduce",)

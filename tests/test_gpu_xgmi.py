@@ -204,7 +204,7 @@ def _worker_twoshot(rank: int, world: int, port: int, q) -> None:
         q.put((rank, {"exception": traceback.format_exc()}))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_xgmi_two_shot_bitexact(world):
     """Two-shot all-reduce (reduce-scatter + all-gather over the peer buffers) equals the
     one-shot result and the host's fixed-order sum BITWISE, on every rank, for uneven

@@ -550,7 +550,14 @@ def test_job_manager_reserves_serving_slot(tmp_path):
     try:
         assert jm.reserve_serving(1) == 1 and jm.sched.load(1) == 1 and jm.sched.load(0) == 0
         s.serve_slots = 4
-        assert jm.reserve_serving(0) == 0            # would take the GPU's last slot
+        assert jm.reserve_serving(0) == 3            # the 4th would take the GPU's last slot
+        assert jm.sched.load(0) == 3
+        assert jm.release_serving() == 4 and jm.sched.load(0) == 0 and jm.sched.load(1) == 0
+        # jobs already placed count — 2 serving slots on a GPU holding 2 jobs of 4
+        s.serve_slots = 2
+        assert jm.sched.reserve(7, 0) and jm.sched.reserve(8, 0)
+        assert jm.reserve_serving(0) == 1 and jm.sched.load(0) == 3
+        assert jm.release_serving() == 1 and jm.sched.load(0) == 2
     finally:
         jm.shutdown()
 
@@ -587,3 +594,56 @@ def test_capture_gc_guard_holds_across_overlapping_threads(monkeypatch):
         t.join(20)
     assert seen["after_first_ended"] is False
     assert gc.isenabled() and graphs.active_captures() == 0
+
+
+def test_job_manager_launches_8_gpu_dp_job(tmp_path):
+    """an 8-GPU data-parallel job is placed on 8 distinct GPUs and launched
+    as ONE torch.distributed.run with 8 local ranks over HIP_VISIBLE_DEVICES=0..7.  The
+    captured launch line is then run for real (gloo, CPU): every rank sees WORLD_SIZE=8,
+    LOCAL_WORLD_SIZE=8 and a distinct LOCAL_RANK (= its GPU under init_distributed)."""
+    import subprocess
+    import sys
+    s = _settings(tmp_path, "process")
+    db = Database(s.db_path)
+    uid = db.create_user("u", "pw-12345678")
+    jm = JobManager(s, db, executor="process", ngpu=8, slots_per_gpu=1)
+
+    class _Q:
+        def __init__(self):
+            self.items = []
+
+        def put(self, item):
+            self.items.append(item)
+
+    real, jm._req = jm._req, _Q()
+    try:
+        _prep_model(s, uid, "m8", n=40)
+        jid = jm.submit(uid, "m8", "file", dict(SMALL, iter=4), ngpus=8)
+        t0 = time.time()
+        while not jm._req.items and time.time() - t0 < 30:
+            time.sleep(0.05)
+        kind, got, argv, env, mdir, log = jm._req.items[0]
+        assert kind == "launch" and got == jid
+        assert sorted(jm.running[jid]["gpus"]) == list(range(8))
+        assert all(jm.sched.load(g) == 1 for g in range(8))
+        assert env["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7"
+        assert "--nproc-per-node=8" in argv and argv[1:3] == ["-m", "torch.distributed.run"]
+        # run the launch line with a probe in place of the worker module's arguments
+        i = argv.index("cloud_server_amd.runtime.worker")
+        probe = tmp_path / "probe.py"
+        probe.write_text(
+            "import json, os\n"
+            "keys = ['RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE', 'HIP_VISIBLE_DEVICES']\n"
+            f"open(os.path.join(r'{tmp_path}', 'probe_%s.json' % os.environ['RANK']), 'w').write("
+            "json.dumps({k: os.environ.get(k) for k in keys}))\n")
+        assert argv[i - 1] == "-m"          # torchrun runs the worker as a module
+        cmd = argv[:i - 1] + [str(probe)]
+        r = subprocess.run(cmd, env=dict(env, OMP_NUM_THREADS="1"), capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        seen = [json.load(open(tmp_path / f"probe_{k}.json")) for k in range(8)]
+        assert sorted(int(d["LOCAL_RANK"]) for d in seen) == list(range(8))
+        assert all(d["WORLD_SIZE"] == "8" and d["LOCAL_WORLD_SIZE"] == "8" for d in seen)
+        assert all(d["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7" for d in seen)
+    finally:
+        jm._req = real
+        jm.shutdown()
