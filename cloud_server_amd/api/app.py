@@ -684,7 +684,14 @@ def create_app(settings: Optional[Settings] = None, executor: Optional[str] = No
         if os.path.exists(p):
             with open(p) as fh:
                 rows = [json.loads(x) for x in fh if x.strip()]
-        return J({"metrics": rows})
+        st = {}
+        try:
+            with open(os.path.join(settings.model_dir(u["id"], m), STATUS)) as fh:
+                st = json.load(fh)
+        except (OSError, json.JSONDecodeError):
+            pass
+        # the step program in use and, when it is not the HIP one, why (never silent)
+        return J({"metrics": rows, "backend": st.get("backend"), "fallback_reason": st.get("fallback") or ""})
 
     @app.get("/generation/run/runtime/")
     async def run_runtime(request: Request):

@@ -32,7 +32,7 @@ struct ZeroList { float* p[MAXZ]; long n[MAXZ]; int count; };
 struct Fold { long off, n, ld; float* src; int S; int zero; };
 struct FoldList { Fold f[MAXF]; int count; long lo, hi; };
 
-constexpr int MAXK = 8;
+constexpr int MAXK = 32;
 // Gradient ranges whose producer STORES every element each step: the update need not
 // re-zero them.
 struct KeepList { long lo[MAXK], hi[MAXK]; int count; };
@@ -287,6 +287,31 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
                             const uint8_t* st_img, const int64_t* st_labels, const int64_t* st_rows,
                             const int64_t* st_cursor, int st_B, long st_imsz, uint8_t* st_out_img,
                             int64_t* st_out_lbl, hipStream_t st);
+
+// A network whose first unit reads no raw images (a dense / standalone norm / pool first
+// layer) takes its float input [B][D] = images[rows[cursor]] / 255 from this one launch
+// (was index_select + to(float) + mul: three torch kernels per step).  One thread per
+// 4 pixels: a uint32 load, a float4 store.
+__global__ __launch_bounds__(256) void gather_f32_kernel(const uint32_t* img, const int64_t* rows,
+                                                         const int64_t* cursor, int B, long words, float4* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * words) return;
+  const long b = i / words, off = i - b * words;
+  const int64_t r = rows[*cursor * B + b];
+  const uint32_t v = img[r * words + off];
+  constexpr float k = 1.0f / 255.0f;
+  out[i] = make_float4((float)(v & 255u) * k, (float)((v >> 8) & 255u) * k, (float)((v >> 16) & 255u) * k,
+                       (float)(v >> 24) * k);
+}
+
+CSA_API int csa_gather_images_f32(const uint8_t* img, const int64_t* rows, const int64_t* cursor, int B, long imsz,
+                                  float* out, hipStream_t st) {
+  if (B <= 0 || imsz <= 0 || imsz % 4 || !img || !rows || !cursor || !out) return -1;
+  const long words = imsz / 4, total = (long)B * words;
+  hipLaunchKernelGGL(gather_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t*>(img), rows, cursor, B, words, reinterpret_cast<float4*>(out));
+  return (int)hipGetLastError();
+}
 
 CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, long n, const long* seg_lo,
                            const long* seg_hi, int nseg, int zero_grad, float lr, const int64_t* step,

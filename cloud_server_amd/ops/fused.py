@@ -90,6 +90,7 @@ _SIGS = {
     "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),
     "csa_head_part2": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P, L, P]),
     "csa_gather_batch": (I, [P, P, P, P, I, L, P, P, P]),
+    "csa_gather_images_f32": (I, [P, P, P, I, L, P, P]),
     "csa_zero": (I, [P, P, I, P]),
     "csa_gemm_debug": (I, [P]),
     "csa_conv_debug": (I, [P]),

@@ -53,9 +53,19 @@ class Unsupported(Exception):
 def _act_id(sp: Optional[ActSpec]) -> int:
     if sp is None:
         return 0
-    if sp.func == "leaky_relu" and sp.alpha <= 0:
-        raise Unsupported("leaky_relu with alpha <= 0")
+    if sp.func == "leaky_relu" and sp.alpha == 0:
+        return K.ACT_IDS["relu"]        # tf.maximum(x, 0 * x) IS relu
     return K.ACT_IDS[sp.func]
+
+
+def _y_ok(sp: Optional[ActSpec]) -> bool:
+    """Can this activation's backward be formed from its OUTPUT alone?  The kernels that
+    fuse an activation into a producer's epilogue (conv / pair outputs, the row head's
+    input) keep only y; ``maximum(x, a x)`` with a < 0 maps x > 0 and x < 0 both to y > 0,
+    so such an activation is lowered where x is at hand instead: as a consumer transform
+    (the dgrad epilogues read the pre-transform input) or a standalone act unit
+    (construct_distribute.py:147-150 accepts any alpha)."""
+    return sp is None or not (sp.func == "leaky_relu" and sp.alpha < 0)
 
 
 def _alpha(sp: Optional[ActSpec]) -> float:
@@ -337,6 +347,13 @@ class HipProgram:
             # hand-off, so fc2's 32 row groups still use 128 CUs: profiles/r2_dense_fused.md)
             groups = (fin + 15) // 16
             u.fused = bool(self.lib.csa_dense_bwd_update_ok(B, fin, fout, C)) and groups >= 1
+        # the flat optimizer launch updates at most 16 spans between the fused layers' own
+        # parameters: beyond 15 fused layers the rest take the materialised-gradient path
+        nf = 0
+        for u in self.units:
+            if getattr(u, "fused", False):
+                nf += 1
+                u.fused = nf <= 15
         self.head_rg = 0
         self.head_row = False
         self.head_sep = False
@@ -405,9 +422,7 @@ class HipProgram:
                 h1, w1, lb.spec.kh, lb.spec.kw, lb.pads[0], lb.pads[2], lb.spec.cout, h2, w2, pool, ph, pw]
         if not self.lib.csa_conv_pair_ok(K.ints(geom)):
             return
-        try:
-            _act_id(ua.act), _act_id(ub.act)
-        except Unsupported:
+        if not (_y_ok(ua.act) and _y_ok(ub.act)):
             return
         self.pair = geom
 
@@ -486,6 +501,8 @@ class HipProgram:
                     if tf.act is not None:
                         return None              # two activations in a row
                     tf.act = lp.spec
+            if consumer == "head" and not _y_ok(tf.act):
+                return None                      # the row head's backward reads y only
             if tf.norm is not None:
                 # the forward statistics come from a conv unit's epilogue, the tables live
                 # in LDS (<= 128 channels), and the head has no BN-apply prologue
@@ -530,7 +547,7 @@ class HipProgram:
                 u = Unit(kind, lp, in_tf=tf)
                 j = i + 1
                 if kind == "conv":
-                    if j < len(layers) and isinstance(layers[j].spec, ActSpec):
+                    if j < len(layers) and isinstance(layers[j].spec, ActSpec) and _y_ok(layers[j].spec):
                         u.act = layers[j].spec
                         j += 1
                     if j < len(layers) and isinstance(layers[j].spec, PoolSpec):
@@ -1086,8 +1103,13 @@ class HipProgram:
         e, lib, B = self.e, self.lib, self.B
         rows, cur = e.stream.rows, e.stream.cursor
         if self.__dict__.get("x_dense_in") is not None:
-            idx = rows.index_select(0, cur).view(-1)
-            self.x_dense_in.copy_(e.data.images.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
+            D = self.x_dense_in.shape[1]
+            if e.data.images.dtype == torch.uint8 and D % 4 == 0:
+                self._rc(lib.csa_gather_images_f32(K.ptr(e.data.images), K.ptr(rows), K.ptr(cur), B, D,
+                                                   K.ptr(self.x_dense_in), st), "gather_images_f32")
+            else:
+                idx = rows.index_select(0, cur).view(-1)
+                self.x_dense_in.copy_(e.data.images.index_select(0, idx).to(torch.float32).mul_(1.0 / 255.0))
         img = e.data.images
         V = self.views
         # ---------------- forward ----------------
@@ -1464,8 +1486,7 @@ class HipProgram:
                 segs[-1][1] = max(segs[-1][1], hi)
             else:
                 segs.append([lo, hi])
-        if len(segs) > 16:
-            raise Unsupported("more than 16 optimizer segments")
+        assert len(segs) <= 16, "at most 15 fused dense layers (_plan_fused)"
         return segs
 
     def _optimizer(self, st) -> None:
@@ -1504,9 +1525,11 @@ class HipProgram:
         fS = (C.c_int * 8)(*[f[3] for f in folds])
         fl = (C.c_long * 8)(*[f[4] for f in folds])
         fz = (C.c_int * 8)(*[f[5] for f in folds])
-        keep = self.keep_ranges[:8]
-        klo = (C.c_long * 8)(*[k[0] for k in keep])
-        khi = (C.c_long * 8)(*[k[1] for k in keep])
+        keep = self.keep_ranges
+        if len(keep) > 32:
+            raise RuntimeError(f"{len(keep)} stored dense gradient ranges (optimizer holds 32)")
+        klo = (C.c_long * 32)(*[k[0] for k in keep])
+        khi = (C.c_long * 32)(*[k[1] for k in keep])
         segs = self.opt_segments
         slo = (C.c_long * 16)(*[x[0] for x in segs])
         shi = (C.c_long * 16)(*[x[1] for x in segs])

@@ -211,6 +211,8 @@ class JobRun:
             self.eng = eng = TrainEngine(cfg, train, device=device, ctx=ctx, backend=backend, packed=packed,
                                          strategy=config.get("options", {}).get("strategy", "allreduce")
                                          if isinstance(config.get("options"), dict) else "allreduce")
+            if chief:       # which program runs, and why not the HIP one if it does not
+                write_status(model_dir, backend=eng.backend, fallback=eng.fallback_reason)
             last = ckpt.latest(model_dir)
             if last is not None:
                 ckpt.restore_engine(eng, ckpt.load(last[1]))

@@ -213,7 +213,9 @@ def test_full_user_flow(client):
     assert models[0]["name"] == "m1" and models[0]["state"] == "done"
     assert client.get("/models/m1/", headers=h).json()["job"]["state"] == "done"
     assert "m1" in client.get("/models/compare/", params={"models": "m1"}, headers=h).json()
-    assert len(client.get("/generation/run/details/", params={"modelName": "m1"}, headers=h).json()["metrics"]) >= 4
+    det = client.get("/generation/run/details/", params={"modelName": "m1"}, headers=h).json()
+    assert len(det["metrics"]) >= 4
+    assert det["backend"] == "torch" and det["fallback_reason"] == ""      # (CPU: the eager program)
     assert client.get("/generation/run/runtime/", params={"modelName": "m1"}, headers=h).json()["state"] == "done"
     img = _png(ds.images[0].reshape(28, 28))
     r = _mp(client, "/construct/inference/m1/", {}, {"file": ("q.png", img, "image/png")}, h)

@@ -163,6 +163,42 @@ CASES = {
         {"layer": "active", "active_func": "relu"},
         {"layer": "connect", "hidden": 32},
     ],
+    # leaky_relu with alpha = 0 (relu) and alpha < 0 (backward not recoverable from y:
+    # lowered as consumer transforms / standalone act units, never fused into a producer)
+    "leaky_alpha": [
+        {"layer": "conv", "filter": [3, 3, 6], "isBias": "True"},
+        {"layer": "active", "active_func": "leaky_relu", "param": [0]},
+        {"layer": "conv", "filter": [2, 2, 8]},
+        {"layer": "active", "active_func": "leaky_relu", "param": [-0.1]},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 32},
+        {"layer": "active", "active_func": "leaky_relu", "param": [-0.1]},
+        {"layer": "connect", "hidden": 32},
+        {"layer": "active", "active_func": "leaky_relu", "param": [-0.3]},
+    ],
+    # a 20-layer network (every layer kind, several of each)
+    "deep20": [
+        {"layer": "conv", "filter": [3, 3, 8], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [3, 3, 8]},
+        {"layer": "active", "active_func": "leaky_relu", "param": [0.1]},
+        {"layer": "pool"},
+        {"layer": "norm"},
+        {"layer": "conv", "filter": [3, 3, 12], "isBias": "True"},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "conv", "filter": [2, 2, 12]},
+        {"layer": "norm"},
+        {"layer": "active"},
+        {"layer": "pool"},
+        {"layer": "connect", "hidden": 128},
+        {"layer": "active", "active_func": "relu"},
+        {"layer": "connect", "hidden": 128},
+        {"layer": "active", "active_func": "leaky_relu", "param": [-0.2]},
+        {"layer": "connect", "hidden": 64},
+        {"layer": "active"},
+        {"layer": "connect", "hidden": 64},
+        {"layer": "active", "active_func": "relu"},
+    ],
     # three dense layers with activations between them and before the head: the
     # horizontal-fusion program (three deferred update segments, the head + last-dense
     # input gradient launch with an activation epilogue)
