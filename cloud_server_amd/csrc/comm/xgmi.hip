@@ -53,6 +53,10 @@ struct XgArgs {
                                 // two-shot: [2 parity][2 phase][world][shard] in the same bytes
   unsigned* flags[XG_MAXR];     // rank r's flags [2 phase][2 parity][XG_MAXB][XG_MAXR] (mapped)
   XgSeg seg[XG_MAXSEG];
+  // op 3 (reduce-scatter of a range with GLOBAL ownership): the message is units
+  // [rs_lo, rs_lo + msg) of a flat buffer whose unit g belongs to rank g / rs_sh; the
+  // owner writes the sum of its units to rs_dst[g - rank * rs_sh]
+  long rs_lo, rs_sh; char* rs_dst;
   unsigned* seq; unsigned* done; int* err;
   unsigned long long timeout_ticks;
 };
@@ -188,11 +192,17 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   const long u1 = u0 + per < units ? u0 + per : units;
   const long my_slot = ((long)par * a.world + a.rank) * a.slot_bytes;
 
-  // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included)
+  // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included);
+  // op 3: only into its OWNER's slot [rank] (each unit leaves the GPU at most once)
   for (long u = u0 + t; u < u1; u += blockDim.x) {
     const long off = u << 4;
     const XgSeg& s = a.seg[xg_find(a, off)];
     const uint4 v = *reinterpret_cast<const uint4*>(s.src + (off - s.off));
+    if (a.op == 3) {
+      const int p = (int)((a.rs_lo + u) / a.rs_sh);
+      *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
+      continue;
+    }
 #pragma unroll
     for (int p = 0; p < XG_MAXR; ++p)
       if (p < a.world) *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
@@ -235,6 +245,20 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
       const long off = u << 4;
       const XgSeg& s = a.seg[xg_find(a, off)];
       const long so = off - s.off;
+      if (a.op == 3) {           // reduce-scatter: my units of the range, fixed rank order
+        const long g = a.rs_lo + u;
+        if (g / a.rs_sh != a.rank) continue;
+        float4 v[XG_MAXR];
+#pragma unroll
+        for (int r = 0; r < XG_MAXR; ++r)
+          if (r < a.world) v[r] = *reinterpret_cast<const float4*>(mine + (long)r * a.slot_bytes + off);
+        float4 acc = v[0];
+#pragma unroll
+        for (int r = 1; r < XG_MAXR; ++r)
+          if (r < a.world) { acc.x += v[r].x; acc.y += v[r].y; acc.z += v[r].z; acc.w += v[r].w; }
+        *reinterpret_cast<float4*>(a.rs_dst + ((g - (long)a.rank * a.rs_sh) << 4)) = acc;
+        continue;
+      }
       if (a.op == 0) {           // all-gather: out is rank-major [world][seg.bytes]
         uint4 v[XG_MAXR];
 #pragma unroll
@@ -326,6 +350,37 @@ CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* con
   const long units = off >> 4;
   // ~8 KB per block: measured 9.6 us vs 16.9 (32 KB) / 52.5 (128 KB) for the 0.9 MB
   // lowrank gather (profiles/r1s4_xgmi_collectives.md)
+  int nb = nblocks > 0 ? nblocks : (int)((units + 511) / 512);
+  nb = nb < 1 ? 1 : (nb > XG_MAXB ? XG_MAXB : nb);
+  hipLaunchKernelGGL(xgmi_kernel, dim3(nb), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Reduce-scatter of the range [lo, lo + bytes) of a flat fp32 buffer (src = its start,
+// lo and bytes in bytes, 16-aligned) whose shard of shard_bytes belongs to rank
+// offset / shard_bytes: this rank receives the fixed-rank-order sum of its part of the
+// range in dst_shard (the start of ITS shard's buffer).  Issued per gradient bucket as the
+// backward produces it (the "ps" strategy: construct_distribute.py:355-357, 413).
+CSA_API int csa_xgmi_reduce_scatter(int rank, int world, long slot_bytes, void* const* bufs, void* const* flags,
+                                    const void* src, long lo, long bytes, long shard_bytes, void* dst_shard,
+                                    unsigned* state, double timeout_s, int nblocks, hipStream_t st) {
+  if (world < 1 || world > XG_MAXR || rank < 0 || rank >= world) return -1;
+  if ((lo & 15) || bytes <= 0 || (bytes & 15) || (shard_bytes & 15) || shard_bytes <= 0) return -2;
+  if (((uintptr_t)src & 15) || ((uintptr_t)dst_shard & 15)) return -2;
+  if (bytes > slot_bytes) return -3;
+  if ((lo + bytes + shard_bytes - 1) / shard_bytes > world) return -4;     // range beyond the last shard
+  XgArgs a{};
+  a.op = 3; a.rank = rank; a.world = world; a.nseg = 1; a.slot_bytes = slot_bytes;
+  a.seg[0] = XgSeg{static_cast<const char*>(src) + lo, nullptr, bytes, 0};
+  a.msg_bytes = bytes;
+  a.rs_lo = lo >> 4; a.rs_sh = shard_bytes >> 4; a.rs_dst = static_cast<char*>(dst_shard);
+  for (int r = 0; r < world; ++r) {
+    a.buf[r] = static_cast<char*>(bufs[r]);
+    a.flags[r] = static_cast<unsigned*>(flags[r]);
+  }
+  a.seq = state; a.done = state + 1; a.err = reinterpret_cast<int*>(state + 2);
+  a.timeout_ticks = (unsigned long long)(timeout_s * 1.0e8);
+  const long units = bytes >> 4;
   int nb = nblocks > 0 ? nblocks : (int)((units + 511) / 512);
   nb = nb < 1 ? 1 : (nb > XG_MAXB ? XG_MAXB : nb);
   hipLaunchKernelGGL(xgmi_kernel, dim3(nb), dim3(256), 0, st, a);

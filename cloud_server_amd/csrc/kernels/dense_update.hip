@@ -242,7 +242,9 @@ CSA_API int csa_dense_bwd_dgrad(const float* dY, const float* W, float* dX, int 
   a.act = act; a.alpha = alpha;
   a.bn = BNRef{bn_slab, bn_nslab, bn_slab ? bn_C : 1, bn_count, bn_eps, bn_scale, bn_offset};
   a.bn_on = bn_slab != nullptr; a.bn_tab = bn_slab ? bn_tab : nullptr;
-  a.bwd_slab = bwd_slab; a.Xw = dY; a.det = g_csa_det; a.scale = 1.f;
+  // Xw is not read in this mode, but it is the epilogue's address-select fallback for
+  // x_fwd, so it must have the [M][K] shape: the input gradient buffer itself
+  a.bwd_slab = bwd_slab; a.Xw = x_fwd ? x_fwd : dX; a.det = g_csa_det; a.scale = 1.f;
   const int groups = (K + DU_FT - 1) / DU_FT;
   a.cs = du_cs(K, N);
   a.part = part; a.cnt = cnt;

@@ -253,11 +253,56 @@ class GradSync:
         with self._timed():
             dist.reduce_scatter_tensor(shard_out, flat_grad)
 
+    def reduce_scatter_range(self, flat_grad: torch.Tensor, shard_out: torch.Tensor, lo: int, hi: int) -> None:
+        """The [lo, hi) part of ``reduce_scatter``: every element is summed into its owner's
+        shard (owner = index // shard).  Issued per gradient bucket as the backward produces
+        it (the HIP program's overlapped ps step); once every bucket covering the buffer has
+        run, ``shard_out`` equals ``reduce_scatter``'s.  xGMI: one launch, each element
+        leaves its GPU at most once; otherwise one RCCL reduce per owner portion."""
+        if not self.ctx.enabled:
+            shard_out[lo:hi].copy_(flat_grad[lo:hi])
+            return
+        sh, W, r = self.shard, self.ctx.world, self.ctx.rank
+        ch = None
+        if self.xgmi is not None and not torch.cuda.is_current_stream_capturing() and f"rs:{lo}:{hi}" not in self._choice:
+            ok = lo % 4 == 0 and hi % 4 == 0 and sh % 4 == 0 and flat_grad.data_ptr() % 16 == 0 \
+                and shard_out.data_ptr() % 16 == 0
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            self._choice[f"rs:{lo}:{hi}"] = self.xgmi.channel(f"rs:{lo}:{hi}", (hi - lo) * 4) if flag.item() else None
+        ch = self._choice.get(f"rs:{lo}:{hi}")
+        with self._timed():
+            if ch is not None:
+                ch.reduce_scatter_range(flat_grad, lo, hi, sh, shard_out)
+                return
+            for p in range(W):
+                a, b = max(lo, p * sh), min(hi, (p + 1) * sh)
+                if a >= b:
+                    continue
+                part = flat_grad[a:b]
+                if self.ctx.backend == "gloo":
+                    buf = part.clone()
+                    dist.reduce(buf, dst=p)
+                    if p == r:
+                        shard_out[a - r * sh:b - r * sh].copy_(buf)
+                else:
+                    dist.reduce(part, dst=p)
+                    if p == r:
+                        shard_out[a - r * sh:b - r * sh].copy_(part)
+
     def all_gather_params(self, flat_param: torch.Tensor) -> None:
+        """Every owner's updated shard to every rank (xGMI: one push of the shard to the 7
+        peers at once; else RCCL all-gather)."""
         if not self.ctx.enabled:
             return
         lo, hi = self.shard_range()
+        ch = None
+        if self.ctx.backend == "nccl":
+            ch = self._xg_channel("ps_ag", [flat_param[lo:hi]], [flat_param])
         with self._timed():
+            if ch is not None:
+                ch.all_gather([(flat_param[lo:hi], flat_param)])
+                return
             dist.all_gather_into_tensor(flat_param, flat_param[lo:hi].clone()
                                         if self.ctx.backend == "gloo" else flat_param[lo:hi])
 

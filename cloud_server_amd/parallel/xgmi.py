@@ -132,6 +132,18 @@ class XgmiChannel:
             p = "twoshot" if nbytes >= TWO_SHOT_MIN_BYTES and self.world > 2 else "oneshot"
         self._run(OP_ALLREDUCE_2SHOT if p == "twoshot" else OP_ALLREDUCE, tensors, tensors)
 
+    def reduce_scatter_range(self, flat: torch.Tensor, lo: int, hi: int, shard: int,
+                             shard_out: torch.Tensor) -> None:
+        """Elements [lo, hi) of the flat fp32 buffer, summed over ranks into their OWNERS
+        (element i belongs to rank i // shard): this rank's part of the range lands in
+        ``shard_out[i - rank * shard]``.  Every element leaves its GPU at most once."""
+        rc = self.lib.csa_xgmi_reduce_scatter(
+            self.rank, self.world, self.slot_bytes, self._bufs, self._flags, flat.data_ptr(), lo * 4,
+            (hi - lo) * 4, shard * 4, shard_out.data_ptr(), self.state.data_ptr(), self.timeout_s,
+            self.nblocks, torch.cuda.current_stream(self.device).cuda_stream)
+        if rc:
+            raise RuntimeError(f"xgmi reduce-scatter launch failed ({rc})")
+
     def fits(self, tensors: Sequence[torch.Tensor]) -> bool:
         return (len(tensors) <= 8 and all(_aligned(t) for t in tensors)
                 and sum(t.numel() * t.element_size() for t in tensors) <= self.slot_bytes)

@@ -195,7 +195,10 @@ class HipProgram:
         sample config that is one ~1 MB bucket (head+fc2) launched after fc2, the 8 MB
         fc1 bucket launched right after fc1's weight gradient, and a small tail."""
         e = self.e
-        self.overlap = (e.ctx.enabled and e.sync.strategy == "allreduce" and
+        # ps (the parameter-server capability): the same suffix buckets are REDUCE-SCATTERED
+        # to their owner shards (GradSync.reduce_scatter_range; xGMI: one launch per bucket,
+        # every element leaves its GPU at most once) while the backward continues
+        self.overlap = (e.ctx.enabled and e.sync.strategy in ("allreduce", "ps") and
                         os.environ.get("CSA_DP_OVERLAP", "1") == "1")
         self.bucket_at: Dict[object, tuple] = {}
         if not self.overlap:
@@ -311,7 +314,10 @@ class HipProgram:
         cur = torch.cuda.current_stream(self.e.device)
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
-            self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
+            if self.e.sync.strategy == "ps":
+                self.e.sync.reduce_scatter_range(self.e.flat_grad, self.e.grad_shard, b[0], b[1])
+            else:
+                self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
 
     # ------------------------------------------------------------------ fused updates
     def _plan_fused(self) -> None:
