@@ -77,7 +77,11 @@ def lowrank_worth_trying(cfg, world: int) -> bool:
 
 
 def default_candidates(cfg, world: int) -> Tuple[str, ...]:
-    return ("lowrank", "allreduce") if lowrank_worth_trying(cfg, world) else ("allreduce",)
+    """lowrank where it can win, allreduce, and ps (the parameter-server capability:
+    bucketed reduce-scatter to owner shards overlapped with the backward, owner-side
+    optimizer, xGMI all-gather — construct_distribute.py:355-357, 413)."""
+    base = ("allreduce", "ps")
+    return (("lowrank",) + base) if lowrank_worth_trying(cfg, world) else base
 
 
 def pick_strategy(cfg, ds, ctx: DistContext, candidates: Optional[Sequence[str]] = None,

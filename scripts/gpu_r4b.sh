@@ -2,7 +2,7 @@
 # Round-4 horizontal fusion: numerics (test_hip_step), bench A/B (CSA_HFUSE 0/1, 2000 steps)
 # and a kernel trace of the fused program.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp; R=$GRAFT_REPO_ROOT
-timeout -k 10 400 python3 -u -m pytest tests/test_hip_step.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r4b_pytest.log 2>&1
+timeout -k 10 600 python3 -u -m pytest tests/test_hip_step.py tests/test_gpu_dp_overlap.py tests/test_gpu_xgmi.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r4b_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/r4b_pytest.log | tail -3
 [ $rc -ne 0 ] && { grep -B2 -A40 "FAILED\|Error" gpurun_out/r4b_pytest.log | tail -80; exit $rc; }
 for i in 1 2; do for h in 0 1; do

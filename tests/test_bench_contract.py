@@ -33,7 +33,7 @@ def test_bench_world2_cpu_one_json_line():
     assert d["config"]["global_batch"] == 100 and d["config"]["per_gpu_batch"] == 50
     assert d["config"]["parallelism"].startswith("dp2")
     assert d["config"]["collectives"] == "gloo"
-    assert set(d["config"]["strategy_tuning_ms_per_step"]) == {"lowrank", "allreduce"}
+    assert set(d["config"]["strategy_tuning_ms_per_step"]) == {"lowrank", "allreduce", "ps"}
     assert d["value"] > 0 and d["ms_per_step"] > 0
 
 

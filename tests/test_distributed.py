@@ -78,6 +78,15 @@ def _collectives(rank, world, port, out):
     g_ar = x.t() @ dy
     dist.all_reduce(g_ar)
     ok &= torch.allclose(xa.t() @ dya, g_ar, atol=1e-5)
+    # bucketed reduce-scatter to owners: suffix ranges (as the backward produces them)
+    # cover the buffer and end as the whole-buffer reduce-scatter
+    g3 = torch.arange(n, dtype=torch.float32) * (rank + 1) + 0.5
+    sh3 = torch.zeros(n // world)
+    for lo, hi in ((n - 7 * 4, n), (20, n - 7 * 4), (0, 20)):
+        gs.reduce_scatter_range(g3, sh3, lo, hi)
+    ref3 = torch.zeros(n // world)
+    gs.reduce_scatter(g3.clone(), ref3)
+    ok &= torch.allclose(sh3, ref3)
     flat = torch.arange(12, dtype=torch.float32) * (rank + 1)
     ga.allreduce_ranges(flat, [(0, 3), (8, 12)])
     s = float(sum(range(1, world + 1)))
@@ -339,5 +348,5 @@ def test_lowrank_candidate_pruned_at_width():
     from cloud_server_amd.models.dsl import SAMPLE_CONFIG
     from cloud_server_amd.parallel.strategy import default_candidates
     cfg = parse_train_config(dict(SAMPLE_CONFIG, options={"batch_size": 50}))
-    assert default_candidates(cfg, 2) == ("lowrank", "allreduce")
-    assert default_candidates(cfg, 8) == ("allreduce",)
+    assert default_candidates(cfg, 2) == ("lowrank", "allreduce", "ps")
+    assert default_candidates(cfg, 8) == ("allreduce", "ps")

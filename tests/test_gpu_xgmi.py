@@ -230,3 +230,76 @@ def test_xgmi_two_shot_bitexact(world):
         assert "exception" not in res[r], res[r].get("exception")
         assert all(v for k, v in res[r].items() if k != "errors"), (r, res[r])
         assert res[r]["errors"] == 0, res[r]
+
+
+def _worker_ps(rank: int, world: int, port: int, q) -> None:
+    """The ps training step on the xGMI kernels in ``world`` real processes (one GPU):
+    bucketed range reduce-scatter to the owner shards overlapped with the backward, the
+    owner's optimizer on its shard, the xGMI all-gather of the parameters.  The process
+    group is gloo (RCCL refuses two ranks on one device); every collective of the step
+    goes through the peer buffers (CSA_XGMI=1)."""
+    import torch.distributed as dist
+    os.environ.update(CSA_XGMI="1", LOCAL_WORLD_SIZE=str(world), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        from cloud_server_amd.data.datasets import synthetic_mnist
+        from cloud_server_amd.models.dsl import SAMPLE_CONFIG, parse_train_config
+        from cloud_server_amd.parallel.dist import DistContext
+        from cloud_server_amd.runtime.engine import TrainEngine
+        cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3,
+                                      options={"batch_size": 50}))
+        ds = synthetic_mnist(2000, seed=0)
+        res = {}
+        for tag, strategy in (("ps1", "ps"), ("ps2", "ps"), ("ar", "allreduce")):
+            ctx = DistContext(rank=rank, world=world, local_rank=0, backend="nccl", device=dev)
+            eng = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
+            assert eng.backend == "hip", eng.fallback_reason
+            assert eng.sync.xgmi is not None, eng.sync.xgmi_reason
+            if strategy == "ps":
+                assert eng.program.overlap and eng.program.bucket_at
+            for _ in range(12):
+                eng.step()
+            torch.cuda.synchronize()
+            eng.sync.check()
+            res[tag] = {k: eng.model.state.view(k, eng.flat).cpu().clone() for k in eng.model.state.shapes}
+            res[tag + "_ch"] = sorted(eng.sync._choice)
+            eng.sync.xgmi.close()
+            del eng
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, {"exception": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
+    """the ps step on the xGMI kernels is bitwise identical across two runs
+    and on every rank, and within fp32 tolerance of the all-reduce program (same global
+    gradient, different summation grouping)."""
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker_ps, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, d = q.get(timeout=110)
+            res[r] = d
+    finally:
+        for p in ps:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert "exception" not in res[r], res[r].get("exception")
+    assert any(c.startswith("rs:") for c in res[0]["ps1_ch"]) and "ps_ag" in res[0]["ps1_ch"]
+    for k, v in res[0]["ps1"].items():
+        assert torch.equal(v, res[0]["ps2"][k]), k                      # run to run
+        for r in range(1, world):
+            assert torch.equal(v, res[r]["ps1"][k]), (r, k)             # replicas
+        torch.testing.assert_close(v, res[0]["ar"][k], rtol=2e-3, atol=2e-5)
