@@ -61,6 +61,11 @@ class GradSync:
         self.xgmi_tuning: dict = {}      # tag -> {"bytes", "xgmi_us", "rccl_us"} (auto mode)
         self._choice: dict = {}
         self.timing: Optional[list] = None   # set by TrainEngine.probe: (start, end) events per call
+        # CSA_DETERMINISTIC=1: every SUM is formed in a fixed rank order — the
+        # xGMI kernels (one-/two-shot, range reduce-scatter: fixed-order by construction),
+        # or, where they do not apply, an exact all-gather followed by a rank-ordered fold.
+        # Bitwise-repeatable and identical on every rank; never RCCL's reductions.
+        self.det = os.environ.get("CSA_DETERMINISTIC", "0") == "1"
         self._setup_xgmi()
 
     @contextlib.contextmanager
@@ -125,6 +130,8 @@ class GradSync:
         if tag in self._choice:
             return self._choice[tag]
         if torch.cuda.is_current_stream_capturing():
+            if self.det:
+                raise RuntimeError(f"deterministic collective {tag!r} first used inside graph capture")
             return None                  # undecided inside capture: RCCL (same on all ranks)
         nbytes = sum(t.numel() * t.element_size() for t in srcs)
         try:
@@ -137,7 +144,7 @@ class GradSync:
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         choice = ch if flag.item() else None
-        if choice is not None and self.xgmi_mode == "auto":
+        if choice is not None and self.xgmi_mode == "auto" and not self.det:
             times = self._time_paths(ch, srcs, dsts)
             rc_us = times.pop("rccl")
             proto = min(times, key=times.get)
@@ -242,13 +249,33 @@ class GradSync:
             with self._timed():
                 if ch is not None:
                     ch.all_reduce([flat_grad[a:b]])
+                elif self.det:
+                    self._det_sum(flat_grad[a:b])
                 else:
                     dist.all_reduce(flat_grad[a:b])
+
+    # ---- deterministic fallback (no xGMI channel) ----
+    def _det_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape]: every rank's copy of ``t`` (exact: an all-gather moves bits)."""
+        out = torch.empty((self.ctx.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
+        return out
+
+    def _det_sum(self, t: torch.Tensor) -> None:
+        """In-place SUM over ranks, added in rank order 0, 1, .. W-1 on every rank."""
+        g = self._det_gather(t)
+        acc = g[0].clone()
+        for r in range(1, self.ctx.world):
+            acc.add_(g[r])
+        t.copy_(acc)
 
     # ---- ps (sharded) ----
     def reduce_scatter(self, flat_grad: torch.Tensor, shard_out: torch.Tensor) -> None:
         if not self.ctx.enabled:
             shard_out.copy_(flat_grad)
+            return
+        if self.det:
+            self.reduce_scatter_range(flat_grad, shard_out, 0, self.numel)
             return
         with self._timed():
             dist.reduce_scatter_tensor(shard_out, flat_grad)
@@ -274,6 +301,13 @@ class GradSync:
         with self._timed():
             if ch is not None:
                 ch.reduce_scatter_range(flat_grad, lo, hi, sh, shard_out)
+                return
+            if self.det:
+                a, b = max(lo, r * sh), min(hi, (r + 1) * sh)
+                part = flat_grad[lo:hi].clone()
+                self._det_sum(part)              # (every rank sums the range; keeps its part)
+                if a < b:
+                    shard_out[a - r * sh:b - r * sh].copy_(part[a - lo:b - lo])
                 return
             for p in range(W):
                 a, b = max(lo, p * sh), min(hi, (p + 1) * sh)
@@ -341,7 +375,10 @@ class GradSync:
                 ch.all_reduce([flat[lo:hi] for lo, hi in ranges])
                 return
             for lo, hi in ranges:
-                dist.all_reduce(flat[lo:hi])
+                if self.det:
+                    self._det_sum(flat[lo:hi])
+                else:
+                    dist.all_reduce(flat[lo:hi])
 
     def allreduce_tensors(self, tensors, tag: str) -> None:
         """In-place SUM of small fp32 tensors across ranks (SyncBN statistics slabs)."""
@@ -353,7 +390,10 @@ class GradSync:
                 ch.all_reduce(list(tensors))
                 return
             for t in tensors:
-                dist.all_reduce(t)
+                if self.det:
+                    self._det_sum(t)
+                else:
+                    dist.all_reduce(t)
 
     def broadcast_params(self, flat_param: torch.Tensor) -> None:
         """Initial sync from rank 0 (reference: chief runs init_op, construct_distribute.py:379)."""

@@ -85,6 +85,9 @@ class TrainEngine:
         (``runtime.multijob``): its HIP program uses the packed launch profile."""
         self.cfg = cfg
         self.packed = packed
+        if deterministic_mode() and strategy == "lowrank" and ctx is not None and ctx.enabled:
+            # same exact DP math; its gathered-operand GEMMs have no fixed-order variant
+            strategy = "allreduce"
         self.ctx = ctx or DistContext(device=torch.device(device))
         self.device = torch.device(device)
         self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world,

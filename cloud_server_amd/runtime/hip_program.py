@@ -473,8 +473,12 @@ class HipProgram:
         lowering raises Unsupported, and the engine runs the step on eager PyTorch with its
         deterministic algorithms instead."""
         e = self.e
-        if e.ctx.enabled:
-            raise Unsupported("deterministic mode: data parallel steps run on the eager program")
+        # data parallel: every collective of the step is fixed-order (GradSync.det: the xGMI
+        # kernels or an exact all-gather + rank-ordered fold), the pair's stripes are
+        # exclusive rows folded in order before the exchange, the dense layers run the fused
+        # backward in gradient mode (exclusive BN-backward rows)
+        if e.ctx.enabled and e.sync.strategy not in ("allreduce", "ps"):
+            raise Unsupported(f"deterministic mode: {e.sync.strategy} data parallelism")
         if self.pair is None or not self.lib.csa_conv_pair_valu_ok(K.ints(self.pair)):
             raise Unsupported("deterministic mode: network does not start with a VALU conv pair")
         for u in self.units[2:]:

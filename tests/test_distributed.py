@@ -350,3 +350,31 @@ def test_lowrank_candidate_pruned_at_width():
     cfg = parse_train_config(dict(SAMPLE_CONFIG, options={"batch_size": 50}))
     assert default_candidates(cfg, 2) == ("lowrank", "allreduce", "ps")
     assert default_candidates(cfg, 8) == ("allreduce", "ps")
+
+
+def _train_det(rank, world, port, strategy, steps, out):
+    os.environ["CSA_DETERMINISTIC"] = "1"
+    from cloud_server_amd.parallel.dist import shutdown
+    from cloud_server_amd.runtime.engine import TrainEngine
+    ctx = _init(rank, world, port)
+    cfg = parse_train_config(CFG)
+    res = []
+    for _ in range(2):
+        eng = TrainEngine(cfg, synthetic_mnist(256, seed=1), device="cpu", ctx=ctx, strategy=strategy)
+        assert eng.sync.det
+        for _ in range(steps):
+            eng.step()
+        res.append(eng.flat.clone())
+    out[rank] = res
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("strategy", ["allreduce", "ps"])
+def test_deterministic_dp_world4_bitwise(strategy):
+    """CSA_DETERMINISTIC=1 under data parallelism: every sum is rank-ordered (exact
+    all-gather + fold on gloo; the xGMI kernels on the GPU), so two runs and all four
+    replicas are bitwise identical."""
+    out = _spawn(_train_det, 4, strategy, 4)
+    for r in range(4):
+        assert torch.equal(out[r][0], out[r][1]), r
+        assert torch.equal(out[r][0], out[0][0]), r

@@ -239,7 +239,10 @@ def _worker_ps(rank: int, world: int, port: int, q) -> None:
     group is gloo (RCCL refuses two ranks on one device); every collective of the step
     goes through the peer buffers (CSA_XGMI=1)."""
     import torch.distributed as dist
-    os.environ.update(CSA_XGMI="1", LOCAL_WORLD_SIZE=str(world), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    # deterministic mode: the pair's stripes / BN rows are exclusive and folded in order,
+    # so the whole step (not only the collectives) is bitwise repeatable
+    os.environ.update(CSA_XGMI="1", LOCAL_WORLD_SIZE=str(world), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      CSA_DETERMINISTIC="1")
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
@@ -257,6 +260,7 @@ def _worker_ps(rank: int, world: int, port: int, q) -> None:
             eng = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
             assert eng.backend == "hip", eng.fallback_reason
             assert eng.sync.xgmi is not None, eng.sync.xgmi_reason
+            assert eng.program.det and eng.sync.det
             if strategy == "ps":
                 assert eng.program.overlap and eng.program.bucket_at
             for _ in range(12):
@@ -276,9 +280,10 @@ def _worker_ps(rank: int, world: int, port: int, q) -> None:
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
-    """the ps step on the xGMI kernels is bitwise identical across two runs
-    and on every rank, and within fp32 tolerance of the all-reduce program (same global
-    gradient, different summation grouping)."""
+    """the ps step on the xGMI kernels (deterministic mode: data
+    parallel on the HIP program) is bitwise identical across two runs and on every rank,
+    and within fp32 tolerance of the all-reduce program (same global gradient, different
+    summation grouping)."""
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
