@@ -386,17 +386,21 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
       float v = lane < M ? sdy[lane * SN + lcol] : 0.f;
       v = wave_sum(v);
       if (lane == 0) {
-        if (u != wave && !a.gW) {
-          bw = a.bias[n];
-          if (nslot >= 1) bs0 = a.s0b[n];
-          if (nslot >= 2) bs1 = a.s1b[n];
-        }
-        if (a.gW) bw = v * a.scale;
-        else opt_update(a.opt, lr, bw, v * a.scale, bs0, bs1);
-        if (u != wave) {                                   // the first column is stored late
-          (a.gW ? a.gb : a.bias)[n] = bw;
-          if (nslot >= 1) a.s0b[n] = bs0;
-          if (nslot >= 2) a.s1b[n] = bs1;
+        if (u == wave) {                                   // the prefetched first column,
+          if (a.gW) bw = v * a.scale;                      // stored late (du_store_w)
+          else opt_update(a.opt, lr, bw, v * a.scale, bs0, bs1);
+        } else {                                           // further columns (bper > WAVES):
+          float cw = 0.f, c0 = 0.f, c1 = 0.f;              // their own registers — the first
+          if (!a.gW) {                                     // column's values must survive
+            cw = a.bias[n];
+            if (nslot >= 1) c0 = a.s0b[n];
+            if (nslot >= 2) c1 = a.s1b[n];
+          }
+          if (a.gW) cw = v * a.scale;
+          else opt_update(a.opt, lr, cw, v * a.scale, c0, c1);
+          (a.gW ? a.gb : a.bias)[n] = cw;
+          if (nslot >= 1) a.s0b[n] = c0;
+          if (nslot >= 2) a.s1b[n] = c1;
         }
       }
     }

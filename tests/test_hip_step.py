@@ -209,9 +209,7 @@ CASES = {
         {"layer": "norm"},
         {"layer": "active"},
         {"layer": "connect", "hidden": 256},
-        {"layer": "active", "active_func": "relu"},
         {"layer": "connect", "hidden": 256},
-        {"layer": "active", "active_func": "sigmoid"},
         {"layer": "connect", "hidden": 128},
         {"layer": "active", "active_func": "leaky_relu", "param": [0.2]},
     ],
