@@ -192,17 +192,11 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   const long u1 = u0 + per < units ? u0 + per : units;
   const long my_slot = ((long)par * a.world + a.rank) * a.slot_bytes;
 
-  // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included);
-  // op 3: only into its OWNER's slot [rank] (each unit leaves the GPU at most once)
+  // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included)
   for (long u = u0 + t; u < u1; u += blockDim.x) {
     const long off = u << 4;
     const XgSeg& s = a.seg[xg_find(a, off)];
     const uint4 v = *reinterpret_cast<const uint4*>(s.src + (off - s.off));
-    if (a.op == 3) {
-      const int p = (int)((a.rs_lo + u) / a.rs_sh);
-      *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
-      continue;
-    }
 #pragma unroll
     for (int p = 0; p < XG_MAXR; ++p)
       if (p < a.world) *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
@@ -245,20 +239,6 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
       const long off = u << 4;
       const XgSeg& s = a.seg[xg_find(a, off)];
       const long so = off - s.off;
-      if (a.op == 3) {           // reduce-scatter: my units of the range, fixed rank order
-        const long g = a.rs_lo + u;
-        if (g / a.rs_sh != a.rank) continue;
-        float4 v[XG_MAXR];
-#pragma unroll
-        for (int r = 0; r < XG_MAXR; ++r)
-          if (r < a.world) v[r] = *reinterpret_cast<const float4*>(mine + (long)r * a.slot_bytes + off);
-        float4 acc = v[0];
-#pragma unroll
-        for (int r = 1; r < XG_MAXR; ++r)
-          if (r < a.world) { acc.x += v[r].x; acc.y += v[r].y; acc.z += v[r].z; acc.w += v[r].w; }
-        *reinterpret_cast<float4*>(a.rs_dst + ((g - (long)a.rank * a.rs_sh) << 4)) = acc;
-        continue;
-      }
       if (a.op == 0) {           // all-gather: out is rank-major [world][seg.bytes]
         uint4 v[XG_MAXR];
 #pragma unroll
@@ -283,6 +263,59 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   }
 
   // 4) the last block to finish advances the epoch for the next call on this channel
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(a.done, 1u);
+    if (prev == (unsigned)nb - 1) {
+      *a.done = 0;
+      *a.seq = e;
+      __threadfence();
+    }
+  }
+}
+
+// op 3: reduce-scatter of a range with GLOBAL ownership (its own kernel: the extra code
+// raised the shared kernel's registers from 89 to 149, which cut its residency to 3
+// blocks per CU — several ranks sharing one GPU then no longer fit co-resident and their
+// peer waits time out).  Same slot / flag / epoch protocol as the one-shot path: every
+// unit goes only to its OWNER's slot [rank] (it leaves the GPU at most once), flags go to
+// every rank, the owner sums its units of the range in fixed rank order.
+__global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs a) {
+  __shared__ int s_abort;
+  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  if (t == 0) s_abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  __syncthreads();
+  if (s_abort) return;
+  const unsigned e = *a.seq + 1u;
+  const int par = e & 1u;
+  const long units = a.msg_bytes >> 4;
+  const long per = (units + nb - 1) / nb;
+  const long u0 = b * per < units ? b * per : units;
+  const long u1 = u0 + per < units ? u0 + per : units;
+  const long my_slot = ((long)par * a.world + a.rank) * a.slot_bytes;
+  const char* src = a.seg[0].src;
+  for (long u = u0 + t; u < u1; u += blockDim.x) {
+    const int p = (int)((a.rs_lo + u) / a.rs_sh);
+    *reinterpret_cast<uint4*>(a.buf[p] + my_slot + (u << 4)) = *reinterpret_cast<const uint4*>(src + (u << 4));
+  }
+  const long fidx = ((long)par * XG_MAXB + b) * XG_MAXR;
+  xg_publish(a, fidx, e);
+  if (xg_wait(a, fidx, e, &s_abort)) {
+    const char* mine = a.buf[a.rank] + (long)par * a.world * a.slot_bytes;
+    // my units of this block's chunk: [max(u0, own_lo), min(u1, own_hi))
+    const long own_lo = (long)a.rank * a.rs_sh - a.rs_lo, own_hi = own_lo + a.rs_sh;
+    const long c0 = u0 > own_lo ? u0 : own_lo, c1 = u1 < own_hi ? u1 : own_hi;
+    for (long u = c0 + t; u < c1; u += blockDim.x) {
+      const long off = u << 4;
+      float4 acc = *reinterpret_cast<const float4*>(mine + off);
+      for (int r = 1; r < a.world; ++r) {
+        const float4 v = *reinterpret_cast<const float4*>(mine + (long)r * a.slot_bytes + off);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      *reinterpret_cast<float4*>(a.rs_dst + ((u - own_lo) << 4)) = acc;
+    }
+  }
   __syncthreads();
   if (t == 0) {
     __threadfence();
@@ -383,6 +416,6 @@ CSA_API int csa_xgmi_reduce_scatter(int rank, int world, long slot_bytes, void* 
   const long units = bytes >> 4;
   int nb = nblocks > 0 ? nblocks : (int)((units + 511) / 512);
   nb = nb < 1 ? 1 : (nb > XG_MAXB ? XG_MAXB : nb);
-  hipLaunchKernelGGL(xgmi_kernel, dim3(nb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(xgmi_rs_kernel, dim3(nb), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
