@@ -161,6 +161,10 @@ def _worker_twoshot(rank: int, world: int, port: int, q) -> None:
             segs = [xs[rank].clone()] + ([ys[rank].clone()] if n2 else [])
             one = [t.clone() for t in segs]
             ch = comm.channel(f"c{n1}", sum(t.nbytes for t in segs))
+            # every rank shares this ONE GPU here: all ranks' workgroups must be co-resident
+            # (each waits on the others' flags), so they split the chip's ~1280 block slots
+            # (5 x 256-thread blocks per CU); on a node each rank owns a GPU and uses 256
+            ch.nblocks = min(256, 1024 // world)
             ch.all_reduce(one, protocol="oneshot")
             two = [t.clone() for t in segs]
             ch.all_reduce(two, protocol="twoshot")
