@@ -267,10 +267,17 @@ def _worker_ps(rank: int, world: int, port: int, q) -> None:
             assert eng.program.det and eng.sync.det
             if strategy == "ps":
                 assert eng.program.overlap and eng.program.bucket_at
-            for _ in range(12):
+            for i in range(12):
                 eng.step()
+                if i < 3:                       # diagnostics: the first steps one by one
+                    torch.cuda.synchronize()
+                    bad = sorted(t for t, c in eng.sync.xgmi.channels.items() if c.error())
+                    if bad:
+                        raise RuntimeError(f"{tag}: step {i}: channels timed out: {bad}")
             torch.cuda.synchronize()
-            eng.sync.check()
+            bad = sorted(t for t, c in eng.sync.xgmi.channels.items() if c.error())
+            if bad:
+                raise RuntimeError(f"{tag}: channels timed out: {bad}")
             res[tag] = {k: eng.model.state.view(k, eng.flat).cpu().clone() for k in eng.model.state.shapes}
             res[tag + "_ch"] = sorted(eng.sync._choice)
             eng.sync.xgmi.close()
