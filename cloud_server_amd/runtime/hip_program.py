@@ -1459,6 +1459,9 @@ class HipProgram:
                 K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(xw), 1.0, K.ptr(getattr(tf, "bn_tab", None)),
                 K.ptr(u.du_part), K.ptr(u.du_cnt), K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]),
                 *head, K.ptr(e.dstep), st), "dense_bwd_grad")
+            if self.det and tf.has_bn:        # exclusive rows -> row 0, fixed order
+                self._row_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],
+                               tf.bwd_slab, 0, st)
             return
         self._rc(lib.csa_dense_bwd_update_head(
             K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),

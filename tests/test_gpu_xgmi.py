@@ -243,6 +243,9 @@ def _worker_ps(rank: int, world: int, port: int, q) -> None:
     group is gloo (RCCL refuses two ranks on one device); every collective of the step
     goes through the peer buffers (CSA_XGMI=1)."""
     import torch.distributed as dist
+    import faulthandler
+    os.makedirs("gpurun_out", exist_ok=True)
+    faulthandler.enable(open(f"gpurun_out/ps_worker_{world}_{rank}.txt", "w"), all_threads=True)
     # deterministic mode: the pair's stripes / BN rows are exclusive and folded in order,
     # so the whole step (not only the collectives) is bitwise repeatable
     os.environ.update(CSA_XGMI="1", LOCAL_WORLD_SIZE=str(world), HSA_ENABLE_IPC_MODE_LEGACY="0",
@@ -304,13 +307,17 @@ def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
     res = {}
     try:
         for _ in range(world):
-            r, d = q.get(timeout=110)
+            try:
+                r, d = q.get(timeout=110)
+            except EOFError:
+                break
             res[r] = d
     finally:
         for p in ps:
             p.join(timeout=20)
             if p.is_alive():
                 p.kill()
+    assert len(res) == world, f"workers died: exit codes {[p.exitcode for p in ps]}, results {sorted(res)}"
     for r in range(world):
         assert "exception" not in res[r], res[r].get("exception")
     assert any(c.startswith("rs:") for c in res[0]["ps1_ch"]) and "ps_ag" in res[0]["ps1_ch"]
