@@ -281,7 +281,9 @@ def _worker_ps(rank: int, world: int, port: int, q) -> None:
             bad = sorted(t for t, c in eng.sync.xgmi.channels.items() if c.error())
             if bad:
                 raise RuntimeError(f"{tag}: channels timed out: {bad}")
-            res[tag] = {k: eng.model.state.view(k, eng.flat).cpu().clone() for k in eng.model.state.shapes}
+            # numpy copies: a tensor would travel through shared memory that dies with this
+            # process before the parent reads it
+            res[tag] = {k: eng.model.state.view(k, eng.flat).cpu().numpy().copy() for k in eng.model.state.shapes}
             res[tag + "_ch"] = sorted(eng.sync._choice)
             eng.sync.xgmi.close()
             del eng
@@ -321,8 +323,9 @@ def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
     for r in range(world):
         assert "exception" not in res[r], res[r].get("exception")
     assert any(c.startswith("rs:") for c in res[0]["ps1_ch"]) and "ps_ag" in res[0]["ps1_ch"]
+    import numpy as np
     for k, v in res[0]["ps1"].items():
-        assert torch.equal(v, res[0]["ps2"][k]), k                      # run to run
+        assert np.array_equal(v, res[0]["ps2"][k]), k                   # run to run
         for r in range(1, world):
-            assert torch.equal(v, res[r]["ps1"][k]), (r, k)             # replicas
-        torch.testing.assert_close(v, res[0]["ar"][k], rtol=2e-3, atol=2e-5)
+            assert np.array_equal(v, res[r]["ps1"][k]), (r, k)          # replicas
+        torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(res[0]["ar"][k]), rtol=2e-3, atol=2e-5)
