@@ -199,11 +199,19 @@ def self_test(comm: XgmiComm) -> bool:
     rank-dependent data, verified on the host; every rank learns whether ALL passed."""
     dev = comm.device
     ok = True
+    # every rank loads the kernel library's code object BEFORE any rank launches a waiting
+    # kernel: a rank still loading it (seconds, with several processes starting at once)
+    # would otherwise leave its peers' bounded waits to time out
+    lib = K.load(required=True)
+    z = torch.zeros(4, device=dev)
+    lib.csa_zero((C.c_void_p * 1)(z.data_ptr()), (C.c_long * 1)(4), 1, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier(group=comm.group)
     try:
         W, r = comm.world, comm.rank
         x = torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * r
         out = torch.empty(W * 1024, dtype=torch.float32, device=dev)
-        ch = XgmiChannel(comm.rank, W, 4096, dev, comm.group, timeout_s=5.0)
+        ch = XgmiChannel(comm.rank, W, 4096, dev, comm.group, timeout_s=20.0)
         ch.all_gather([(x, out)])
         want = torch.cat([torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * k for k in range(W)])
         y = x.clone()
