@@ -98,7 +98,8 @@ class GradSync:
             return
         comm.close()
         if mode in ("1", "on", "true"):
-            raise RuntimeError("CSA_XGMI=1 but the xGMI peer-buffer self-test failed")
+            raise RuntimeError("CSA_XGMI=1 but the xGMI peer-buffer self-test failed (rank "
+                               f"{self.ctx.rank}: {getattr(comm, 'self_test_reason', 'another rank failed')})")
         self.xgmi_reason = "self-test failed: RCCL"
 
     def check(self) -> None:

@@ -220,11 +220,15 @@ def self_test(comm: XgmiComm) -> bool:
         ch.all_reduce([y2], protocol="twoshot" if W > 2 else "oneshot")
         torch.cuda.synchronize(dev)
         want_sum = W * torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * sum(range(W))
-        ok = (ch.error() == 0 and torch.equal(out, want) and torch.equal(y, want_sum)
-              and torch.equal(y2, want_sum))
+        checks = {"timeout": ch.error() == 0, "gather": torch.equal(out, want),
+                  "oneshot": torch.equal(y, want_sum), "twoshot": torch.equal(y2, want_sum)}
+        ok = all(checks.values())
+        if not ok:
+            comm.self_test_reason = "failed: " + ",".join(k for k, v in checks.items() if not v)
         ch.close()
-    except Exception:
+    except Exception as exc:
         ok = False
+        comm.self_test_reason = f"{type(exc).__name__}: {exc}"
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
     return bool(flag.item())
