@@ -320,8 +320,8 @@ def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
             if p.is_alive():
                 p.kill()
     assert len(res) == world, f"workers died: exit codes {[p.exitcode for p in ps]}, results {sorted(res)}"
-    for r in range(world):
-        assert "exception" not in res[r], res[r].get("exception")
+    errs = {r: res[r]["exception"].strip().splitlines()[-1] for r in range(world) if "exception" in res[r]}
+    assert not errs, errs
     assert any(c.startswith("rs:") for c in res[0]["ps1_ch"]) and "ps_ag" in res[0]["ps1_ch"]
     import numpy as np
     for k, v in res[0]["ps1"].items():
