@@ -61,6 +61,12 @@ struct XgArgs {
   unsigned long long timeout_ticks;
 };
 
+// Byte offset of parity half `par` of a receive buffer [2][world][slot + 32]: every
+// protocol (one-shot slots, two-shot phases, range reduce-scatter) stays inside its half.
+__host__ __device__ __forceinline__ long xg_par_base(const XgArgs& a, int par) {
+  return (long)par * ((long)a.world * a.slot_bytes + 32L * a.world);
+}
+
 __device__ __forceinline__ int xg_find(const XgArgs& a, long off) {
   int s = 0;
 #pragma unroll 1
@@ -121,8 +127,11 @@ __device__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
   const long per = (S + nb - 1) / nb;
   const long v0 = b * per < S ? b * per : S;
   const long v1 = v0 + per < S ? v0 + per : S;
-  const long area0 = ((long)par * 2 + 0) * W * shard;   // phase-1 slots [src][shard]
-  const long area1 = ((long)par * 2 + 1) * W * shard;   // phase-2 slots [owner][shard]
+  // inside THIS parity's half of the buffer, exactly where the one-shot layout keeps its
+  // parity: a channel may mix the protocols, and the double-buffer guarantee (a peer one
+  // epoch ahead writes only the OTHER half) must hold across them
+  const long area0 = xg_par_base(a, par);                // phase-1 slots [src][shard]
+  const long area1 = area0 + (long)W * shard;            // phase-2 slots [owner][shard]
   const long f1 = ((long)(0 * 2 + par) * XG_MAXB + b) * XG_MAXR;
   const long f2 = ((long)(1 * 2 + par) * XG_MAXB + b) * XG_MAXR;
 
@@ -190,7 +199,7 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   const long per = (units + nb - 1) / nb;
   const long u0 = b * per < units ? b * per : units;
   const long u1 = u0 + per < units ? u0 + per : units;
-  const long my_slot = ((long)par * a.world + a.rank) * a.slot_bytes;
+  const long my_slot = xg_par_base(a, par) + (long)a.rank * a.slot_bytes;
 
   // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included)
   for (long u = u0 + t; u < u1; u += blockDim.x) {
@@ -234,7 +243,7 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
 
   // 3) consume from local memory
   if (!s_abort) {
-    const char* mine = a.buf[a.rank] + (long)par * a.world * a.slot_bytes;
+    const char* mine = a.buf[a.rank] + xg_par_base(a, par);
     for (long u = u0 + t; u < u1; u += blockDim.x) {
       const long off = u << 4;
       const XgSeg& s = a.seg[xg_find(a, off)];
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs a) {
   const long per = (units + nb - 1) / nb;
   const long u0 = b * per < units ? b * per : units;
   const long u1 = u0 + per < units ? u0 + per : units;
-  const long my_slot = ((long)par * a.world + a.rank) * a.slot_bytes;
+  const long my_slot = xg_par_base(a, par) + (long)a.rank * a.slot_bytes;
   const char* src = a.seg[0].src;
   for (long u = u0 + t; u < u1; u += blockDim.x) {
     const int p = (int)((a.rs_lo + u) / a.rs_sh);
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs a) {
   const long fidx = ((long)par * XG_MAXB + b) * XG_MAXR;
   xg_publish(a, fidx, e);
   if (xg_wait(a, fidx, e, &s_abort)) {
-    const char* mine = a.buf[a.rank] + (long)par * a.world * a.slot_bytes;
+    const char* mine = a.buf[a.rank] + xg_par_base(a, par);
     // my units of this block's chunk: [max(u0, own_lo), min(u1, own_hi))
     const long own_lo = (long)a.rank * a.rs_sh - a.rs_lo, own_hi = own_lo + a.rs_sh;
     const long c0 = u0 > own_lo ? u0 : own_lo, c1 = u1 < own_hi ? u1 : own_hi;
@@ -369,9 +378,9 @@ CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* con
     off += seg_bytes[i];
   }
   if (off > slot_bytes) return -3;
-  if (op == 2) {                // [2 parity][2 phase][world][shard] must fit the slot area
+  if (op == 2) {                // [2 phase][world][shard] must fit one parity half
     const long S = ((off >> 4) + world - 1) / world;
-    if (4L * world * (S << 4) > 2L * world * slot_bytes + 64L * world) return -4;
+    if (2L * world * (S << 4) > (long)world * slot_bytes + 32L * world) return -4;
   }
   a.msg_bytes = off;
   for (int r = 0; r < world; ++r) {
