@@ -170,9 +170,11 @@ class XgmiComm:
     """Channels by call-site tag, created lazily (collectively) on first use — which must
     happen outside HIP-graph capture (the engine's eager warm-up steps do it)."""
 
-    def __init__(self, rank: int, world: int, device: torch.device, group=None, timeout_s: float = 20.0):
+    def __init__(self, rank: int, world: int, device: torch.device, group=None, timeout_s: Optional[float] = None):
         self.rank, self.world, self.device, self.group = rank, world, device, group
-        self.timeout_s = timeout_s
+        # bound of every peer wait (CSA_XGMI_TIMEOUT_S, default 20 s): a missing peer
+        # poisons the channel instead of hanging the GPU
+        self.timeout_s = timeout_s if timeout_s is not None else float(os.environ.get("CSA_XGMI_TIMEOUT_S", "20"))
         self.channels: Dict[str, XgmiChannel] = {}
 
     def channel(self, tag: str, nbytes: int) -> XgmiChannel:

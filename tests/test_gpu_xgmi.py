@@ -144,98 +144,6 @@ def test_xgmi_two_processes():
     assert poisoned and 0.3 < first < 5.0 and second < 0.5, res[0]["timeout"]
 
 
-def _worker_twoshot(rank: int, world: int, port: int, q) -> None:
-    import torch.distributed as dist
-    from cloud_server_amd.parallel import xgmi as X
-    try:
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        comm = X.XgmiComm(rank, world, dev)
-        res = {}
-        gens = [torch.Generator(dev).manual_seed(1000 + r) for r in range(world)]
-        # sizes: uneven shards, fewer units than ranks x blocks, multi-segment, 9.1 MB grad
-        for n1, n2 in ((4, 0), (1028, 0), (6400, 36), (2276220, 0)):
-            xs = [torch.randn(n1, device=dev, generator=gens[r]) for r in range(world)]
-            ys = [torch.randn(n2, device=dev, generator=gens[r]) for r in range(world)] if n2 else None
-            segs = [xs[rank].clone()] + ([ys[rank].clone()] if n2 else [])
-            one = [t.clone() for t in segs]
-            ch = comm.channel(f"c{n1}", sum(t.nbytes for t in segs))
-            # every rank shares this ONE GPU here: all ranks' workgroups must be co-resident
-            # (each waits on the others' flags), so they split the chip's ~1280 block slots
-            # (5 x 256-thread blocks per CU); on a node each rank owns a GPU and uses 256
-            ch.nblocks = min(256, 1024 // world)
-            ch.all_reduce(one, protocol="oneshot")
-            two = [t.clone() for t in segs]
-            ch.all_reduce(two, protocol="twoshot")
-            torch.cuda.synchronize()
-            want = xs[0].clone()
-            for r in range(1, world):
-                want += xs[r]                  # the kernels' fixed rank order
-            ok = torch.equal(two[0], one[0]) and torch.equal(two[0], want)
-            if n2:
-                w2 = ys[0].clone()
-                for r in range(1, world):
-                    w2 += ys[r]
-                ok &= torch.equal(two[1], w2) and torch.equal(one[1], w2)
-            res[f"n{n1}"] = ok
-        # 40 back-to-back two-shot calls, then the same inside a replayed HIP graph
-        ch = comm.channel("seq", 4 * 50000)
-        outs = []
-        for i in range(40):
-            v = torch.full((50000,), float(i + rank), device=dev)
-            ch.all_reduce([v], protocol="twoshot")
-            outs.append((i, v))
-        torch.cuda.synchronize()
-        res["sequence"] = all(bool(torch.all(v == sum(i + r for r in range(world))).item()) for i, v in outs)
-        buf = torch.zeros(50000, device=dev)
-        g = torch.cuda.CUDAGraph()
-        with capture(g):
-            ch.all_reduce([buf], protocol="twoshot")
-        ok = True
-        for it in range(10):
-            buf.fill_(float(it * 7 + rank))
-            g.replay()
-            torch.cuda.synchronize()
-            ok &= bool(torch.all(buf == sum(it * 7 + r for r in range(world))).item())
-        res["graph"] = ok
-        res["errors"] = sum(c.error() for c in comm.channels.values())
-        comm.close()
-        dist.destroy_process_group()
-        q.put((rank, res))
-    except Exception:  # pragma: no cover - reported to the parent
-        import traceback
-        q.put((rank, {"exception": traceback.format_exc()}))
-
-
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_xgmi_two_shot_bitexact(world):
-    """Two-shot all-reduce (reduce-scatter + all-gather over the peer buffers) equals the
-    one-shot result and the host's fixed-order sum BITWISE, on every rank, for uneven
-    shards, multi-segment messages, back-to-back calls and graph replays."""
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_worker_twoshot, args=(r, world, port, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = {}
-    try:
-        for _ in range(world):
-            r, d = q.get(timeout=100)
-            res[r] = d
-    finally:
-        for p in ps:
-            p.join(timeout=20)
-            if p.is_alive():
-                p.kill()
-    for r in range(world):
-        assert "exception" not in res[r], res[r].get("exception")
-        assert all(v for k, v in res[r].items() if k != "errors"), (r, res[r])
-        assert res[r]["errors"] == 0, res[r]
-
-
 def _worker_ps(rank: int, world: int, port: int, q) -> None:
     """The ps training step on the xGMI kernels in ``world`` real processes (one GPU):
     bucketed range reduce-scatter to the owner shards overlapped with the backward, the
@@ -329,3 +237,95 @@ def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
         for r in range(1, world):
             assert np.array_equal(v, res[r]["ps1"][k]), (r, k)          # replicas
         torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(res[0]["ar"][k]), rtol=2e-3, atol=2e-5)
+
+
+def _worker_twoshot(rank: int, world: int, port: int, q) -> None:
+    import torch.distributed as dist
+    from cloud_server_amd.parallel import xgmi as X
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        comm = X.XgmiComm(rank, world, dev)
+        res = {}
+        gens = [torch.Generator(dev).manual_seed(1000 + r) for r in range(world)]
+        # sizes: uneven shards, fewer units than ranks x blocks, multi-segment, 9.1 MB grad
+        for n1, n2 in ((4, 0), (1028, 0), (6400, 36), (2276220, 0)):
+            xs = [torch.randn(n1, device=dev, generator=gens[r]) for r in range(world)]
+            ys = [torch.randn(n2, device=dev, generator=gens[r]) for r in range(world)] if n2 else None
+            segs = [xs[rank].clone()] + ([ys[rank].clone()] if n2 else [])
+            one = [t.clone() for t in segs]
+            ch = comm.channel(f"c{n1}", sum(t.nbytes for t in segs))
+            # every rank shares this ONE GPU here: all ranks' workgroups must be co-resident
+            # (each waits on the others' flags), so they split the chip's ~1280 block slots
+            # (5 x 256-thread blocks per CU); on a node each rank owns a GPU and uses 256
+            ch.nblocks = min(256, 1024 // world)
+            ch.all_reduce(one, protocol="oneshot")
+            two = [t.clone() for t in segs]
+            ch.all_reduce(two, protocol="twoshot")
+            torch.cuda.synchronize()
+            want = xs[0].clone()
+            for r in range(1, world):
+                want += xs[r]                  # the kernels' fixed rank order
+            ok = torch.equal(two[0], one[0]) and torch.equal(two[0], want)
+            if n2:
+                w2 = ys[0].clone()
+                for r in range(1, world):
+                    w2 += ys[r]
+                ok &= torch.equal(two[1], w2) and torch.equal(one[1], w2)
+            res[f"n{n1}"] = ok
+        # 40 back-to-back two-shot calls, then the same inside a replayed HIP graph
+        ch = comm.channel("seq", 4 * 50000)
+        outs = []
+        for i in range(40):
+            v = torch.full((50000,), float(i + rank), device=dev)
+            ch.all_reduce([v], protocol="twoshot")
+            outs.append((i, v))
+        torch.cuda.synchronize()
+        res["sequence"] = all(bool(torch.all(v == sum(i + r for r in range(world))).item()) for i, v in outs)
+        buf = torch.zeros(50000, device=dev)
+        g = torch.cuda.CUDAGraph()
+        with capture(g):
+            ch.all_reduce([buf], protocol="twoshot")
+        ok = True
+        for it in range(10):
+            buf.fill_(float(it * 7 + rank))
+            g.replay()
+            torch.cuda.synchronize()
+            ok &= bool(torch.all(buf == sum(it * 7 + r for r in range(world))).item())
+        res["graph"] = ok
+        res["errors"] = sum(c.error() for c in comm.channels.values())
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, {"exception": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_xgmi_two_shot_bitexact(world):
+    """Two-shot all-reduce (reduce-scatter + all-gather over the peer buffers) equals the
+    one-shot result and the host's fixed-order sum BITWISE, on every rank, for uneven
+    shards, multi-segment messages, back-to-back calls and graph replays."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker_twoshot, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, d = q.get(timeout=100)
+            res[r] = d
+    finally:
+        for p in ps:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert "exception" not in res[r], res[r].get("exception")
+        assert all(v for k, v in res[r].items() if k != "errors"), (r, res[r])
+        assert res[r]["errors"] == 0, res[r]
