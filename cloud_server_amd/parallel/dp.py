@@ -46,11 +46,13 @@ DEFAULT_BUCKET_BYTES = 32 << 20   # one bucket covers the sample model's 9.1 MB 
 class GradSync:
     def __init__(self, ctx: DistContext, numel: int, strategy: str = "allreduce",
                  bucket_bytes: int = DEFAULT_BUCKET_BYTES):
-        if strategy not in ("allreduce", "ps", "lowrank"):
+        if strategy not in ("allreduce", "ps", "lowrank", "async_ps"):
             raise ValueError(f"unknown DP strategy {strategy!r}")
         self.ctx, self.numel, self.strategy = ctx, numel, strategy
-        if strategy == "ps" and ctx.enabled and numel % ctx.world:
-            raise ValueError("ps strategy needs the flat buffer padded to a multiple of world")
+        # parameters / optimizer slots sharded over owner ranks (the PS placement)
+        self.sharded = strategy in ("ps", "async_ps") and ctx.enabled
+        if self.sharded and numel % ctx.world:
+            raise ValueError(f"{strategy} strategy needs the flat buffer padded to a multiple of world")
         self.shard = numel // ctx.world if ctx.enabled else numel
         self.bucket_elems = max(1, bucket_bytes // 4)
         # (grouped RCCL launches for the multi-tensor collectives are not used: a grouped
@@ -225,10 +227,12 @@ class GradSync:
     @property
     def grad_scale(self) -> float:
         """Factor folded into dL/dlogits so that SUM-reduced grads are the global mean."""
+        if self.strategy == "async_ps":
+            return 1.0        # each push is ONE worker's update, applied on its own (PS semantics)
         return 1.0 / self.ctx.world if self.ctx.enabled else 1.0
 
     def shard_range(self) -> Tuple[int, int]:
-        if self.strategy != "ps" or not self.ctx.enabled:
+        if not self.sharded:
             return 0, self.numel
         r = self.ctx.rank
         return r * self.shard, (r + 1) * self.shard

@@ -76,7 +76,7 @@ def load(path: str, map_location="cpu") -> Dict[str, Any]:
 def full_slots(eng) -> torch.Tensor:
     """Optimizer slots for the WHOLE flat buffer.  Under the sharded "ps" strategy each
     rank owns a slice, so this is a collective (every rank must call it)."""
-    if eng.sync.strategy == "ps" and eng.ctx.enabled and eng.slots.numel():
+    if eng.sync.sharded and eng.slots.numel():
         import torch.distributed as dist
         full = torch.empty(eng.slots.shape[0], eng.flat.numel(), device=eng.slots.device)
         for i in range(eng.slots.shape[0]):
@@ -147,7 +147,7 @@ class AsyncCheckpointer:
         import threading
         self.eng, self.model_dir, self.keep = eng, model_dir, keep
         self._threading = threading
-        self.async_ok = (eng.device.type == "cuda" and not (eng.sync.strategy == "ps" and eng.ctx.enabled))
+        self.async_ok = eng.device.type == "cuda" and not eng.sync.sharded
         self._thread = None
         self._error: Optional[BaseException] = None
         self.saved = 0

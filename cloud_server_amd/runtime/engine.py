@@ -104,6 +104,12 @@ class TrainEngine:
         lo, hi = self.sync.shard_range()
         self.slots = optim_ref.init_slots(self.opt_id, hi - lo, self.device)
         self.grad_shard = torch.zeros(hi - lo, device=self.device) if strategy == "ps" else None
+        # asynchronous bounded-staleness PS (parallel/async_ps.py): the reference's own
+        # semantics — pushes applied one by one by their shard's owner as they arrive
+        self.aps = None
+        if strategy == "async_ps" and self.ctx.enabled:
+            from ..parallel.async_ps import make_async_ps
+            self.aps = make_async_ps(self, lo, hi)
         self.data = DeviceDataset(train, self.device)
         self.stream = BatchStream(self.data.n, cfg.batch_size, self.device, seed=cfg.seed,
                                   chunk=stream_chunk, rank=self.ctx.rank, world=self.ctx.world)
@@ -152,6 +158,9 @@ class TrainEngine:
 
     def apply_update(self) -> None:
         """Grad sync + optimizer on the flat buffers (torch ops; the HIP program fuses this)."""
+        if self.aps is not None:
+            self.aps.step(self.flat_grad, self.flat, self.slots)
+            return
         if self.sync.strategy == "ps" and self.ctx.enabled:
             lo, hi = self.sync.shard_range()
             self.sync.reduce_scatter(self.flat_grad, self.grad_shard)
@@ -351,6 +360,18 @@ class TrainEngine:
         self.sync_device()
         self._comm_ms = float(sum(a.elapsed_time(b) for a, b in ev))
         return self._comm_ms
+
+    def finish_async(self) -> None:
+        """async_ps: apply every outstanding push and pull the final shards (replicas then
+        agree); a no-op for the synchronous strategies."""
+        if self.aps is not None:
+            self.sync_device()
+            self.aps.finish(self.flat, self.slots)
+            self.sync_device()
+
+    def staleness(self) -> int:
+        """async_ps: the largest parameter staleness (clocks) any step of this rank saw."""
+        return int(self.aps.max_staleness) if self.aps is not None else 0
 
     def comm_ms_per_step(self) -> float:
         return getattr(self, "_comm_ms", 0.0)

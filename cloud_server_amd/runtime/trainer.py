@@ -323,6 +323,7 @@ class JobRun:
 
     def finish(self) -> Dict[str, Any]:
         eng, state, chief = self.eng, self.state, self.chief
+        eng.finish_async()            # async_ps: drain outstanding pushes, pull final shards
         eng.sync_device()
         # a peer wait that timed out after the last log step left this rank's gradient
         # un-reduced: fail before evaluating / checkpointing diverged parameters
