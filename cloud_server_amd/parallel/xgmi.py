@@ -191,6 +191,15 @@ class XgmiComm:
             ch.check()
 
     def close(self) -> None:
+        """Collective (every rank calls it): a rank frees its buffers only once EVERY rank's
+        last call has drained — a peer still running would otherwise write through its
+        mapping into memory this rank has freed, and the allocator may already have handed
+        those bytes to a new channel (whose flags then read stale epochs)."""
+        if not self.channels:
+            return
+        torch.cuda.synchronize(self.device)
+        if dist.is_initialized():
+            dist.barrier(group=self.group)
         for ch in self.channels.values():
             ch.close()
         self.channels.clear()
@@ -209,6 +218,7 @@ def self_test(comm: XgmiComm) -> bool:
     lib.csa_zero((C.c_void_p * 1)(z.data_ptr()), (C.c_long * 1)(4), 1, torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
     dist.barrier(group=comm.group)
+    ch = None
     try:
         W, r = comm.world, comm.rank
         x = torch.arange(1024, dtype=torch.float32, device=dev) + 1000.0 * r
@@ -227,13 +237,16 @@ def self_test(comm: XgmiComm) -> bool:
         ok = all(checks.values())
         if not ok:
             comm.self_test_reason = "failed: " + ",".join(k for k, v in checks.items() if not v)
-        ch.close()
     except Exception as exc:
         ok = False
         comm.self_test_reason = f"{type(exc).__name__}: {exc}"
+    torch.cuda.synchronize(dev)
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
-    return bool(flag.item())
+    passed = bool(flag.item())       # every rank's kernels have drained: safe to free
+    if ch is not None:
+        ch.close()
+    return passed
 
 
 def enabled_by_env() -> str:
