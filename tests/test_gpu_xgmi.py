@@ -208,6 +208,11 @@ def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
     parallel on the HIP program) is bitwise identical across two runs and on every rank,
     and within fp32 tolerance of the all-reduce program (same global gradient, different
     summation grouping)."""
+    import subprocess
+    try:       # which processes share the GPU now (reported only when the test fails)
+        gpu_pids = subprocess.run(["rocm-smi", "--showpids"], capture_output=True, text=True, timeout=20).stdout
+    except Exception as exc:  # pragma: no cover
+        gpu_pids = repr(exc)
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -229,7 +234,7 @@ def test_xgmi_ps_step_bitwise_and_matches_allreduce(world):
                 p.kill()
     assert len(res) == world, f"workers died: exit codes {[p.exitcode for p in ps]}, results {sorted(res)}"
     errs = {r: res[r]["exception"].strip().splitlines()[-1] for r in range(world) if "exception" in res[r]}
-    assert not errs, errs
+    assert not errs, (errs, gpu_pids)
     assert any(c.startswith("rs:") for c in res[0]["ps1_ch"]) and "ps_ag" in res[0]["ps1_ch"]
     import numpy as np
     for k, v in res[0]["ps1"].items():
