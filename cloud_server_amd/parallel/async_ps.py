@@ -181,6 +181,138 @@ class AsyncPSGloo:
         self.sends = []
 
 
+class AsyncPSDevice:
+    """The protocol on the GPU: IPC-mapped uncached peer buffers (inbox ring, arrival flags,
+    double-buffered seqlocked outbox) and ONE ``aps_kernel`` launch per step
+    (csrc/comm/async_ps.hip), capturable in the step's HIP graph."""
+
+    def __init__(self, rank: int, world: int, shard: int, staleness: int, opt_id: int, lr: float,
+                 device: torch.device, group=None, timeout_s: Optional[float] = None):
+        from ..ops import fused as K
+        if shard % 4:
+            raise ValueError("async_ps: the shard must be a multiple of 4 floats")
+        self.lib = K.load(required=True)
+        self.r, self.W, self.sh, self.s = rank, world, shard, staleness
+        self.opt_id, self.lr, self.device = opt_id, lr, device
+        self.R = 2 * staleness + 2
+        self.nb = max(1, min(256, (shard + 4095) // 4096))
+        self.timeout_s = timeout_s if timeout_s is not None else float(os.environ.get("CSA_XGMI_TIMEOUT_S", "20"))
+        sizes = [self.R * world * shard * 4, self.R * world * self.nb * 4, 2 * shard * 4, 2 * self.nb * 4,
+                 2 * self.nb * 4]
+        hb = self.lib.csa_xgmi_handle_bytes()
+        self._local: List[int] = []
+        self._opened: List[int] = []
+        handles: Optional[List[bytes]] = []
+        with torch.cuda.device(device):
+            try:
+                for n in sizes:
+                    p = C.c_void_p()
+                    h = C.create_string_buffer(hb)
+                    if self.lib.csa_xgmi_alloc(n, C.byref(p), h):
+                        raise RuntimeError("async_ps alloc failed")
+                    self._local.append(p.value)
+                    handles.append(h.raw)
+            except Exception:
+                handles = None
+            allh: List[Optional[List[bytes]]] = [None] * world
+            dist.all_gather_object(allh, handles, group=group)
+            if any(h is None for h in allh):
+                self.close(barrier=False)
+                raise RuntimeError("async_ps: a rank could not allocate its peer buffers")
+            ptrs: List[int] = []
+            ok = True
+            for q in range(world):
+                for k in range(5):
+                    if q == rank:
+                        ptrs.append(self._local[k])
+                        continue
+                    p = C.c_void_p()
+                    if self.lib.csa_xgmi_open(C.create_string_buffer(allh[q][k], hb), C.byref(p)):
+                        ok = False
+                        ptrs.append(0)
+                        continue
+                    self._opened.append(p.value)
+                    ptrs.append(p.value)
+            oks: List[Optional[bool]] = [None] * world
+            dist.all_gather_object(oks, ok, group=group)
+            if not all(oks):
+                self.close(barrier=False)
+                raise RuntimeError("async_ps: mapping a peer buffer failed")
+        self._bufs = (C.c_void_p * (5 * world))(*ptrs)
+        self.prog = torch.zeros(3 * self.nb, dtype=torch.int32, device=device)
+        self.stale = torch.zeros(1, dtype=torch.int32, device=device)
+        self.state = torch.zeros(4, dtype=torch.int32, device=device)     # t, done, err
+        self.group = group
+
+    def reset(self) -> None:
+        """Collective: back to clock 0 with empty mailboxes (after the engine's throw-away
+        warm-up steps restored the model state)."""
+        torch.cuda.synchronize(self.device)
+        if dist.is_initialized():
+            dist.barrier(group=self.group)
+        nbytes = [self.R * self.W * self.nb * 4, 2 * self.nb * 4, 2 * self.nb * 4]
+        ptrs = [self._local[1], self._local[3], self._local[4]]
+        self.lib.csa_zero((C.c_void_p * 3)(*ptrs), (C.c_long * 3)(*[n // 4 for n in nbytes]), 3,
+                          torch.cuda.current_stream(self.device).cuda_stream)
+        self.prog.zero_(); self.stale.zero_(); self.state.zero_()
+        torch.cuda.synchronize(self.device)
+        if dist.is_initialized():
+            dist.barrier(group=self.group)
+
+    def _launch(self, flat_grad, flat, slots, drain: int) -> None:
+        lo = self.r * self.sh
+        s0 = slots[0, :] if slots.shape[0] > 0 else None
+        s1 = slots[1, :] if slots.shape[0] > 1 else None
+        rc = self.lib.csa_aps_step(
+            self.r, self.W, self.R, self.s, self.sh, self.nb, self._bufs, flat_grad.data_ptr(), flat.data_ptr(),
+            None if s0 is None else s0.data_ptr(), None if s1 is None else s1.data_ptr(), self.opt_id,
+            float(self.lr), self.prog.data_ptr(), self.stale.data_ptr(), self.state.data_ptr(), drain,
+            self.timeout_s, torch.cuda.current_stream(self.device).cuda_stream)
+        del lo
+        if rc:
+            raise RuntimeError(f"async_ps step launch failed ({rc})")
+
+    def step(self, flat_grad: torch.Tensor, flat: torch.Tensor, slots: torch.Tensor) -> None:
+        self._launch(flat_grad, flat, slots, 0)
+
+    def finish(self, flat: torch.Tensor, slots: torch.Tensor) -> None:
+        self._launch(flat, flat, slots, 1)             # (the gradient is not read when draining)
+        torch.cuda.synchronize(self.device)
+        self.check()
+
+    def error(self) -> int:
+        return int(self.state[2].item())
+
+    def check(self) -> None:
+        if self.error():
+            raise RuntimeError("async_ps: a peer wait timed out (state poisoned)")
+
+    @property
+    def max_staleness(self) -> int:
+        return int(self.stale.item())
+
+    @property
+    def applied(self) -> int:
+        return int(self.prog[2].item())
+
+    @property
+    def t(self) -> int:
+        return int(self.state[0].item())
+
+    def close(self, barrier: bool = True) -> None:
+        """Collective: every rank's kernels drain before any buffer is freed."""
+        if not self._local and not self._opened:
+            return
+        torch.cuda.synchronize(self.device)
+        if barrier and dist.is_initialized():
+            dist.barrier(group=self.group)
+        for p in self._opened:
+            self.lib.csa_xgmi_close(p)
+        for p in self._local:
+            self.lib.csa_xgmi_free(p)
+        self._local, self._opened = [], []
+
+
 def make_async_ps(eng, lo: int, hi: int):
     """The transport for this engine: IPC peer buffers on a GPU, gloo point-to-point on CPU."""
     from .dist import DistContext  # noqa: F401  (documented dependency)

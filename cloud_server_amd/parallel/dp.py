@@ -87,6 +87,9 @@ class GradSync:
 
     def _setup_xgmi(self) -> None:
         mode = self.xgmi_mode
+        if self.strategy == "async_ps":
+            self.xgmi_reason = "async_ps: its own peer-buffer transport"
+            return
         if mode in ("0", "off", "false") or self.ctx.backend != "nccl" or not self.ctx.enabled:
             self.xgmi_reason = "disabled" if self.ctx.enabled else "single rank"
             return

@@ -269,6 +269,8 @@ class TrainEngine:
         self.dstep.copy_(dstep); self.stream.cursor.copy_(cursor)
         for b, v in bufs:
             b.copy_(v)
+        if self.aps is not None and hasattr(self.aps, "reset"):
+            self.aps.reset()             # async_ps mailboxes / clocks back to step 0 (collective)
         if hasattr(self.program, "reset_after_warmup"):
             self.program.reset_after_warmup()
 

@@ -332,7 +332,7 @@ class HipProgram:
         e, B = self.e, self.B
         on = os.environ.get("CSA_FUSED_UPDATE", "1") == "1" and not self.forward_only
         self.fused = on and not e.ctx.enabled
-        self.fused_grad = on and e.ctx.enabled and e.sync.strategy in ("allreduce", "ps")
+        self.fused_grad = on and e.ctx.enabled and e.sync.strategy in ("allreduce", "ps", "async_ps")
         # measured on MI355X (profiles/r2_dense_fused.md): the row-group kernel (one
         # 1024-thread workgroup per 16 input features) replaces fc1's split-K pair + its
         # share of the flat optimizer (bench 0.1166 -> 0.1107 ms/step); CSA_FUSED_DENSE=0
@@ -478,6 +478,7 @@ class HipProgram:
         # exclusive rows folded in order before the exchange, the dense layers run the fused
         # backward in gradient mode (exclusive BN-backward rows)
         if e.ctx.enabled and e.sync.strategy not in ("allreduce", "ps"):
+            # (async_ps applies pushes in arrival order: nondeterministic by definition)
             raise Unsupported(f"deterministic mode: {e.sync.strategy} data parallelism")
         if self.pair is None or not self.lib.csa_conv_pair_valu_ok(K.ints(self.pair)):
             raise Unsupported("deterministic mode: network does not start with a VALU conv pair")
@@ -813,7 +814,9 @@ class HipProgram:
                 lo = offs[n]
                 if self.gviews[n].numel() >= 4:
                     self.keep_ranges.append((lo, lo + (self.gviews[n].numel() // 4) * 4))
-        self.ps_mode = self.e.sync.strategy == "ps" and self.e.ctx.enabled
+        # sharded parameters (ps, async_ps): the update reads a shard, the flat gradient is
+        # zeroed through the zero list after the exchange consumed it
+        self.ps_mode = self.e.sync.sharded
         regions = regs + (flat if self.ps_mode else [])
         # the optimizer's zero list holds 16; any further accumulators are cleared at the
         # start of the step instead (one fill launch each, inside the same graph)
@@ -1095,6 +1098,12 @@ class HipProgram:
 
         # ---------------- gradient sync + optimizer ----------------
         main = torch.cuda.current_stream(e.device)
+        if e.aps is not None:
+            # async_ps: push / apply-on-arrival / publish / pull in one launch; the optimizer
+            # launch below keeps only its side jobs (zeroing, metrics, batch staging)
+            e.aps.step(e.flat_grad, e.flat, e.slots)
+            self._optimizer(st)
+            return
         if self.overlap:
             main.wait_stream(self.side)
         elif e.ctx.enabled and e.sync.strategy == "lowrank":
@@ -1505,12 +1514,18 @@ class HipProgram:
     def _optimizer(self, st) -> None:
         e, lib = self.e, self.lib
         lo, hi = e.sync.shard_range()
-        if e.sync.strategy == "ps" and e.ctx.enabled:
+        s0 = e.slots[0] if e.slots.shape[0] > 0 else None
+        s1 = e.slots[1] if e.slots.shape[0] > 1 else None
+        if e.aps is not None:
+            # parameters / slots were updated by the async_ps launch: the update part of this
+            # launch runs on four scratch floats (w, g, two slots) and changes nothing real
+            if getattr(self, "_aps_dummy", None) is None:
+                self._aps_dummy = torch.zeros(4, 4, device=e.device)
+            w, g, s0, s1 = self._aps_dummy[0], self._aps_dummy[1], self._aps_dummy[2], self._aps_dummy[3]
+        elif e.sync.strategy == "ps" and e.ctx.enabled:
             w, g = e.flat[lo:hi], e.grad_shard
         else:
             w, g = e.flat, e.flat_grad
-        s0 = e.slots[0] if e.slots.shape[0] > 0 else None
-        s1 = e.slots[1] if e.slots.shape[0] > 1 else None
         zp = (C.c_void_p * 16)(*[r.data_ptr() for r in self.zero_regions])
         zn = (C.c_long * 16)(*[r.numel() for r in self.zero_regions])
         folds = []          # striped conv weight gradients / head partials -> summed inside the update
