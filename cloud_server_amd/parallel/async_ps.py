@@ -43,6 +43,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import optim_ref
+from .xgmi import _line_up
 
 GRAD, PARAM = 0, 1
 
@@ -249,7 +250,7 @@ class AsyncPSDevice:
         warm-up steps restored the model state)."""
         torch.cuda.synchronize(self.device)
         if dist.is_initialized():
-            dist.barrier(group=self.group)
+            _line_up(self.group, self.device)
         nbytes = [self.R * self.W * self.nb * 4, 2 * self.nb * 4, 2 * self.nb * 4]
         ptrs = [self._local[1], self._local[3], self._local[4]]
         self.lib.csa_zero((C.c_void_p * 3)(*ptrs), (C.c_long * 3)(*[n // 4 for n in nbytes]), 3,
@@ -257,7 +258,7 @@ class AsyncPSDevice:
         self.prog.zero_(); self.stale.zero_(); self.state.zero_()
         torch.cuda.synchronize(self.device)
         if dist.is_initialized():
-            dist.barrier(group=self.group)
+            _line_up(self.group, self.device)
 
     def _launch(self, flat_grad, flat, slots, drain: int) -> None:
         lo = self.r * self.sh
@@ -305,7 +306,7 @@ class AsyncPSDevice:
             return
         torch.cuda.synchronize(self.device)
         if barrier and dist.is_initialized():
-            dist.barrier(group=self.group)
+            _line_up(self.group, self.device)
         for p in self._opened:
             self.lib.csa_xgmi_close(p)
         for p in self._local:

@@ -36,6 +36,15 @@ OP_GATHER, OP_ALLREDUCE, OP_ALLREDUCE_2SHOT = 0, 1, 2
 TWO_SHOT_MIN_BYTES = 256 * 1024
 
 
+def _line_up(group, device) -> None:
+    """Every rank reaches this point before any goes on: a 1-element all-reduce waited on
+    by the host (the collective the tuner already uses to line ranks up; a ``dist.barrier``
+    here was followed by a process abort in the next test's graph capture under RCCL)."""
+    t = torch.zeros(1, device=device)
+    dist.all_reduce(t, group=group)
+    t.item()
+
+
 def _aligned(t: torch.Tensor) -> bool:
     return t.is_contiguous() and t.data_ptr() % 16 == 0 and (t.numel() * t.element_size()) % 16 == 0
 
@@ -199,7 +208,7 @@ class XgmiComm:
             return
         torch.cuda.synchronize(self.device)
         if dist.is_initialized():
-            dist.barrier(group=self.group)
+            _line_up(self.group, self.device)
         for ch in self.channels.values():
             ch.close()
         self.channels.clear()
@@ -217,7 +226,7 @@ def self_test(comm: XgmiComm) -> bool:
     z = torch.zeros(4, device=dev)
     lib.csa_zero((C.c_void_p * 1)(z.data_ptr()), (C.c_long * 1)(4), 1, torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
-    dist.barrier(group=comm.group)
+    _line_up(comm.group, dev)
     ch = None
     try:
         W, r = comm.world, comm.rank
