@@ -156,10 +156,13 @@ class _Entry:
         self.retired = False
 
     def retire(self) -> None:
-        """Dropped from the cache (caller holds the service lock): close its batchers."""
+        """Dropped from the cache (caller holds the service lock): close its batchers and
+        drop them — each batcher's callback holds this entry, so the dict closed a
+        reference cycle that only a gen-2 collection would have freed."""
         self.retired = True
         for bt in self.batchers.values():
             bt.close()
+        self.batchers = {}
 
 
 class InferenceService:
@@ -203,6 +206,8 @@ class InferenceService:
                 return ent
             ent = self._load_entry(path)
             with self._lock:
+                if self._loading.get(key[0]) is load_lock:
+                    del self._loading[key[0]]        # (waiters hold their own reference)
                 self.misses += 1
                 # drop older checkpoints of the same model
                 for k in [k for k in self._cache if k[0] == key[0]]:
@@ -216,9 +221,6 @@ class InferenceService:
     def _load_entry(self, path: str) -> _Entry:
         obj = ckpt.load(path)
         cfg = parse_train_config(json.loads(obj["config"]))
-        net = DigitNet(cfg.plan(), device=self.device, bn_mode=cfg.bn_mode)
-        net.import_state(obj["model"])
-        net.eval()
         hip = None
         if self.use_hip and self.device.type == "cuda":
             from .hip_infer import try_build
@@ -227,6 +229,12 @@ class InferenceService:
             except Exception as exc:        # outside the HIP family: eager torch forward
                 self.hip_error = repr(exc)
                 hip = None
+        if hip is not None:
+            net = hip.state.model           # ONE resident copy of the weights per entry
+        else:
+            net = DigitNet(cfg.plan(), device=self.device, bn_mode=cfg.bn_mode)
+            net.import_state(obj["model"])
+            net.eval()
         return _Entry(net, cfg, hip)
 
     def _load(self, model_dir: str) -> Optional[DigitNet]:

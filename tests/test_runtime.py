@@ -281,6 +281,14 @@ def test_inference_service_cache(tmp_path):
     assert svc.misses == 1 and svc.hits >= 1
     many = svc.predict_many(mdir, [img.getvalue()] * 5)
     assert len(many) == 5 and all(m["result"] == "success" for m in many)
+    # no per-model lock left behind after the load; a retired entry drops its
+    # batchers (they referenced the entry: a cycle only the cyclic GC would free)
+    assert svc._loading == {}
+    ent = next(iter(svc._cache.values()))
+    assert ent.batchers
+    with svc._lock:
+        ent.retire()
+    assert ent.batchers == {} and ent.retired
 
 
 def test_watchdog_kills_hung_worker(tmp_path, monkeypatch):
