@@ -170,6 +170,31 @@ __device__ __forceinline__ void slab_sum_to_lds(const float* slab, int nslab, in
   __syncthreads();
 }
 
+// Deterministic-mode replacement of the per-thread LDS atomics that fold channel partials:
+// thread t holds partials v1[c], v2[c] of channel (t % G) * CB + c; out[ch] / out[C + ch]
+// receive the sums over t = g, g + G, g + 2G, ... in ascending order (plain stores, every
+// channel < C written once).  s_scr holds 2 * blockDim.x floats.  Every thread must call;
+// ends with a barrier.
+template <int CB>
+__device__ __forceinline__ void det_fold_groups(const float (&v1)[CB], const float (&v2)[CB], int G, int C,
+                                                float* s_scr, float* out) {
+  const int t = threadIdx.x, nt = blockDim.x;
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    s_scr[t] = v1[c];
+    s_scr[nt + t] = v2[c];
+    __syncthreads();
+    const int ch = t * CB + c;
+    if (t < G && ch < C) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int u = t; u < nt; u += G) { s1 += s_scr[u]; s2 += s_scr[nt + u]; }
+      out[ch] = s1;
+      out[C + ch] = s2;
+    }
+    __syncthreads();
+  }
+}
+
 // Reduce the forward slab into LDS tables with y = x * s_a[c] + s_b[c]
 // (a = scale*rstd, b = offset - mean*a).  s_tmp needs 2C floats.  Every thread must call.
 __device__ __forceinline__ void bn_reduce_to_lds(const BNRef& bn, float* s_mean, float* s_rstd,

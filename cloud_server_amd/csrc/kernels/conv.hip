@@ -45,6 +45,7 @@ struct ConvFwdArgs {
   int nbands, band_rows;       // output rows (pooled rows if pool) per band
   int band_rows_in;            // max staged input rows per band (LDS carve)
   int nslab;                   // BN slab rows (workgroups fold into blockIdx % nslab)
+  int det;                     // deterministic mode: row blockIdx (nslab = #workgroups)
   const float* x;              // fp32 NHWC input (or null)
   const uint8_t* img;          // uint8 dataset [N][H*W*Cin] (first layer) ...
   const int64_t* idx;          // ... gathered through idx[b] (rows of the index stream)
@@ -177,7 +178,13 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_fwd_kernel(ConvFwdArgs a) {
         if (c < nco) arow[c] = (uint8_t)amax[c];
     }
   }
-  if (a.stat_slab) {
+  if (a.stat_slab && a.det) {
+    // deterministic mode: fixed-order fold (s_bn is dead after staging), then this
+    // workgroup's EXCLUSIVE slab row (nslab = #workgroups) with plain stores
+    det_fold_groups<CB>(bsum, bsq, G, g.Cout, s_bn, s_stat);
+    float* row = a.stat_slab + (size_t)blockIdx.x * 2 * g.Cout;
+    for (int i = threadIdx.x; i < 2 * g.Cout; i += blockDim.x) row[i] = s_stat[i];
+  } else if (a.stat_slab) {
 #pragma unroll
     for (int c = 0; c < CB; ++c)
       if (c < nco) { atomicAdd(&s_stat[co0 + c], bsum[c]); atomicAdd(&s_stat[g.Cout + co0 + c], bsq[c]); }
@@ -346,6 +353,7 @@ struct ConvDgradArgs {
   int nbands, band_rows;       // input rows per band
   int band_rows_in;            // max staged dc rows per band
   int nslab;
+  int det;                     // deterministic mode: exclusive bwd_slab row per workgroup
   const float* dc; const float* w; float* dx;
   const float* x_fwd; int in_act; float in_alpha; BNRef in_bn; int in_bn_on;
   float* bwd_slab;   // [B*nbands][2][Cin]
@@ -449,7 +457,12 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvDgradArgs& a, int bid,
       dxrow[c] = gv;
     }
   }
-  if (a.in_bn_on && a.bwd_slab) {
+  if (a.in_bn_on && a.bwd_slab && a.det) {
+    // deterministic mode: fixed-order fold (s_bn is dead after the loop), exclusive row bid
+    det_fold_groups<CB>(dsum, dxs, G, g.Cin, s_bn, s_stat);
+    float* row = a.bwd_slab + (size_t)bid * 2 * g.Cin;
+    for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) row[i] = s_stat[i];
+  } else if (a.in_bn_on && a.bwd_slab) {
 #pragma unroll
     for (int c = 0; c < CB; ++c)
       if (c < nci) { atomicAdd(&s_stat[ci0 + c], dsum[c]); atomicAdd(&s_stat[g.Cin + ci0 + c], dxs[c]); }
@@ -493,6 +506,7 @@ struct ConvMfmaArgs {
   BNRef in_bn; int in_bn_on; int in_act; float in_alpha;
   const float* w; const float* bias; int out_act; float out_alpha;
   float* y; uint8_t* argmax; float* stat_slab; int nslab;
+  int det;                      // deterministic mode: exclusive slab row per workgroup
 };
 
 template <bool U8, bool POOL>
@@ -671,7 +685,27 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_fwd_mfma_kernel(ConvMfmaArg
       }
     }
   }
-  if (a.stat_slab) {
+  if (a.stat_slab && a.det) {
+    // deterministic mode: the 4 waves' column sums folded in wave order through s_bn
+    // (dead after staging), one statistic per pass, then the EXCLUSIVE row blockIdx
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) {
+        if (nt >= ntn) break;
+        float s = pass ? bsq[nt] : bsum[nt];
+        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+        const int co = nt * 16 + lr;
+        if (lk == 0 && co < g.Cout) s_bn[wave * 128 + co] = s;
+      }
+      __syncthreads();
+      for (int co = tid; co < g.Cout; co += CONV_THREADS)
+        s_stat[pass * g.Cout + co] = ((s_bn[co] + s_bn[128 + co]) + s_bn[256 + co]) + s_bn[384 + co];
+      __syncthreads();
+    }
+    float* row = a.stat_slab + (size_t)blockIdx.x * 2 * g.Cout;
+    for (int i = tid; i < 2 * g.Cout; i += CONV_THREADS) row[i] = s_stat[i];
+  } else if (a.stat_slab) {
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
       if (nt >= ntn) break;
@@ -999,14 +1033,13 @@ static bool set_lds_attr(const void* fn) {
 
 // Launch the MFMA conv forward when the shape is inside its family; false = use the VALU
 // kernel.  Bands: ~700 workgroups over the batch.
-static bool conv_fwd_mfma(const ConvFwdArgs& f, hipStream_t st) {
+// Geometry of the MFMA forward (false: shape outside its family).
+static bool conv_fwd_mfma_plan(const ConvGeom& g, const PoolGeom& p, ConvMfmaArgs& a, size_t& shm) {
   constexpr int target = 700;
-  const ConvGeom& g = f.g;
-  const PoolGeom& p = f.pool;
   const bool pool = p.on != 0;
   if (pool && !(p.KH == 2 && p.KW == 2 && p.SH == 2 && p.SW == 2 && p.PT == 0 && p.PL == 0)) return false;
   if (g.Cout > 128) return false;
-  ConvMfmaArgs a{};
+  a = ConvMfmaArgs{};
   a.g = g; a.pool_on = pool;
   a.OHo = pool ? p.OH : g.OH; a.OWo = pool ? p.OW : g.OW;
   const int K = g.KH * g.KW * g.Cin;
@@ -1024,17 +1057,26 @@ static bool conv_fwd_mfma(const ConvFwdArgs& f, hipStream_t st) {
   a.band_rows = rows;
   a.tile_rows = tile_rows(rows);
   a.nbands = (a.OHo + rows - 1) / rows;
+  shm = lds(rows);
+  return true;
+}
+
+static bool conv_fwd_mfma(const ConvFwdArgs& f, hipStream_t st) {
+  ConvMfmaArgs a;
+  size_t shm;
+  if (!conv_fwd_mfma_plan(f.g, f.pool, a, shm)) return false;
+  const ConvGeom& g = f.g;
+  const bool pool = a.pool_on != 0;
   a.x = f.x; a.img = f.img; a.idx = f.idx; a.cursor = f.cursor;
   a.in_bn = f.in_bn; a.in_bn_on = f.in_bn_on; a.in_act = f.in_act; a.in_alpha = f.in_alpha;
   a.w = f.w; a.bias = f.bias; a.out_act = f.out_act; a.out_alpha = f.out_alpha;
-  a.y = f.y; a.argmax = f.argmax; a.stat_slab = f.stat_slab; a.nslab = f.nslab;
+  a.y = f.y; a.argmax = f.argmax; a.stat_slab = f.stat_slab; a.nslab = f.nslab; a.det = f.det;
   static bool attr = set_lds_attr((const void*)conv_fwd_mfma_kernel<true, true>) &&
                      set_lds_attr((const void*)conv_fwd_mfma_kernel<true, false>) &&
                      set_lds_attr((const void*)conv_fwd_mfma_kernel<false, true>) &&
                      set_lds_attr((const void*)conv_fwd_mfma_kernel<false, false>);
   (void)attr;
   dim3 grid((unsigned)(g.B * a.nbands));
-  const size_t shm = lds(rows);
   if (f.img) {
     if (pool) hipLaunchKernelGGL((conv_fwd_mfma_kernel<true, true>), grid, dim3(CONV_THREADS), shm, st, a);
     else hipLaunchKernelGGL((conv_fwd_mfma_kernel<true, false>), grid, dim3(CONV_THREADS), shm, st, a);
@@ -1055,8 +1097,24 @@ CSA_API int csa_conv_debug(long long* p) {
 
 // Number of BN partial-slab rows a csa_conv_fwd launch writes (the slab must be zeroed
 // before every launch: rows are accumulated with atomics).
+static PoolGeom pool_from(const int* v) {
+  return PoolGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]};
+}
+
+// Workgroups of a csa_conv_fwd launch (the MFMA kernel when the shape is in its family).
+static int conv_fwd_blocks(const ConvGeom& g, const PoolGeom& p) {
+  ConvMfmaArgs m;
+  size_t shm;
+  if (conv_fwd_mfma_plan(g, p, m, shm)) return g.B * m.nbands;
+  int nb, rows, rows_in;
+  fwd_bands(g, p, nb, rows, rows_in);
+  return g.B * nb;
+}
+
+// Deterministic mode: every workgroup writes its own row (rows = workgroups), folded in
+// row order by the consumer (csa_rows_fold) instead of atomics into SLAB_ROWS rows.
 CSA_API int csa_conv_fwd_nslab(const int* geom, const int* pool) {
-  (void)geom; (void)pool;
+  if (g_csa_det && geom && pool) return conv_fwd_blocks(geom_from(geom), pool_from(pool));
   return SLAB_ROWS;
 }
 
@@ -1071,14 +1129,16 @@ CSA_API int csa_conv_fwd(const float* x, const uint8_t* img, const int64_t* idx,
   ConvFwdArgs a{};
   a.cursor = cursor;
   a.g = geom_from(geom);
-  a.pool = PoolGeom{pool[0], pool[1], pool[2], pool[3], pool[4], pool[5], pool[6], pool[7], pool[8]};
+  a.pool = pool_from(pool);
   if (a.g.Cin > 128 || a.g.Cout > 128) return -1;
   a.x = x; a.img = img; a.idx = idx;
   a.in_bn = BNRef{in_bn_slab, in_bn_nslab, a.g.Cin, in_bn_count, in_bn_eps, in_bn_scale, in_bn_offset};
   a.in_bn_on = in_bn_slab != nullptr;
   a.in_act = in_act; a.in_alpha = in_alpha;
   a.w = w; a.bias = bias; a.out_act = out_act; a.out_alpha = out_alpha;
-  a.y = y; a.argmax = argmax; a.stat_slab = stat_slab; a.nslab = SLAB_ROWS;
+  a.y = y; a.argmax = argmax; a.stat_slab = stat_slab;
+  a.det = g_csa_det;
+  a.nslab = a.det ? conv_fwd_blocks(a.g, a.pool) : SLAB_ROWS;
   if (conv_fwd_mfma(a, st)) return (int)hipGetLastError();
   fwd_bands(a.g, a.pool, a.nbands, a.band_rows, a.band_rows_in);
   const size_t nin = ((size_t)a.band_rows_in * a.g.W * a.g.Cin + 3) & ~(size_t)3;
@@ -1118,8 +1178,11 @@ CSA_API int csa_route_bwd(const float* dz, const float* y, const uint8_t* argmax
 }
 
 CSA_API int csa_conv_dgrad_nslab(const int* geom) {
-  (void)geom;
-  return SLAB_ROWS;
+  if (!g_csa_det || !geom) return SLAB_ROWS;
+  int nb, rows, rows_in;             // deterministic mode: one row per dgrad workgroup
+  const ConvGeom g = geom_from(geom);
+  dgrad_bands(g, nb, rows, rows_in);
+  return g.B * nb;
 }
 
 static int dgrad_args(const float* dc, const float* w, float* dx, const int* geom, const float* x_fwd,
@@ -1132,7 +1195,7 @@ static int dgrad_args(const float* dc, const float* w, float* dx, const int* geo
   a.dc = dc; a.w = w; a.dx = dx; a.x_fwd = x_fwd; a.in_act = in_act; a.in_alpha = in_alpha;
   a.in_bn = BNRef{bn_slab, bn_nslab, a.g.Cin, bn_count, bn_eps, bn_scale, bn_offset};
   a.in_bn_on = bn_slab != nullptr;
-  a.bwd_slab = bwd_slab; a.nslab = SLAB_ROWS;
+  a.bwd_slab = bwd_slab; a.nslab = SLAB_ROWS; a.det = g_csa_det;
   dgrad_bands(a.g, a.nbands, a.band_rows, a.band_rows_in);
   const size_t nd = ((size_t)a.band_rows_in * a.g.OW * a.g.Cout + 3) & ~(size_t)3;
   shm = (nd + (size_t)a.g.KH * a.g.KW * a.g.Cin * a.g.Cout) * sizeof(float);
@@ -1193,6 +1256,23 @@ static int wgrad_args(const float* x, const uint8_t* img, const int64_t* idx, co
   a.nbands = (OH + rows - 1) / rows;
   shm = lds(rows);
   return 0;
+}
+
+// Workgroups of a conv weight-gradient launch (csa_conv_wgrad, or the wgrad half of
+// csa_conv_bwd): with that many stripes every workgroup owns one stripe and adds each of
+// its outputs ONCE into a zeroed row — the deterministic-mode layout, folded in stripe
+// order by csa_rows_fold.  geom = {B, H, W, Cin, KH, KW, SH, SW, PT, PL, OH, OW, Cout}.
+CSA_API int csa_conv_wgrad_blocks(const int* geom, int bias) {
+  static const float probe = 0.f;    // wgrad_args needs an input; the plan never reads it
+  float dummy_db = 0.f;
+  const ConvGeom g = geom_from(geom);
+  ConvWgradArgs a;
+  size_t shm;
+  if (wgrad_args(&probe, nullptr, nullptr, nullptr, nullptr, bias ? &dummy_db : nullptr, 1, g.B, g.H, g.W,
+                 g.Cin, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, g.OH, g.OW, g.Cout, nullptr, 0, 0.f, 0.f, nullptr,
+                 nullptr, 0, 0.f, nullptr, a, shm))
+    return -1;
+  return g.B * a.nbands;
 }
 
 // dW/db (+)= conv weight gradient, accumulated with atomics into `stripes` copies

@@ -27,13 +27,15 @@ constexpr int NP_THREADS = 256;
 constexpr int NP_ROWS = 64;            // rows per stats / reduce block
 
 // Per-channel sums of f(row, c) over this block's rows, folded atomically into
-// slab row (blockIdx.x % nslab): out[0][c] += sum f0, out[1][c] += sum f1.
+// slab row (blockIdx.x % nslab): out[0][c] += sum f0, out[1][c] += sum f1.  The in-block
+// fold is fixed-order; with det (deterministic mode, nslab = gridDim.x) the block STORES
+// its exclusive row blockIdx.x (the finalize kernels sum the rows in row order).
 template <class F>
-__device__ __forceinline__ void np_col_sums(long N, int C, float* slab, int nslab, F f) {
+__device__ __forceinline__ void np_col_sums(long N, int C, float* slab, int nslab, int det, F f) {
   __shared__ float s_acc[2 * NP_THREADS];
   const int t = threadIdx.x;
   const long r0 = (long)blockIdx.x * NP_ROWS, r1 = r0 + NP_ROWS < N ? r0 + NP_ROWS : N;
-  float* row = slab + (size_t)(blockIdx.x % nslab) * 2 * C;
+  float* row = slab + (size_t)(det ? blockIdx.x : blockIdx.x % nslab) * 2 * C;
   if (C <= NP_THREADS) {
     const int per = NP_THREADS / C, sub = t / C, c = t - sub * C;
     float a0 = 0.f, a1 = 0.f;
@@ -44,15 +46,16 @@ __device__ __forceinline__ void np_col_sums(long N, int C, float* slab, int nsla
         a0 += v0;
         a1 += v1;
       }
-    // fold the `per` row groups of each channel through LDS
-    for (int i = t; i < 2 * C; i += NP_THREADS) s_acc[i] = 0.f;
+    // fold the `per` row groups of each channel through LDS, in row-group order
+    s_acc[t] = a0;
+    s_acc[NP_THREADS + t] = a1;
     __syncthreads();
-    if (sub < per) {
-      atomicAdd(&s_acc[c], a0);
-      atomicAdd(&s_acc[C + c], a1);
+    if (t < C) {
+      float s0 = 0.f, s1 = 0.f;
+      for (int u = 0; u < per; ++u) { s0 += s_acc[u * C + t]; s1 += s_acc[NP_THREADS + u * C + t]; }
+      if (det) { row[t] = s0; row[C + t] = s1; }
+      else { atomicAdd(&row[t], s0); atomicAdd(&row[C + t], s1); }
     }
-    __syncthreads();
-    for (int i = t; i < 2 * C; i += NP_THREADS) atomicAdd(&row[i], s_acc[i]);
   } else {
     for (int c = t; c < C; c += NP_THREADS) {
       float a0 = 0.f, a1 = 0.f;
@@ -62,15 +65,15 @@ __device__ __forceinline__ void np_col_sums(long N, int C, float* slab, int nsla
         a0 += v0;
         a1 += v1;
       }
-      atomicAdd(&row[c], a0);
-      atomicAdd(&row[C + c], a1);
+      if (det) { row[c] = a0; row[C + c] = a1; }
+      else { atomicAdd(&row[c], a0); atomicAdd(&row[C + c], a1); }
     }
   }
 }
 
 __global__ __launch_bounds__(NP_THREADS) void bn_stats_kernel(const float* __restrict__ x, long N, int C,
-                                                             float* slab, int nslab) {
-  np_col_sums(N, C, slab, nslab, [&](long r, int c, float& v0, float& v1) {
+                                                             float* slab, int nslab, int det) {
+  np_col_sums(N, C, slab, nslab, det, [&](long r, int c, float& v0, float& v1) {
     const float v = x[r * C + c];
     v0 = v;
     v1 = v * v;
@@ -134,8 +137,8 @@ __device__ __forceinline__ float np_dz(const float* x, const float* y, const flo
 __global__ __launch_bounds__(NP_THREADS) void bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ y,
                                                                   const float* __restrict__ dy, long N, int C,
                                                                   const float* __restrict__ tab, int act, float alpha,
-                                                                  float* slab, int nslab) {
-  np_col_sums(N, C, slab, nslab, [&](long r, int c, float& v0, float& v1) {
+                                                                  float* slab, int nslab, int det) {
+  np_col_sums(N, C, slab, nslab, det, [&](long r, int c, float& v0, float& v1) {
     const long i = r * C + c;
     const float dz = np_dz(x, y, dy, i, c, C, tab, act, alpha);
     const float xhat = (x[i] - tab[c]) * tab[C + c];
@@ -253,10 +256,16 @@ using namespace csa;
 // [rows][2][C] and zeroes it before every step).
 CSA_API int csa_bn_slab_rows() { return 16; }
 
+// Statistic-slab rows for N rows of input: 16 atomically-folded rows, or in deterministic
+// mode one exclusive row per stats / reduce workgroup.
+CSA_API int csa_bn_stat_rows(long N) { return g_csa_det ? (int)((N + NP_ROWS - 1) / NP_ROWS) : 16; }
+
 CSA_API int csa_bn_stats(const float* x, long N, int C, float* slab, int nslab, hipStream_t st) {
   if (N <= 0 || C <= 0 || nslab <= 0) return -1;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3((unsigned)((N + NP_ROWS - 1) / NP_ROWS)), dim3(NP_THREADS), 0, st,
-                     x, N, C, slab, nslab);
+  const long nb = (N + NP_ROWS - 1) / NP_ROWS;
+  if (g_csa_det && nslab < nb) return -3;          // det: one exclusive row per workgroup
+  hipLaunchKernelGGL(bn_stats_kernel, dim3((unsigned)nb), dim3(NP_THREADS), 0, st, x, N, C, slab, nslab,
+                     g_csa_det);
   return (int)hipGetLastError();
 }
 
@@ -279,8 +288,10 @@ CSA_API int csa_bn_apply(const float* x, float* y, long n, int C, const float* t
 CSA_API int csa_bn_bwd_reduce(const float* x, const float* y, const float* dy, long N, int C, const float* tab,
                               int act, float alpha, float* slab, int nslab, hipStream_t st) {
   if (N <= 0 || C <= 0 || !tab) return -1;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)((N + NP_ROWS - 1) / NP_ROWS)), dim3(NP_THREADS), 0, st,
-                     x, y, dy, N, C, tab, act, alpha, slab, nslab);
+  const long nb = (N + NP_ROWS - 1) / NP_ROWS;
+  if (g_csa_det && nslab < nb) return -3;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)nb), dim3(NP_THREADS), 0, st, x, y, dy, N, C, tab, act,
+                     alpha, slab, nslab, g_csa_det);
   return (int)hipGetLastError();
 }
 

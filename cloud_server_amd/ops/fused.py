@@ -42,6 +42,7 @@ _SIGS = {
     "csa_conv_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, F, F, P, P, I, F, I, F, P, P]),
     "csa_route_bwd": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, I, P, P, P, P, F, P]),
     "csa_conv_dgrad_nslab": (I, [P]),
+    "csa_conv_wgrad_blocks": (I, [P, I]),
     "csa_conv_dgrad": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, P]),
     "csa_conv_bwd": (I, [P, P, P, P, P, I, F, P, I, F, F, P, P, P, P, P, I, P]),
     "csa_head": (I, [P, I, I, I, F, P, P, P, P, I, F, P, P, P, P, P, P, P, I, P, P, P]),
@@ -112,6 +113,7 @@ _SIGS = {
     "csa_gconv_dgrad": (I, [P, P, P, P, P]),
     # standalone BatchNorm / activation / max-pool units (norm_pool.hip)
     "csa_bn_slab_rows": (I, []),
+    "csa_bn_stat_rows": (I, [L]),
     "csa_bn_stats": (I, [P, L, I, P, I, P]),
     "csa_bn_finalize": (I, [P, I, I, F, F, P, P, P, P, F, I, P, P]),
     "csa_bn_apply": (I, [P, P, L, I, P, I, F, P]),

@@ -430,6 +430,8 @@ class HipProgram:
             return
         if not (_y_ok(ua.act) and _y_ok(ub.act)):
             return
+        if self.det and not self.lib.csa_conv_pair_valu_ok(K.ints(geom)):
+            return                       # deterministic mode: two conv units instead
         self.pair = geom
 
     # ------------------------------------------------------------------ horizontal fusion
@@ -465,30 +467,29 @@ class HipProgram:
 
     # ------------------------------------------------------------------ deterministic mode
     def _check_det(self) -> None:
-        """Deterministic mode covers the fused one-GPU family: the VALU conv pair (fixed-order
-        in-workgroup reductions; exclusive statistic rows and weight-gradient stripes), fused
-        dense backward + update units (exclusive BN-backward rows, fixed-order column-block
-        hand-off), register-direct dense forwards without split-K, and the row-per-workgroup
-        head (fixed-order batch reductions in the last dense layer's epilogue).  Any other
-        lowering raises Unsupported, and the engine runs the step on eager PyTorch with its
-        deterministic algorithms instead."""
+        """Deterministic mode covers every one-GPU lowering and allreduce / ps data
+        parallelism: the VALU conv pair and the conv units (fixed-order in-workgroup folds;
+        one exclusive statistic row and weight-gradient stripe per workgroup, folded in row
+        order by csa_rows_fold), standalone BatchNorm units (exclusive statistic rows summed
+        in row order by the finalize kernels), gather-form pools (overlapping pools are never
+        fused), gconv units (implicit GEMM without split-K), fused dense backward + update
+        units (exclusive BN-backward rows, fixed-order column-block hand-off), register-direct
+        dense forwards, and the row-per-workgroup or partial-row heads.  What remains —
+        materialised-gradient dense units and the atomic head — raises Unsupported, and the
+        engine runs the step on eager PyTorch with its deterministic algorithms instead."""
         e = self.e
         # data parallel: every collective of the step is fixed-order (GradSync.det: the xGMI
-        # kernels or an exact all-gather + rank-ordered fold), the pair's stripes are
-        # exclusive rows folded in order before the exchange, the dense layers run the fused
-        # backward in gradient mode (exclusive BN-backward rows)
+        # kernels or an exact all-gather + rank-ordered fold), the stripes are exclusive rows
+        # folded in order before the exchange, the dense layers run the fused backward in
+        # gradient mode (exclusive BN-backward rows)
         if e.ctx.enabled and e.sync.strategy not in ("allreduce", "ps"):
             # (async_ps applies pushes in arrival order: nondeterministic by definition)
             raise Unsupported(f"deterministic mode: {e.sync.strategy} data parallelism")
-        if self.pair is None or not self.lib.csa_conv_pair_valu_ok(K.ints(self.pair)):
-            raise Unsupported("deterministic mode: network does not start with a VALU conv pair")
-        for u in self.units[2:]:
-            if u.kind != "dense" or not u.fused or not u.direct:
-                raise Unsupported(f"deterministic mode: {u.kind} unit {u.layer.name} has no fixed-order variant")
-            if u.in_tf.has_bn and u is not self.units[2]:
-                raise Unsupported("deterministic mode: BatchNorm after a dense layer")
-        if not self.head_row:
-            raise Unsupported("deterministic mode: head outside the row-per-workgroup family")
+        for u in self.units:
+            if u.kind == "dense" and not (u.fused and u.direct):
+                raise Unsupported(f"deterministic mode: dense unit {u.layer.name} has no fixed-order variant")
+        if not (self.head_row or self.head_rg):
+            raise Unsupported("deterministic mode: head outside the row-per-workgroup / partial-row family")
 
     def _row_fold(self, t: torch.Tensor, rows: int, width: int, dst: torch.Tensor, zero_src: int, st) -> None:
         """dst[:width] = fixed-order sum of the first ``rows`` rows of ``t`` (row stride width)."""
@@ -561,7 +562,10 @@ class HipProgram:
                     if j < len(layers) and isinstance(layers[j].spec, ActSpec) and _y_ok(layers[j].spec):
                         u.act = layers[j].spec
                         j += 1
-                    if j < len(layers) and isinstance(layers[j].spec, PoolSpec):
+                    if (j < len(layers) and isinstance(layers[j].spec, PoolSpec)
+                            and not (self.det and tuple(layers[j].spec.kernel) != tuple(layers[j].spec.stride))):
+                        # (deterministic mode: an overlapping pool's routing adds windows into
+                        # dc with atomics — it stays a standalone gather-form pool unit)
                         u.pool = layers[j]
                         j += 1
                 units.append(u)
@@ -612,7 +616,7 @@ class HipProgram:
                 u.y = torch.zeros_like(u.x)
                 C_ = self._bn_channels(u)
                 if u.norm is not None:
-                    R = self.lib.csa_bn_slab_rows()
+                    R = self.lib.csa_bn_stat_rows(u.x.numel() // C_)
                     u.bn_tab = torch.zeros(4, C_, **f32)
                     u.bn_slab = torch.zeros(R, 2, C_, **f32)
                     if not fo:
@@ -645,9 +649,12 @@ class HipProgram:
             if tf.has_bn:
                 src = self.units[k - 1]
                 ph, pw = src.y.shape[1], src.y.shape[2]
-                nslab = self.lib.csa_conv_fwd_nslab(self._conv_geom(src.layer, B), self._pool_geom(src))
-                if self.det:            # one row per pair workgroup, folded to row 0
-                    nslab = tf.prod_rows = int(self.lib.csa_conv_pair_grid(_FK.ints(self.pair)))
+                # (deterministic mode: one row per producer workgroup, folded to row 0)
+                if self.det and self.pair is not None and k == 2:
+                    nslab = int(self.lib.csa_conv_pair_grid(_FK.ints(self.pair)))
+                else:
+                    nslab = self.lib.csa_conv_fwd_nslab(self._conv_geom(src.layer, B), self._pool_geom(src))
+                tf.prod_rows = nslab
                 tf.slab = torch.zeros(nslab, 2, src.y.shape[3], **f32)
                 tf.nslab = 1 if self.det else nslab
                 tf.count = float(B * ph * pw * self.W)
@@ -762,10 +769,18 @@ class HipProgram:
                 # workgroup — and under data parallelism, where the gradient must be complete
                 # before its all-reduce (700 workgroups adding into ONE copy contend: the pair
                 # backward took 37 us instead of 25)
-                u.row_fold = self.pair is not None and k < 2 and (self.det or self.e.ctx.enabled)
+                # — and every conv unit's in deterministic mode (one stripe per wgrad workgroup)
+                in_pair = self.pair is not None and k < 2
+                u.row_fold = self.det or (in_pair and self.e.ctx.enabled)
                 if u.row_fold:
-                    S = (int(self.lib.csa_conv_pair_grid(_FK.ints(self.pair))) if self.det
-                         else self.WGRAD_STRIPES)
+                    if not self.det:
+                        S = self.WGRAD_STRIPES
+                    elif in_pair:
+                        S = int(self.lib.csa_conv_pair_grid(_FK.ints(self.pair)))
+                    else:
+                        S = int(self.lib.csa_conv_wgrad_blocks(self._conv_geom(lp, B), int(bool(lp.spec.bias))))
+                        if S <= 0:
+                            raise Unsupported(f"conv unit {lp.name}: no weight-gradient plan")
                 elif S > 1:
                     fold_budget -= nf
                 u.wg_stripes = S
@@ -1081,6 +1096,7 @@ class HipProgram:
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
                         K.ptr(u.x), in_act, in_alpha, *bn, K.ptr(tf.bwd_slab),
                         K.ptr(u.dw_acc), K.ptr(u.db_acc) if sp.bias else None, u.wg_stripes, st), "conv_bwd")
+                    self._conv_det_folds(u, tf, st)
                     self._grad_ready(k)
                     continue
                 ws = st
@@ -1094,6 +1110,7 @@ class HipProgram:
                     self._rc(lib.csa_conv_dgrad(
                         K.ptr(dc), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), geom,
                         K.ptr(u.x), in_act, in_alpha, *bn, K.ptr(tf.bwd_slab), st), "conv_dgrad")
+                self._conv_det_folds(u, tf, st)
             self._grad_ready(k)
 
         # ---------------- gradient sync + optimizer ----------------
@@ -1170,6 +1187,8 @@ class HipProgram:
                     K.ptr(u.y), K.ptr(u.argmax), K.ptr(oslab),
                     self._conv_geom(lp, B), self._pool_geom(u), *bn, in_act, in_alpha,
                     _act_id(u.act), _alpha(u.act), K.ptr(cur) if raw else None, st), "conv_fwd")
+                if oslab is not None and self.det:        # exclusive rows -> row 0, in order
+                    self._row_fold(oslab, next_tf.prod_rows, oslab.shape[1] * oslab.shape[2], oslab, 0, st)
                 if oslab is not None and self.sync_bn:
                     e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
             else:
@@ -1366,6 +1385,21 @@ class HipProgram:
                 self._row_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
                 if u.db_acc is not None:
                     self._row_fold(u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"], 1, st)
+
+    def _conv_det_folds(self, u: Unit, tf, st) -> None:
+        """Deterministic mode, after a conv unit's backward: its BN-backward rows (one per
+        dgrad workgroup) to row 0 and its weight-gradient stripes (one per wgrad workgroup)
+        into the flat gradient, both in row order (the stripes are re-zeroed by the fold)."""
+        if not self.det:
+            return
+        if tf.has_bn and u.x is not None:
+            self._row_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],
+                           tf.bwd_slab, 0, st)
+        if u.row_fold and u.wg_stripes > 1:
+            G, lp = self.gviews, u.layer
+            self._row_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
+            if u.db_acc is not None:
+                self._row_fold(u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"], 1, st)
 
     def _route_geom(self, u: Unit):
         lp, B = u.layer, self.B

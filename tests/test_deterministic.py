@@ -152,3 +152,53 @@ def test_launch_profile_flags_are_per_thread():
     t.join()
     assert seen["other"] == (1, 1)
     assert (lib.csa_deterministic(), lib.csa_packed()) == (0, 0)
+
+
+DET_CASES = ("five_biased_convs", "wide_conv_192", "dense_norm_head", "pool_after_norm_act")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", DET_CASES)
+def test_deterministic_hip_every_lowering_bitwise(monkeypatch, name):
+    """deterministic mode on the conv units (exclusive statistic rows and
+    weight-gradient stripes per workgroup, folded in row order), standalone BatchNorm
+    units, gconv units, gather-form pools and the partial-row head — the HIP program stays
+    on (no eager fallback), two graph runs and an eager run are bitwise equal, and one
+    step's gradients match the fp32 eager reference."""
+    from test_hip_step import CASES, _cfg
+
+    monkeypatch.setenv("CSA_DETERMINISTIC", "1")
+    try:
+        runs = []
+        for mode in ("graph", "graph", "eager"):
+            cfg = _cfg(CASES[name], optimizer="AdamOptimizer", lr=1e-3)
+            eng = TrainEngine(cfg, synthetic_mnist(400, seed=5), device="cuda:0", backend="hip",
+                              use_graph=mode == "graph")
+            assert eng.backend == "hip" and eng.program.det, eng.fallback_reason
+            for _ in range(8):
+                eng.step()
+            eng.sync_device()
+            runs.append((eng.flat.clone(), eng.slots.clone(), eng.metrics_since(0)["loss"]))
+        for i in (1, 2):
+            assert torch.equal(runs[0][0], runs[i][0]), f"run {i}: params differ"
+            assert torch.equal(runs[0][1], runs[i][1]), f"run {i}: optimizer slots differ"
+            assert runs[0][2] == runs[i][2]
+
+        def grads(backend):
+            cfg = _cfg(CASES[name])
+            eng = TrainEngine(cfg, synthetic_mnist(300, seed=13), device="cuda:0", backend=backend,
+                              use_graph=False)
+            w0 = eng.flat.clone()
+            eng.step()
+            eng.sync_device()
+            return eng, (w0 - eng.flat) / cfg.effective_lr
+
+        e_det, g_det = grads("hip")
+        assert e_det.program.det
+        _, g_ref = grads("torch")
+    finally:
+        torch.use_deterministic_algorithms(False)
+    for k in e_det.model.state.shapes:
+        a, b = e_det.model.state.view(k, g_det), e_det.model.state.view(k, g_ref)
+        scale = b.abs().max().item() + 1e-6
+        assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6, k
