@@ -851,14 +851,8 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
 // of their layer, so they run inside this launch instead of as serial links of the chain.
 // The pair's workgroups come first: the dispatcher deals blocks in index order, so the
 // critical pair blocks all start before any update block takes a slot.
-struct CPUpd {
-  DUArgs seg[DU_MAXDEF];
-  int start[DU_MAXDEF + 1];          // segment s = extra blocks [start[s], start[s + 1])
-  int nseg, head;
-};
-
 template <bool ONE, int NSLOT>
-__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, CPUpd u) {
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npair = a.g.B * a.g.nbands;
   const int bid = (int)blockIdx.x;
@@ -866,14 +860,7 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs
     cp_bwd_body<ONE>(a, bid, smem);
     return;
   }
-  const int e = bid - npair;
-  int s = 0;
-#pragma unroll
-  for (int k = 1; k < DU_MAXDEF; ++k) s += (k < u.nseg && e >= u.start[k]) ? 1 : 0;
-  const DUArgs& d = u.seg[s];
-  const int lb = e - u.start[s], nb = u.start[s + 1] - u.start[s];
-  if (s == u.head) du_body<NSLOT, 4, true, false, true>(d, lb, nb, smem);
-  else du_body<NSLOT, 4, false, false, true>(d, lb, nb, smem);
+  du_segs_body<NSLOT, true>(u, bid - npair, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1609,7 +1596,7 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
 }
 
 template <bool ONE, int NSLOT>
-static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const CPUpd& u, size_t lds, hipStream_t st) {
+static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const DUSegs& u, size_t lds, hipStream_t st) {
   static const bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_upd_kernel<ONE, NSLOT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
@@ -1618,18 +1605,8 @@ static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const CPUpd& u, size_t lds, h
   return (int)hipGetLastError();
 }
 
-// The MFMA pair backward carrying the deferred dense update segments (consumes them).
-static int cp_launch_bwd_upd(const CPBwdArgs& a, hipStream_t st) {
-  CPUpd u{};
-  u.nseg = g_du_def.n;
-  u.head = g_du_def.head;
-  u.start[0] = 0;
-  for (int s = 0; s < DU_MAXDEF; ++s) {
-    if (s < u.nseg) u.seg[s] = g_du_def.seg[s];
-    u.start[s + 1] = u.start[s] + (s < u.nseg ? g_du_def.blocks[s] : 0);
-  }
-  g_du_def.n = 0;
-  g_du_def.head = -1;
+// The MFMA pair backward carrying the deferred dense update segments taken for it.
+static int cp_launch_bwd_upd(const CPBwdArgs& a, const DUSegs& u, hipStream_t st) {
   size_t lds = cp_lds(a.g, true);
   const size_t dl = du_lds_floats(u.seg[0].M, 4) * sizeof(float);
   for (int s = 1; s < u.nseg; ++s)
@@ -1674,10 +1651,12 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
     if (!vattr) return -3;
     if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_bwd_kernel<2, 2>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
     else hipLaunchKernelGGL((cpv_bwd_kernel<3, 3>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
-    if (g_du_def.n > 0) return csa_dense_update_flush(st);     // deferred updates on their own
+    DUSegs u;                                                   // deferred updates on their own
+    if (du_take(DU_CARRY_PAIR, u) > 0) return du_flush_segs(u, st);
     return (int)hipGetLastError();
   }
-  if (g_du_def.n > 0) return cp_launch_bwd_upd(a, st);
+  DUSegs u;
+  if (du_take(DU_CARRY_PAIR, u) > 0) return cp_launch_bwd_upd(a, u, st);
   if (cp_bwd_one_batch(a))
     hipLaunchKernelGGL(conv_pair_bwd_kernel<true>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
   else
