@@ -458,7 +458,9 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvDgradArgs& a, int bid,
     }
   }
   if (a.in_bn_on && a.bwd_slab && a.det) {
-    // deterministic mode: fixed-order fold (s_bn is dead after the loop), exclusive row bid
+    // deterministic mode: fixed-order fold through s_bn, exclusive row bid — once every
+    // thread is past the loop, which reads the BN tables in s_bn
+    __syncthreads();
     det_fold_groups<CB>(dsum, dxs, G, g.Cin, s_bn, s_stat);
     float* row = a.bwd_slab + (size_t)bid * 2 * g.Cin;
     for (int i = threadIdx.x; i < 2 * g.Cin; i += blockDim.x) row[i] = s_stat[i];

@@ -479,10 +479,11 @@ class HipProgram:
         order by csa_rows_fold), standalone BatchNorm units (exclusive statistic rows summed
         in row order by the finalize kernels), gather-form pools (overlapping pools are never
         fused), gconv units (implicit GEMM without split-K), fused dense backward + update
-        units (exclusive BN-backward rows, fixed-order column-block hand-off), register-direct
-        dense forwards, and the row-per-workgroup or partial-row heads.  What remains —
-        materialised-gradient dense units and the atomic head — raises Unsupported, and the
-        engine runs the step on eager PyTorch with its deterministic algorithms instead."""
+        units (exclusive BN-backward rows, fixed-order column-block hand-off), materialised-
+        gradient dense units and dense forwards (no split-K), and the row-per-workgroup or
+        partial-row heads.  What remains — a materialised-gradient dense unit reading a
+        BatchNorm'd input, and the atomic head — raises Unsupported, and the engine runs the
+        step on eager PyTorch with its deterministic algorithms instead."""
         e = self.e
         # data parallel: every collective of the step is fixed-order (GradSync.det: the xGMI
         # kernels or an exact all-gather + rank-ordered fold), the stripes are exclusive rows
@@ -492,8 +493,11 @@ class HipProgram:
             # (async_ps applies pushes in arrival order: nondeterministic by definition)
             raise Unsupported(f"deterministic mode: {e.sync.strategy} data parallelism")
         for u in self.units:
-            if u.kind == "dense" and not (u.fused and u.direct):
-                raise Unsupported(f"deterministic mode: dense unit {u.layer.name} has no fixed-order variant")
+            # materialised-gradient dense units are fixed-order without split-K, except for
+            # the BatchNorm-backward statistics their input-gradient epilogue adds atomically
+            if u.kind == "dense" and not u.fused and u.in_tf.has_bn:
+                raise Unsupported(f"deterministic mode: dense unit {u.layer.name} (BatchNorm input, "
+                                  "materialised gradient) has no fixed-order variant")
         if not (self.head_row or self.head_rg):
             raise Unsupported("deterministic mode: head outside the row-per-workgroup / partial-row family")
 

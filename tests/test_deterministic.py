@@ -58,7 +58,9 @@ def test_deterministic_mode_bitwise_gpu(monkeypatch):
     monkeypatch.setenv("CSA_DETERMINISTIC", "1")
     try:
         a, b = _run("cuda:0", steps=20), _run("cuda:0", steps=20)
-        assert a.backend == "torch" and a.use_graph
+        # conv + relu + overlapping 3x3/2 pool (a standalone gather-form unit in this mode)
+        # + norm + dense: on the HIP kernels since round 4
+        assert a.backend == "hip" and a.program.det and a.use_graph, a.fallback_reason
         assert torch.equal(a.flat, b.flat) and torch.equal(a.slots, b.slots)
     finally:
         torch.use_deterministic_algorithms(False)
@@ -198,7 +200,11 @@ def test_deterministic_hip_every_lowering_bitwise(monkeypatch, name):
         _, g_ref = grads("torch")
     finally:
         torch.use_deterministic_algorithms(False)
+    # (a gradient that is 0 in exact arithmetic — a conv bias feeding a BatchNorm — is fp32
+    # summation noise in both programs: bounded against the model's largest gradient, as in
+    # test_hip_step.py)
+    gmax = g_ref.abs().max().item()
     for k in e_det.model.state.shapes:
         a, b = e_det.model.state.view(k, g_det), e_det.model.state.view(k, g_ref)
         scale = b.abs().max().item() + 1e-6
-        assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6, k
+        assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6 + 1e-5 * gmax, k
