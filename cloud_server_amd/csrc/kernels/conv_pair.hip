@@ -1652,11 +1652,11 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
     if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_bwd_kernel<2, 2>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
     else hipLaunchKernelGGL((cpv_bwd_kernel<3, 3>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
     DUSegs u;                                                   // deferred updates on their own
-    if (du_take(DU_CARRY_PAIR, u) > 0) return du_flush_segs(u, st);
+    if (du_take(u) > 0) return du_flush_segs(u, st);
     return (int)hipGetLastError();
   }
   DUSegs u;
-  if (du_take(DU_CARRY_PAIR, u) > 0) return cp_launch_bwd_upd(a, u, st);
+  if (du_take(u) > 0) return cp_launch_bwd_upd(a, u, st);
   if (cp_bwd_one_batch(a))
     hipLaunchKernelGGL(conv_pair_bwd_kernel<true>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
   else

@@ -53,10 +53,6 @@ struct DUArgs {
   const float* hrl; const int* hrc;   // [M] per-row loss / correct
   float* ring_loss; int* ring_correct; int ring; float ldiv;
   int hact; float halpha;   // the head's input transform: the head reads act(hy)
-  // head update in place (hw != null): dWh / dbh go through the optimizer rule into the
-  // head parameters and their slots instead of hgw / hgb (the segment may then ride in the
-  // optimizer launch, which no longer touches the head)
-  float* hw; float* hb; float* hs0w; float* hs1w; float* hs0b; float* hs1b;
 };
 
 constexpr int DU_HNC = 10;           // head classes
@@ -64,16 +60,11 @@ constexpr int DU_HNC = 10;           // head classes
 // Weight-gradient + update segments recorded by csa_dense_update_defer (host state of the
 // calling thread, like the deterministic flag) until a carrying launch consumes them.
 constexpr int DU_MAXDEF = 4;
-// Carrying launches: the conv-pair backward, or the optimizer launch (a segment without the
-// head epilogue: the optimizer updates the head from the dWh that epilogue stores).
-constexpr int DU_CARRY_PAIR = 0, DU_CARRY_OPT = 1;
 struct DUDeferred {
   DUArgs seg[DU_MAXDEF];
   int blocks[DU_MAXDEF];    // workgroups of each segment (128-column, 256-thread)
-  int carrier[DU_MAXDEF];   // DU_CARRY_* of each segment
   int n = 0;
   int head = -1;            // segment carrying the head epilogue (-1: none)
-  int cur_carrier = DU_CARRY_PAIR;   // carrier given to the next deferred segment
 };
 extern thread_local DUDeferred g_du_def;
 
@@ -83,8 +74,8 @@ struct DUSegs {
   int start[DU_MAXDEF + 1];
   int nseg, head;
 };
-// Host: move the deferred segments of `carrier` into `out` (order kept); returns their count.
-int du_take(int carrier, DUSegs& out);
+// Host: move the deferred segments into `out` (order kept); returns their count.
+int du_take(DUSegs& out);
 // Host: the segments as standalone update-only launches.
 int du_flush_segs(const DUSegs& u, hipStream_t st);
 }  // namespace csa
@@ -185,16 +176,7 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
     } else {
       for (int m = 0; m < M; ++m) v = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), s_d[m * DU_HNC + j], v);
     }
-    const long o2 = (long)n * DU_HNC + j;
-    if (a.hw) {
-      float w = a.hw[o2], s0 = a.hs0w ? a.hs0w[o2] : 0.f, s1 = a.hs1w ? a.hs1w[o2] : 0.f;
-      opt_update(a.opt, opt_step_lr(a.opt, a.lr, a.step), w, v, s0, s1);
-      a.hw[o2] = w;
-      if (a.hs0w) a.hs0w[o2] = s0;
-      if (a.hs1w) a.hs1w[o2] = s1;
-    } else {
-      a.hgw[o2] = v;
-    }
+    a.hgw[(long)n * DU_HNC + j] = v;
   }
   if (last_block) {                                        // dbh and the step's metrics
     const int lane = t & 63, w = t >> 6;
@@ -202,15 +184,7 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
       if (lane < DU_HNC) {
         float v = 0.f;
         for (int m = 0; m < M; ++m) v += s_d[m * DU_HNC + lane];
-        if (a.hb) {
-          float w = a.hb[lane], s0 = a.hs0b ? a.hs0b[lane] : 0.f, s1 = a.hs1b ? a.hs1b[lane] : 0.f;
-          opt_update(a.opt, opt_step_lr(a.opt, a.lr, a.step), w, v, s0, s1);
-          a.hb[lane] = w;
-          if (a.hs0b) a.hs0b[lane] = s0;
-          if (a.hs1b) a.hs1b[lane] = s1;
-        } else {
-          a.hgb[lane] = v;
-        }
+        a.hgb[lane] = v;
       }
     } else if (w == 1) {
       float l = lane < M ? a.hrl[lane] : 0.f;
@@ -570,6 +544,8 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
 
 // Extra block e of a carrying launch: the update-only body of its deferred segment
 // (HEADOK = false: the carrier never holds the head segment, its code is not compiled in).
+// (Measured round 4: fc1's segment riding in the optimizer launch instead ran 0.0906-0.0911
+// ms/step against 0.0885-0.0887 in the pair backward — profiles/r4_notes.md.)
 template <int NSLOT, bool HEADOK>
 __device__ __forceinline__ void du_segs_body(const DUSegs& u, int e, float* smem) {
   int s = 0;

@@ -282,55 +282,23 @@ CSA_API int csa_dense_update_defer(const float* dY, float* W, float* bias, int M
   if (g_du_def.n == 0) g_du_def.head = -1;
   if (hy) g_du_def.head = g_du_def.n;
   g_du_def.blocks[g_du_def.n] = ((K + DU_FT - 1) / DU_FT) * a.cs;
-  g_du_def.carrier[g_du_def.n] = g_du_def.cur_carrier;
   g_du_def.seg[g_du_def.n++] = a;
   return g_du_def.n;
 }
 
-// Carrier of the segments deferred next on this thread: 0 = the conv-pair backward,
-// 1 = the optimizer launch (its fixed-latency chain of stripe folds leaves the CUs idle).
-CSA_API int csa_dense_update_carrier(int c) {
-  if (c != DU_CARRY_PAIR && c != DU_CARRY_OPT) return -1;
-  g_du_def.cur_carrier = c;
-  return 0;
-}
-
 CSA_API int csa_dense_update_pending() { return g_du_def.n; }
 
-// The deferred head segment updates the head parameters in place (see DUArgs::hw): its
-// dWh / dbh never reach the flat gradient, and the optimizer launch must skip the head.
-CSA_API int csa_dense_update_head_inplace(float* hw, float* hb, float* hs0w, float* hs1w, float* hs0b,
-                                          float* hs1b) {
-  if (g_du_def.head < 0 || !hw || !hb) return -1;
-  DUArgs& a = g_du_def.seg[g_du_def.head];
-  const int ns = opt_nslots(a.opt);
-  if ((ns >= 1 && (!hs0w || !hs0b)) || (ns >= 2 && (!hs1w || !hs1b))) return -2;
-  a.hw = hw; a.hb = hb; a.hs0w = hs0w; a.hs1w = hs1w; a.hs0b = hs0b; a.hs1b = hs1b;
-  return 0;
-}
-
 namespace csa {
-int du_take(int carrier, DUSegs& out) {
+int du_take(DUSegs& out) {
   out = DUSegs{};
-  out.head = -1;
-  int keep = 0;
-  for (int s = 0; s < g_du_def.n; ++s) {
-    if (g_du_def.carrier[s] == carrier) {
-      if (s == g_du_def.head) out.head = out.nseg;
-      out.seg[out.nseg] = g_du_def.seg[s];
-      out.start[out.nseg + 1] = out.start[out.nseg] + g_du_def.blocks[s];
-      ++out.nseg;
-    } else {
-      if (s == g_du_def.head) g_du_def.head = keep;
-      g_du_def.seg[keep] = g_du_def.seg[s];
-      g_du_def.blocks[keep] = g_du_def.blocks[s];
-      g_du_def.carrier[keep] = g_du_def.carrier[s];
-      ++keep;
-    }
+  out.head = g_du_def.head;
+  out.nseg = g_du_def.n;
+  for (int s = 0; s < DU_MAXDEF; ++s) {
+    if (s < out.nseg) out.seg[s] = g_du_def.seg[s];
+    out.start[s + 1] = out.start[s] + (s < out.nseg ? g_du_def.blocks[s] : 0);
   }
-  if (out.head >= 0) g_du_def.head = -1;
-  g_du_def.n = keep;
-  for (int s = out.nseg; s < DU_MAXDEF; ++s) out.start[s + 1] = out.start[s];
+  g_du_def.n = 0;
+  g_du_def.head = -1;
   return out.nseg;
 }
 }  // namespace csa
@@ -352,14 +320,8 @@ int du_flush_segs(const DUSegs& u, hipStream_t st) {
 }  // namespace csa
 
 CSA_API int csa_dense_update_flush(hipStream_t st) {
-  int rc = 0;
-  for (int c : {DU_CARRY_PAIR, DU_CARRY_OPT}) {
-    DUSegs u;
-    if (du_take(c, u) > 0 && (rc = du_flush_segs(u, st)) != 0) break;
-  }
-  g_du_def.n = 0;
-  g_du_def.head = -1;
-  return rc;
+  DUSegs u;
+  return du_take(u) > 0 ? du_flush_segs(u, st) : 0;
 }
 
-CSA_API void csa_dense_update_clear() { g_du_def.n = 0; g_du_def.head = -1; g_du_def.cur_carrier = DU_CARRY_PAIR; }
+CSA_API void csa_dense_update_clear() { g_du_def.n = 0; g_du_def.head = -1; }

@@ -17,7 +17,6 @@
 //   * advance the batch-stream cursor (mod its wrap).
 #include "common.h"
 #include "optim_common.h"
-#include "dense_update.h"
 #include <cstdlib>
 
 namespace csa {
@@ -130,10 +129,9 @@ __constant__ long long* g_opt_dbg = nullptr;
     if (g_opt_dbg && threadIdx.x == 0) g_opt_dbg[blockIdx.x * 4 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-// Blocks [0, nblk) of the launch: the update over the segments, then the stage blocks.
-__device__ __forceinline__ void optim_body(const OptArgs& a, int nblk) {
+__global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   OPT_STAMP(0);
-  const int nmain = nblk - a.stage.blocks;
+  const int nmain = (int)gridDim.x - a.stage.blocks;
   if ((int)blockIdx.x >= nmain) {
     stage_gather(a.stage, (int)blockIdx.x - nmain);
     OPT_STAMP(3);
@@ -244,24 +242,6 @@ __device__ __forceinline__ void optim_body(const OptArgs& a, int nblk) {
   OPT_STAMP(3);
 }
 
-__global__ __launch_bounds__(256) void optim_kernel(OptArgs a) { optim_body(a, (int)gridDim.x); }
-
-// Horizontal fusion (round 4): the optimizer's blocks [0, nopt) followed by deferred dense
-// weight-gradient + update segments (csa_dense_update_carrier(1)).  The optimizer launch is
-// a short latency chain (the conv stripe folds: ~5 us of dependent loads on a few blocks,
-// profiles/r3_notes.md) that leaves most CUs idle; a dense layer's update only has to land
-// before the next step's forward of that layer.  Never the head segment: this launch
-// updates the head from the dWh that segment's epilogue stores.
-template <int NSLOT, bool HEAD>
-__global__ __launch_bounds__(256) void optim_upd_kernel(OptArgs a, DUSegs u, int nopt) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  if ((int)blockIdx.x < nopt) {
-    optim_body(a, nopt);
-    return;
-  }
-  du_segs_body<NSLOT, HEAD>(u, (int)blockIdx.x - nopt, smem);
-}
-
 }  // namespace csa
 
 using namespace csa;
@@ -349,13 +329,6 @@ CSA_API int csa_optimizer2(int opt, float* w, float* g, float* s0, float* s1, lo
 
 // ... plus the next step's batch staging (st_out_img != null; the head advanced the
 // cursor, so pass cursor = null here).
-template <int NSLOT>
-static void launch_opt_upd(bool head, unsigned grid, size_t lds, hipStream_t st, const OptArgs& a, const DUSegs& u,
-                           int nopt) {
-  if (head) hipLaunchKernelGGL((optim_upd_kernel<NSLOT, true>), dim3(grid), dim3(256), lds, st, a, u, nopt);
-  else hipLaunchKernelGGL((optim_upd_kernel<NSLOT, false>), dim3(grid), dim3(256), lds, st, a, u, nopt);
-}
-
 CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, long n, const long* seg_lo,
                             const long* seg_hi, int nseg, int zero_grad, float lr, const int64_t* step,
                             float* const* zero_ptrs, const long* zero_ns, int nzero, const long* fold_off,
@@ -411,26 +384,7 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   a.stage = make_stage(st_img, st_labels, st_rows, st_cursor, st_B, st_imsz, st_out_img, st_out_lbl);
-  const int nopt = blocks + a.stage.blocks;
-  DUSegs u;
-  if (du_take(DU_CARRY_OPT, u) > 0) {
-    // a head segment here must update the head in place: this launch no longer reads dWh
-    if (u.head >= 0 && !u.seg[u.head].hw) return -7;
-    size_t lds = 0;
-    for (int s = 0; s < u.nseg; ++s) {
-      if (opt_nslots(u.seg[s].opt) != opt_nslots(opt)) return -6;
-      const size_t l = du_lds_floats(u.seg[s].M, 4) * sizeof(float);
-      lds = l > lds ? l : lds;
-    }
-    const unsigned grid = (unsigned)(nopt + u.start[u.nseg]);
-    const int ns = opt_nslots(opt);
-    const bool hd = u.head >= 0;
-    if (ns == 0) launch_opt_upd<0>(hd, grid, lds, st, a, u, nopt);
-    else if (ns == 1) launch_opt_upd<1>(hd, grid, lds, st, a, u, nopt);
-    else launch_opt_upd<2>(hd, grid, lds, st, a, u, nopt);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(optim_kernel, dim3(nopt), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(optim_kernel, dim3(blocks + a.stage.blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

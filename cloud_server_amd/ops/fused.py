@@ -66,8 +66,6 @@ _SIGS = {
     "csa_dense_update_defer": (I, [P, P, P, I, I, I, P, I, F, P, P, P, P, P, F, P, P, P, P, P, P, P, P, I, F,
                                    I, F]),
     "csa_dense_update_pending": (I, []),
-    "csa_dense_update_carrier": (I, [I]),
-    "csa_dense_update_head_inplace": (I, [P, P, P, P, P, P]),
     "csa_head_dgrad_ok": (I, [I, I, I]),
     "csa_head_dgrad": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, L, P, I, P, I, F, P, P]),
     "csa_dense_update_flush": (I, [P]),

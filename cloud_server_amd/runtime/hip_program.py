@@ -456,12 +456,6 @@ class HipProgram:
         if any(u.layer.spec.hidden % 128 for u in dense):
             return
         self.hfuse = True
-        # the segments ride in the optimizer launch instead of the pair backward; the head
-        # segment then updates the head in place (the optimizer launch skips the head)
-        carrier = os.environ.get("CSA_DU_CARRIER", "pair")
-        self.du_opt_carrier = carrier in ("opt", "split")
-        self.du_head_opt = carrier == "opt"          # "split": the head segment stays in the pair
-        self.head_inplace = self.du_head_opt and self.head_row
         # the last dense layer's input gradient rides in the head launch (csa_head_dgrad:
         # every workgroup recomputes the head for its rows, no batch reduction), when that
         # layer's input transform is at most an activation
@@ -1484,11 +1478,8 @@ class HipProgram:
         else:
             head = (None, None, None, None, None, None, None, None, 1, 1.0, 0, 0.0)
         if self.hfuse:
-            # weight gradient + update deferred into a carrying launch: the pair backward,
-            # or (a segment without the head epilogue) the optimizer launch; the input
+            # weight gradient + update deferred into the pair backward launch; the input
             # gradient (+ transform backward + BN statistics) now
-            lib.csa_dense_update_carrier(
-                1 if self.du_opt_carrier and (head[0] is None or self.du_head_opt) else 0)
             rc = lib.csa_dense_update_defer(
                 K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
                 B, fin, fout, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
@@ -1497,13 +1488,6 @@ class HipProgram:
                 1.0, *head)
             if rc < 0:
                 raise RuntimeError(f"dense_update_defer failed: {rc}")
-            if head[0] is not None and self.head_inplace:
-                hw_, hb_ = offs["head.weight"], offs["head.bias"]
-                self._rc(lib.csa_dense_update_head_inplace(
-                    K.ptr(self.views["head.weight"]), K.ptr(self.views["head.bias"]),
-                    K.ptr(s0[hw_:]) if s0 is not None else None, K.ptr(s1[hw_:]) if s1 is not None else None,
-                    K.ptr(s0[hb_:]) if s0 is not None else None, K.ptr(s1[hb_:]) if s1 is not None else None),
-                    "dense_update_head_inplace")
             if prev is not None and not (self.head_dgrad and u is self.units[-1]):
                 self._rc(lib.csa_dense_bwd_dgrad(
                     K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
@@ -1549,8 +1533,6 @@ class HipProgram:
         for u in self.units:
             if u.kind == "dense" and ((u.fused and self.fused) or u.lr_update):
                 skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
-        if getattr(self, "head_inplace", False):     # updated by the head segment itself
-            skip |= {offs["head.weight"], offs["head.bias"]}
         if not skip:
             return []
         segs: List[list] = []
@@ -1638,6 +1620,6 @@ class HipProgram:
             zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, fz, len(folds), klo, khi, len(keep),
             *met, *cursor_args, *stage, st), "optimizer")
         if getattr(self, "hfuse", False) and lib.csa_dense_update_pending():
-            raise RuntimeError("deferred dense updates were not consumed by their carrying launches")
+            raise RuntimeError("deferred dense updates were not consumed by the pair backward")
         if e.sync.strategy == "ps" and e.ctx.enabled:
             e.sync.all_gather_params(e.flat)
