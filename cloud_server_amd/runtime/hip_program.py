@@ -447,7 +447,10 @@ class HipProgram:
         layer's deferred segment exactly as they rode in its fused backward."""
         self.hfuse = False
         self.head_dgrad = False
-        if (self.forward_only or not self.fused or self.det or self.pair is None
+        # (not in the packed profile: there the other jobs' kernels already fill the CUs the
+        # pair backward leaves idle, and K = 4 / 8 packs measured 1.10 / 1.12 M samples/s with
+        # the deferred updates against 1.17 / 1.23 M without — profiles/r4_multitenant.md)
+        if (self.forward_only or not self.fused or self.det or self.pair is None or self.packed
                 or os.environ.get("CSA_HFUSE", "1") != "1"):
             return
         dense = [u for u in self.units if u.kind == "dense" and u.fused]

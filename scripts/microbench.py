@@ -184,14 +184,27 @@ def main() -> int:
                 t = dbg.tolist()
                 print(f"{i:2d} {name}: stage {t[1]-t[0]} labels+sync {t[2]-t[1]} logits {t[3]-t[2]} "
                       f"loss {t[4]-t[3]} dW/dh {t[5]-t[4]} | total {t[5]-t[0]}")
+    # horizontal fusion: the deferred dense updates are host-side records that the pair
+    # backward consumes, so every replay of that launch re-records them first
+    defers = [(fn, args) for name, fn, args in rec.calls if name == "csa_dense_update_defer"]
+    host_only = ("csa_dense_update_defer", "csa_dense_update_clear", "csa_dense_update_pending")
+
+    def call(name, fn, args):
+        if name == "csa_conv_pair_bwd":
+            for dfn, dargs in defers:
+                dfn(*dargs)
+        fn(*args)
+
     for i, (name, fn, args) in enumerate(rec.calls):
+        if name in host_only:
+            continue
         for _ in range(5):
-            fn(*args)
+            call(name, fn, args)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(a.reps):
-            fn(*args)
+            call(name, fn, args)
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) * 1e3 / a.reps

@@ -53,7 +53,11 @@ def main():
             "csa_bn_act_apply": "bn_act_apply_kernel", "csa_dense_fwd": "gemm_f32_kernel",
             "csa_head_part": "head_part_kernel", "csa_head_part2": "head_part_kernel", "csa_dense_bwd": "gemm_pair_kernel",
             "csa_optimizer2": "optim_kernel", "csa_optimizer2s": "optim_kernel", "csa_dd_fwd": "dd_fwd_kernel", "csa_dd_dgrad": "dd_dgrad_kernel",
-            "csa_dd_wgrad": "dd_wgrad_kernel", "csa_dense_bwd_update": "dense_bwd_update_kernel"}
+            "csa_dd_wgrad": "dd_wgrad_kernel", "csa_dense_bwd_update": "dense_bwd_update_kernel",
+            "csa_dense_bwd_dgrad": "dense_bwd_update_kernel", "csa_head_dgrad": "head_dgrad_kernel"}
+    # the pair backward carrying the deferred dense updates (horizontal fusion)
+    if "conv_pair_bwd_upd_kernel" in a:
+        kmap["csa_conv_pair_bwd"] = "conv_pair_bwd_upd_kernel"
     print("| # | launch | µs (isolated) | HBM read MB | HBM write MB | achieved TB/s | % of 8 TB/s | "
           "f32 MFMA GFLOP | TFLOP/s | % of 157 TF |")
     print("|---|---|---|---|---|---|---|---|---|---|")
