@@ -195,6 +195,39 @@ def main() -> int:
                 dfn(*dargs)
         fn(*args)
 
+    if os.environ.get("MB_HF"):
+        # horizontal fusion: the pair backward alone, the deferred updates alone (their own
+        # launches), and the pair backward carrying them
+        lib = eng.program.lib
+        pb = [(fn, args) for name, fn, args in rec.calls if name == "csa_conv_pair_bwd"][0]
+
+        def timed(f):
+            for _ in range(5):
+                f()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.reps):
+                f()
+            e.record()
+            torch.cuda.synchronize()
+            return s.elapsed_time(e) * 1e3 / a.reps
+
+        def pair_alone():
+            lib.csa_dense_update_clear()
+            pb[0](*pb[1])
+
+        def upd_alone():
+            for dfn, dargs in defers:
+                dfn(*dargs)
+            lib.csa_dense_update_flush(None)
+
+        def fused():
+            for dfn, dargs in defers:
+                dfn(*dargs)
+            pb[0](*pb[1])
+        print(f"HF: pair alone {timed(pair_alone):.2f} us | updates alone {timed(upd_alone):.2f} us | "
+              f"pair + updates in one launch {timed(fused):.2f} us")
     for i, (name, fn, args) in enumerate(rec.calls):
         if name in host_only:
             continue
