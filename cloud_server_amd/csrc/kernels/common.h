@@ -68,6 +68,7 @@ struct FastDiv {
 // serial memory round trip per element.  Pin a batch of loads after issuing all of them.
 __device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 __device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
 
 // Block-cooperative copy global -> LDS with a per-element transform, issuing UNROLL
 // independent loads per thread before any store (branch-free clamped addresses), so a

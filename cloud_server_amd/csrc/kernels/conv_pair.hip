@@ -68,7 +68,7 @@ struct CPBand {
   int TXH, TXW;     // x tile: rows c1y0 - PTA + ty, cols tx - PLB - PLA
 };
 
-__device__ __forceinline__ CPBand cp_band(const CPGeom& g, int r2a, int r2b) {
+__host__ __device__ inline CPBand cp_band(const CPGeom& g, int r2a, int r2b) {
   CPBand t;
   t.r2a = r2a; t.r2b = r2b;
   t.c1y0 = r2a - g.PTB;
@@ -449,6 +449,7 @@ struct CPBwdArgs {
   BNRef bn; int bn_on; const float* bwd_slab; int bwd_nslab;
   float* dscale; float* doffset; float* run_mean; float* run_var; float momentum;
   float* dwA; float* dbA; float* dwB; float* dbB; int stripes;
+  const int* tabs; int tab_stride;  // per-band index tables (csa_conv_pair_bwd_tables) or null
 };
 
 // LDS carve of the backward (float offsets), shared by the kernel and the host size check.
@@ -491,9 +492,64 @@ __host__ __device__ inline CPBwdLayout cp_bwd_layout(const CPGeom& g, int band, 
   return L;
 }
 
+// The backward's per-band index tables (they depend on the band only): into the int region
+// at s_offA (layout: see cp_bwd_body).  Computed once per geometry into global memory by
+// cp_bwd_tables_kernel, or by every workgroup when no table buffer was given.
+__device__ __forceinline__ void cp_bwd_tables(const CPGeom& g, const CPBand& t, const CPBwdLayout& L, int* s_offA) {
+  int* s_offPA = s_offA + L.kpadA;
+  int* s_pix2 = s_offPA + L.kpadA;
+  int* s_pixd = s_pix2 + L.kp2;
+  int* s_offD = s_pixd + L.kp2;
+  int* s_offW = s_offD + L.kpadD;
+  int* s_pix1x = s_offW + L.kpadD;
+  int* s_pix1d = s_pix1x + L.kp1;
+  int* s_tapB = s_pix1d + L.kp1;
+  cp_tables_a(g, t, L.kpadA, s_offA, s_offPA);
+  {
+    const FastDiv dw2(g.W2), dw1(g.W1);
+    const int zrow2 = ((L.D2H - 1) * L.D2W) * g.C2;           // the dc2 tile's zero row
+    for (int p = threadIdx.x; p < L.kp2; p += CP_THREADS) {
+      int yy, xx;
+      dw2.divmod(p < L.npix2 ? p : 0, yy, xx);
+      s_pix2[p] = (yy * t.T1W + xx) * g.C1;                   // y2 - o2a = yy
+      s_pixd[p] = p < L.npix2 ? ((L.o2a + yy - L.d2y0) * L.D2W + xx + g.KBw - 1 - g.PLB) * g.C2 : zrow2;
+    }
+    for (int k = threadIdx.x; k < L.kpadD; k += CP_THREADS) {
+      int od = 0, ow = 0;
+      if (k < L.KD) {
+        const int c2 = k % g.C2, ij = k / g.C2, i = ij / g.KBw, j = ij - i * g.KBw;
+        od = -(i * L.D2W + j) * g.C2 + c2;
+        ow = ij * g.C1 * g.C2 + c2;
+      } else {
+        ow = L.kpadB * L.c16 - 1 - (g.C1 - 1) * g.C2;   // -> zero pad of the weight area
+        if (ow < 0) ow = 0;
+      }
+      s_offD[k] = od;
+      s_offW[k] = ow;
+    }
+    for (int p = threadIdx.x; p < L.kp1; p += CP_THREADS) {
+      int yy, xx;
+      dw1.divmod(p < L.npix1 ? p : 0, yy, xx);
+      s_pix1x[p] = ((L.o1a + yy - t.c1y0) * t.TXW + xx + g.PLB) * g.C0;
+      s_pix1d[p] = (p < L.npix1 ? p : L.npix1) * g.C1;      // padded pixels -> the zero row
+    }
+    for (int k = threadIdx.x; k < L.n16b; k += CP_THREADS) {
+      int o = 0;
+      if (k < L.KB) {
+        const int c1 = k % g.C1, ij = k / g.C1, i = ij / g.KBw, j = ij - i * g.KBw;
+        o = (i * t.T1W + j) * g.C1 + c1;
+      }
+      s_tapB[k] = o;
+    }
+  }
+}
+
+// Ints of one band's table region (the int area of the LDS carve).
+__host__ __device__ inline int cp_bwd_tab_ints(const CPBwdLayout& L) { return L.end - L.offs; }
+
 // Prologue register batch of the backward (ONE = true): weights (panel A + dense wB),
 // x tile and BN slab rows per thread.  The host picks ONE when every band fits.
-constexpr int CPB_UP = 8, CPB_UX = 2, CPB_US = 8;
+constexpr int CPB_UP = 8, CPB_UX = 2, CPB_US = 8, CPB_UT = 4;
 
 template <bool ONE>
 __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, float* smem) {
@@ -538,6 +594,18 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   float pv[CPB_UP], vf[CPB_US], vb[CPB_US], sc = 0.f, of = 0.f;
   bool pok[CPB_UP], xok[CPB_UX];
   uint8_t xv[CPB_UX];
+  // precomputed index tables: issued first (the host checks that a band's region fits
+  // CPB_UT ints per thread)
+  const int ntab = cp_bwd_tab_ints(L);
+  int tv[CPB_UT];
+  if (a.tabs) {
+    const int* tsrc = a.tabs + (long)band * a.tab_stride;
+#pragma unroll
+    for (int u = 0; u < CPB_UT; ++u) {
+      const int e = u * CP_THREADS + (int)threadIdx.x;
+      tv[u] = tsrc[e < ntab ? e : 0];
+    }
+  }
   if (ONE) {
     if (a.bn_on) for (int i = threadIdx.x; i < C2x2; i += CP_THREADS) { s_red[i] = 0.f; s_ss[i] = 0.f; }
 #pragma unroll
@@ -583,45 +651,17 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   CP_STAMP(16);
   for (int i = threadIdx.x; i < L.D2H * L.D2W * g.C2; i += CP_THREADS) s_dc2[i] = 0.f;
   for (int i = threadIdx.x; i < g.C1; i += CP_THREADS) s_dc1[L.npix1 * g.C1 + i] = 0.f;
-  cp_tables_a(g, t, L.kpadA, s_offA, s_offPA);
-  {
-    const FastDiv dw2(g.W2), dw1(g.W1);
-    const int zrow2 = ((L.D2H - 1) * L.D2W) * g.C2;           // the dc2 tile's zero row
-    for (int p = threadIdx.x; p < L.kp2; p += CP_THREADS) {
-      int yy, xx;
-      dw2.divmod(p < L.npix2 ? p : 0, yy, xx);
-      s_pix2[p] = (yy * t.T1W + xx) * g.C1;                   // y2 - o2a = yy
-      s_pixd[p] = p < L.npix2 ? ((L.o2a + yy - L.d2y0) * L.D2W + xx + g.KBw - 1 - g.PLB) * g.C2 : zrow2;
-    }
-    for (int k = threadIdx.x; k < L.kpadD; k += CP_THREADS) {
-      int od = 0, ow = 0;
-      if (k < L.KD) {
-        const int c2 = k % g.C2, ij = k / g.C2, i = ij / g.KBw, j = ij - i * g.KBw;
-        od = -(i * L.D2W + j) * g.C2 + c2;
-        ow = ij * g.C1 * g.C2 + c2;
-      } else {
-        ow = L.kpadB * L.c16 - 1 - (g.C1 - 1) * g.C2;   // -> zero pad of the weight area
-        if (ow < 0) ow = 0;
-      }
-      s_offD[k] = od;
-      s_offW[k] = ow;
-    }
-    for (int p = threadIdx.x; p < L.kp1; p += CP_THREADS) {
-      int yy, xx;
-      dw1.divmod(p < L.npix1 ? p : 0, yy, xx);
-      s_pix1x[p] = ((L.o1a + yy - t.c1y0) * t.TXW + xx + g.PLB) * g.C0;
-      s_pix1d[p] = (p < L.npix1 ? p : L.npix1) * g.C1;      // padded pixels -> the zero row
-    }
-    for (int k = threadIdx.x; k < L.n16b; k += CP_THREADS) {
-      int o = 0;
-      if (k < L.KB) {
-        const int c1 = k % g.C1, ij = k / g.C1, i = ij / g.KBw, j = ij - i * g.KBw;
-        o = (i * t.T1W + j) * g.C1 + c1;
-      }
-      s_tapB[k] = o;
+  if (!a.tabs) cp_bwd_tables(g, t, L, s_offA);
+  CP_STAMP(17);
+  if (a.tabs) {
+#pragma unroll
+    for (int u = 0; u < CPB_UT; ++u) pin(tv[u]);
+#pragma unroll
+    for (int u = 0; u < CPB_UT; ++u) {
+      const int e = u * CP_THREADS + (int)threadIdx.x;
+      if (e < ntab) s_offA[e] = tv[u];
     }
   }
-  CP_STAMP(17);
   if (ONE) {
 #pragma unroll
     for (int u = 0; u < CPB_UP; ++u) pin(pv[u]);
@@ -852,8 +892,7 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
 // The pair's workgroups come first: the dispatcher deals blocks in index order, so the
 // critical pair blocks all start before any update block takes a slot.
 template <bool ONE, int NSLOT>
-__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs& u, float* smem) {
   const int npair = a.g.B * a.g.nbands;
   const int bid = (int)blockIdx.x;
   if (bid < npair) {
@@ -861,6 +900,12 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs
     return;
   }
   du_segs_body<NSLOT, true>(u, bid - npair, smem);
+}
+
+template <bool ONE, int NSLOT>
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cp_bwd_upd_body<ONE, NSLOT>(a, u, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1619,15 +1664,68 @@ static int cp_launch_bwd_upd(const CPBwdArgs& a, const DUSegs& u, hipStream_t st
   return one ? cp_launch_bwd_upd_t<true, 2>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 2>(a, u, lds, st);
 }
 
+__global__ __launch_bounds__(CP_THREADS) void cp_bwd_tables_kernel(CPGeom g, int* out, int stride) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int band = blockIdx.x, pr0 = band * g.PR;
+  const bool last = band == g.nbands - 1;
+  const int o2a = g.pool ? 2 * pr0 : pr0;
+  const int o2b = g.pool ? (last ? g.H2 : 2 * min(g.PH, pr0 + g.PR)) : min(g.PH, pr0 + g.PR);
+  const CPBand t = cp_band(g, o2a, o2b);
+  const CPBwdLayout L = cp_bwd_layout(g, band, t.TXH, t.TXW, t.T1H, t.T1W);
+  int* s = reinterpret_cast<int*>(smem);
+  cp_bwd_tables(g, t, L, s);
+  __syncthreads();
+  for (int i = threadIdx.x; i < cp_bwd_tab_ints(L); i += CP_THREADS) out[(long)band * stride + i] = s[i];
+}
+
+static int cp_bwd_tab_stride(const CPGeom& g) {
+  int m = 0;
+  for (int band = 0; band < g.nbands; ++band) {
+    const int pr0 = band * g.PR;
+    const bool last = band == g.nbands - 1;
+    const int o2a = g.pool ? 2 * pr0 : pr0;
+    const int o2b = g.pool ? (last ? g.H2 : 2 * std::min(g.PH, pr0 + g.PR)) : std::min(g.PH, pr0 + g.PR);
+    const CPBand t = cp_band(g, o2a, o2b);
+    m = std::max(m, cp_bwd_tab_ints(cp_bwd_layout(g, band, t.TXH, t.TXW, t.T1H, t.T1W)));
+  }
+  return (m + 3) & ~3;
+}
+
+// Ints of the backward's per-band index-table buffer (0: the pair keeps computing them per
+// workgroup — a band's region exceeds the prologue's register batch).
+CSA_API long csa_conv_pair_bwd_tables_size(const int* geom) {
+  CPGeom g;
+  if (!cp_geom(geom, g)) return -1;
+  const int stride = cp_bwd_tab_stride(g);
+  if (stride > CPB_UT * CP_THREADS) return 0;
+  return (long)stride * g.nbands;
+}
+
+// Fill the table buffer (once per geometry, at plan time).  The ~440 ints of the sample
+// pair's band were recomputed by all 700 workgroups every step: ~4.6k cycles of integer
+// VALU work at three waves per SIMD in front of the first route store
+// (profiles/r4_roofline.md).
+CSA_API int csa_conv_pair_bwd_tables(const int* geom, int* out, hipStream_t st) {
+  CPGeom g;
+  if (!cp_geom(geom, g) || !out) return -1;
+  const int stride = cp_bwd_tab_stride(g);
+  hipLaunchKernelGGL(cp_bwd_tables_kernel, dim3((unsigned)g.nbands), dim3(CP_THREADS), (size_t)stride * sizeof(int),
+                     st, g, out, stride);
+  return (int)hipGetLastError();
+}
+
 CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
                               const float* bn_slab, int bn_nslab, float bn_count, float bn_eps, const float* bn_scale,
                               const float* bn_offset, const float* bwd_slab, int bwd_nslab, float* dscale,
                               float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
-                              float* dwB, float* dbB, int stripes, hipStream_t st) {
+                              float* dwB, float* dbB, int stripes, const int* tabs, hipStream_t st) {
   CPBwdArgs a{};
   if (!cp_geom(geom, a.g) || cp_lds(a.g, true) > CP_LDS_MAX) return -1;
+  a.tabs = tabs;
+  a.tab_stride = tabs ? cp_bwd_tab_stride(a.g) : 0;
+  if (tabs && a.tab_stride > CPB_UT * CP_THREADS) return -6;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
   a.wB = wB; a.actB = actB; a.alphaB = alphaB; a.hasBiasB = hasBiasB; a.dz = dz; a.y = y; a.argmax = argmax;
   a.bn = BNRef{bn_slab, bn_nslab, a.g.C2, bn_count, bn_eps, bn_scale, bn_offset};

@@ -420,6 +420,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
   if (HEAD) du_head_finish<THREADS>(a, hd, s_hw, bid == nblk - 1);
   if (!dgrad) {                                            // uniform: first layer
     if (!DGO) du_store_w<NSLOT>(a, wv, s0v, s1v, wofs, sok, i, nf, bown, bn0, bw, bs0, bs1);
+    DU_STAMP(6);
     return;
   }
 

@@ -87,7 +87,9 @@ _SIGS = {
     "csa_packed": (I, []),
     "csa_rows_fold": (I, [P, L, I, L, P, I, P]),
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,
-                              P, P, P, P, I, P]),
+                              P, P, P, P, I, P, P]),
+    "csa_conv_pair_bwd_tables_size": (L, [P]),
+    "csa_conv_pair_bwd_tables": (I, [P, P, P]),
     "csa_head_part": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P]),
     "csa_head_part2": (I, [P, I, I, I, F, P, P, P, P, P, I, F, P, P, P, P, P, P, P, L, P]),
     "csa_gather_batch": (I, [P, P, P, P, I, L, P, P, P]),

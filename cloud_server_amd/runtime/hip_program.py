@@ -169,6 +169,14 @@ class HipProgram:
             self._check_det()
         self._alloc()
         self._plan_splits()
+        # the pair backward's per-band index tables, computed once (csa_conv_pair_bwd_tables)
+        self.pair_tabs = None
+        if self.pair is not None and not forward_only:
+            n = int(self.lib.csa_conv_pair_bwd_tables_size(K.ints(self.pair)))
+            if n > 0:
+                self.pair_tabs = torch.zeros(n, dtype=torch.int32, device=eng.device)
+                self._rc(self.lib.csa_conv_pair_bwd_tables(K.ints(self.pair), K.ptr(self.pair_tabs), K.stream()),
+                         "conv_pair_bwd_tables")
         if forward_only:
             self.staged = False
             return
@@ -1382,7 +1390,7 @@ class HipProgram:
             K.ptr(dsc), K.ptr(dof), K.ptr(rm), K.ptr(rv), float(self.model.bn_momentum),
             K.ptr(ua.dw_acc), K.ptr(ua.db_acc) if ua.layer.spec.bias else None,
             K.ptr(ub.dw_acc), K.ptr(ub.db_acc) if ub.layer.spec.bias else None,
-            min(ua.wg_stripes, ub.wg_stripes), st), "conv_pair_bwd")
+            min(ua.wg_stripes, ub.wg_stripes), K.ptr(self.pair_tabs), st), "conv_pair_bwd")
         self._sync_bn_param_grads(nt)
         if ua.row_fold:
             for u in (ua, ub):

@@ -228,6 +228,36 @@ def main() -> int:
             pb[0](*pb[1])
         print(f"HF: pair alone {timed(pair_alone):.2f} us | updates alone {timed(upd_alone):.2f} us | "
               f"pair + updates in one launch {timed(fused):.2f} us")
+        cdbg = torch.zeros(24, dtype=torch.int64, device="cuda")
+        for label, f in (("pair alone", pair_alone), ("pair + updates", fused)):
+            for _ in range(3):
+                cdbg.zero_()
+                lib.csa_cp_debug(cdbg.data_ptr())
+                f()
+                torch.cuda.synchronize()
+                lib.csa_cp_debug(None)
+            t = cdbg.tolist()
+            print(f"  {label} block 0: loads {t[16]-t[8]} tables {t[17]-t[16]} stores {t[18]-t[17]} "
+                  f"bn {t[9]-t[19]} route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} dc1 {t[13]-t[12]} "
+                  f"dwA {t[14]-t[13]} atomics {t[15]-t[14]} | total {t[15]-t[8]} (s_memtime ticks)")
+        # per-block stamps of the update-only launches (100 MHz realtime: start, dY staged,
+        # W landed, MFMA + update done, stores issued)
+        dbg = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
+        for dfn, dargs in defers:
+            dbg.zero_()
+            lib.csa_du_debug(dbg.data_ptr())
+            dfn(*dargs)
+            lib.csa_dense_update_flush(None)
+            torch.cuda.synchronize()
+            lib.csa_du_debug(None)
+            t = dbg.view(-1, 8)
+            t = t[t[:, 0] > 0].double()
+            t0 = t[:, 0].min()
+            d = lambda k1, k0: ((t[:, k1] - t[:, k0]) / 100)
+            print(f"  segment K={dargs[4]} N={dargs[5]}: blocks {len(t)} span {(t[:, 6].max() - t0) / 100:.2f} us | "
+                  f"start spread {(t[:, 0].max() - t0) / 100:.2f} | stage {d(1, 0).mean():.2f}/{d(1, 0).max():.2f} | "
+                  f"W {d(2, 1).mean():.2f}/{d(2, 1).max():.2f} | mfma+upd {d(3, 2).mean():.2f}/{d(3, 2).max():.2f} | "
+                  f"store issue {d(6, 3).mean():.2f}/{d(6, 3).max():.2f} | block life {d(6, 0).mean():.2f}/{d(6, 0).max():.2f} (mean/max us)")
     for i, (name, fn, args) in enumerate(rec.calls):
         if name in host_only:
             continue
