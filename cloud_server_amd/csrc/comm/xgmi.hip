@@ -350,6 +350,14 @@ CSA_API int csa_xgmi_alloc(long bytes, void** ptr, void* handle) {
   return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), *ptr);
 }
 
+// A pooled buffer handed to a new channel: zeroed again, its IPC handle re-exported.
+CSA_API int csa_xgmi_reuse(void* ptr, long bytes, void* handle) {
+  hipError_t e = hipMemset(ptr, 0, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), ptr);
+}
+
 CSA_API int csa_xgmi_open(const void* handle, void** ptr) {
   hipIpcMemHandle_t h;
   memcpy(&h, handle, sizeof(h));

@@ -126,6 +126,7 @@ _SIGS = {
     "csa_maxpool_bwd": (I, [P, P, P, P, P]),
     "csa_xgmi_alloc": (I, [L, C.POINTER(P), P]),
     "csa_xgmi_open": (I, [P, C.POINTER(P)]),
+    "csa_xgmi_reuse": (I, [P, L, P]),
     "csa_xgmi_close": (I, [P]),
     "csa_xgmi_free": (I, [P]),
     "csa_xgmi_handle_bytes": (I, []),

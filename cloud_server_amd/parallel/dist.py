@@ -60,6 +60,10 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 300.0) -> Dis
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = device
+            # RCCL collectives are captured into the step's HIP graphs; with the process-wide
+            # CUDA-event cache a work's end event can be one last recorded inside a capture,
+            # which the watchdog thread may not query (hipErrorCapturedEvent aborts the rank)
+            os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
         dist.init_process_group(**kw)
     return DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
 

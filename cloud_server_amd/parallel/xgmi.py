@@ -49,6 +49,14 @@ def _aligned(t: torch.Tensor) -> bool:
     return t.is_contiguous() and t.data_ptr() % 16 == 0 and (t.numel() * t.element_size()) % 16 == 0
 
 
+# Peer buffers are recycled inside the process, never freed before exit: after a hipFree an
+# uncached allocation of the same size can come back at the same address while a peer's
+# mapping of the old one is stale (a third channel set created in one process timed out
+# with one rank never seeing the other's pushes: profiles/r4_notes.md).  Keyed by
+# (device index, bytes).
+_POOL: Dict[Tuple[int, int], List[int]] = {}
+
+
 class XgmiChannel:
     def __init__(self, rank: int, world: int, slot_bytes: int, device: torch.device,
                  group=None, timeout_s: float = 20.0):
@@ -63,19 +71,30 @@ class XgmiChannel:
         # receive slots (+ slack: two-shot shards round up to 16 B) and per-phase flags
         sizes = (2 * world * self.slot_bytes + 64 * world, 2 * 2 * nblk * 8 * 4)
         self._local: List[int] = []
+        self._local_n: List[int] = []
         self._opened: List[int] = []
+        self._dev = device.index if device.index is not None else torch.cuda.current_device()
         # every failure is agreed on collectively (all ranks raise together), so a rank
         # that cannot allocate or map never leaves its peers inside a collective
         handles: Optional[List[bytes]] = []
         with torch.cuda.device(device):
             try:
                 for n in sizes:
-                    p = C.c_void_p()
                     h = C.create_string_buffer(hb)
-                    rc = self.lib.csa_xgmi_alloc(n, C.byref(p), h)
-                    if rc:
-                        raise RuntimeError(f"xgmi alloc failed ({rc})")
-                    self._local.append(p.value)
+                    free = _POOL.get((self._dev, n))
+                    if free:
+                        ptr = free.pop()
+                        rc = self.lib.csa_xgmi_reuse(C.c_void_p(ptr), n, h)
+                        if rc:
+                            raise RuntimeError(f"xgmi buffer reuse failed ({rc})")
+                    else:
+                        p = C.c_void_p()
+                        rc = self.lib.csa_xgmi_alloc(n, C.byref(p), h)
+                        if rc:
+                            raise RuntimeError(f"xgmi alloc failed ({rc})")
+                        ptr = p.value
+                    self._local.append(ptr)
+                    self._local_n.append(n)
                     handles.append(h.raw)
             except Exception:
                 handles = None
@@ -170,9 +189,9 @@ class XgmiChannel:
         torch.cuda.synchronize(self.device)
         for p in self._opened:
             self.lib.csa_xgmi_close(p)
-        for p in self._local:
-            self.lib.csa_xgmi_free(p)
-        self._local, self._opened = [], []
+        for p, n in zip(self._local, self._local_n):       # back to the process pool
+            _POOL.setdefault((self._dev, n), []).append(p)
+        self._local, self._local_n, self._opened = [], [], []
 
 
 class XgmiComm:

@@ -4,6 +4,10 @@ import sys
 
 import pytest
 
+# (see parallel/dist.py:init_distributed: RCCL works captured into HIP graphs must not
+# share end events with eager works the process-group watchdog still polls)
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

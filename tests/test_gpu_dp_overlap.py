@@ -31,6 +31,11 @@ def pg():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     yield
+    # the test's engines (and the RCCL works captured into their graphs) die with this
+    # group, before the next test's group starts
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
     dist.destroy_process_group()
 
 
