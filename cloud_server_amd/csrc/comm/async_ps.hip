@@ -92,6 +92,7 @@ __global__ __launch_bounds__(APS_T) void aps_kernel(ApsArgs a) {
       for (int p = 0; p < W; ++p)
         __hip_atomic_store(a.inflag[p] + ((long)slot * W + me) * a.nb + b, (unsigned)(t + 1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // flag lines written back (xgmi.hip)
     }
   }
 
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(APS_T) void aps_kernel(ApsArgs a) {
       __hip_atomic_store(a.outat[me] + par * a.nb + b, at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.outver[me] + par * a.nb + b, (unsigned)(t + 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
   }
 

@@ -82,6 +82,10 @@ __device__ __forceinline__ void xg_publish(const XgArgs& a, long fidx, unsigned 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     for (int p = 0; p < a.world; ++p)
       __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // write the flag lines back too: ranks sharing ONE GPU map each other's buffers as
+    // local memory, where a flag store can stay in this XCD's L2 until the next release
+    // (a waiting peer then never sees it: intermittent timeouts in the one-GPU tests)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
 }
 
@@ -219,6 +223,7 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     for (int p = 0; p < a.world; ++p)
       __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // flag lines written back (xg_publish)
   }
 
   // 2) wait for every source's flag of this chunk (one lane polls all sources, bounded),
