@@ -28,6 +28,7 @@ import os
 import queue
 import threading
 import time
+import weakref
 from collections import OrderedDict, deque
 from concurrent.futures import Future
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
@@ -165,8 +166,19 @@ class _Entry:
         self.batchers = {}
 
 
+_LIVE: "weakref.WeakSet[InferenceService]" = weakref.WeakSet()
+
+
+def close_all() -> None:
+    """Retire every live service's cached models (their HIP graphs and batcher threads) in
+    the calling thread — e.g. before a process goes on to capture graphs of its own."""
+    for svc in list(_LIVE):
+        svc.close()
+
+
 class InferenceService:
     def __init__(self, device: Optional[str] = None, capacity: int = 32, use_hip: bool = True):
+        _LIVE.add(self)
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)

@@ -17,6 +17,24 @@ if ROOT not in sys.path:
 _REAL_ERR = None
 
 
+@pytest.fixture(autouse=True)
+def _gpu_test_cleanup(request):
+    """After a @gpu test: retire the inference services it left (their HIP graphs and
+    batcher threads) and collect its garbage here, so nothing of it is destroyed while a
+    later test captures a graph."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+    import torch
+    if not torch.cuda.is_available():
+        return
+    from cloud_server_amd.serve import inference
+    inference.close_all()
+    gc.collect()
+    torch.cuda.synchronize()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP) device")
     config.addinivalue_line("markers", "slow: long-running test")

@@ -27,6 +27,16 @@ def _cfg(iters, **opts):
     return c
 
 
+def _close(*services) -> None:
+    """Retire the services' cached models (their HIP graphs, batcher threads) NOW, in this
+    thread: a later test's graph capture must never overlap their destruction."""
+    import gc
+    for s in services:
+        s.close()
+    gc.collect()
+    torch.cuda.synchronize()
+
+
 def test_gpu_job_hip_backend_and_inference(tmp_path):
     mdir = str(tmp_path / "m")
     os.makedirs(mdir)
@@ -42,10 +52,13 @@ def test_gpu_job_hip_backend_and_inference(tmp_path):
     cpu = InferenceService(device="cpu")
     test = ds.split(0.9)[1]
     x = test.images[:256].astype(np.float32) / 255.0
-    pg = gpu.predict_arrays(mdir, x)
-    pc = cpu.predict_arrays(mdir, x)
-    assert (pg == pc).mean() > 0.99
-    assert (pg == test.labels[:256]).mean() > 0.9
+    try:
+        pg = gpu.predict_arrays(mdir, x)
+        pc = cpu.predict_arrays(mdir, x)
+        assert (pg == pc).mean() > 0.99
+        assert (pg == test.labels[:256]).mean() > 0.9
+    finally:
+        _close(gpu, cpu)
 
 
 def test_gpu_job_on_reference_fixture(tmp_path):
@@ -60,8 +73,11 @@ def test_gpu_job_on_reference_fixture(tmp_path):
     assert out["state"] == "done" and out["backend"] == "hip"
     ds = load_user_data(os.path.join(mdir, "data"), os.path.join(mdir, "tag.json"))
     svc = InferenceService(device="cuda:0")
-    pred = svc.predict_arrays(mdir, ds.images[:79].astype(np.float32) / 255.0)
-    assert (pred == ds.labels[:79]).mean() > 0.9        # fits its training split
+    try:
+        pred = svc.predict_arrays(mdir, ds.images[:79].astype(np.float32) / 255.0)
+        assert (pred == ds.labels[:79]).mean() > 0.9        # fits its training split
+    finally:
+        _close(svc)
 
 
 def test_job_manager_process_executor_on_gpu(tmp_path):
