@@ -206,8 +206,12 @@ class HipProgram:
         # ps (the parameter-server capability): the same suffix buckets are REDUCE-SCATTERED
         # to their owner shards (GradSync.reduce_scatter_range; xGMI: one launch per bucket,
         # every element leaves its GPU at most once) while the backward continues
-        self.overlap = (e.ctx.enabled and e.sync.strategy in ("allreduce", "ps") and
-                        os.environ.get("CSA_DP_OVERLAP", "1") == "1")
+        # (ps overlaps only on the xGMI range reduce-scatter: on RCCL its per-owner reduces
+        # per bucket measured 0.156 ms/step at world 1 against 0.107 for one reduce-scatter
+        # after the backward — profiles/r4_notes.md)
+        self.overlap = (e.ctx.enabled and
+                        (e.sync.strategy == "allreduce" or (e.sync.strategy == "ps" and e.sync.xgmi is not None))
+                        and os.environ.get("CSA_DP_OVERLAP", "1") == "1")
         self.bucket_at: Dict[object, tuple] = {}
         if not self.overlap:
             return
