@@ -65,13 +65,18 @@ __device__ __forceinline__ bool aps_poll(const unsigned* f, unsigned want, bool 
 }
 
 __global__ __launch_bounds__(APS_T) void aps_kernel(ApsArgs a) {
-  __shared__ int s_abort, s_go, s_c, s_q, s_n, s_par;
+  __shared__ int s_abort, s_go, s_c, s_q, s_n, s_par, s_t;
   const int tid = threadIdx.x, b = blockIdx.x, W = a.world, me = a.rank;
-  if (tid == 0) s_abort = __hip_atomic_load(reinterpret_cast<int*>(a.state + 2), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (tid == 0) {
+    s_abort = __hip_atomic_load(reinterpret_cast<int*>(a.state + 2), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT) != 0;
+    // the clock is advanced by whichever workgroup finished last, on any XCD: one agent-
+    // scope load (never a possibly stale line of this XCD's L2), broadcast through LDS
+    s_t = (int)__hip_atomic_load(a.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   if (s_abort) return;
-  const int t = (int)a.state[0];                       // this rank's clock
+  const int t = s_t;                                   // this rank's clock
   const long c0 = (long)b * a.chunk;
   const long c1 = c0 + a.chunk < a.sh ? c0 + a.chunk : a.sh;
   const unsigned long long t0 = wall_clock64();
@@ -121,12 +126,20 @@ __global__ __launch_bounds__(APS_T) void aps_kernel(ApsArgs a) {
     const float lr = a.opt == OPT_ADAM
                          ? a.lr * sqrtf(1.f - powf(0.999f, (float)n)) / (1.f - powf(0.9f, (float)n))
                          : a.lr;
-    for (long i = c0 + tid; i < c1; i += APS_T) {
-      float wv = w[i], z0 = a.s0 ? a.s0[i] : 0.f, z1 = a.s1 ? a.s1[i] : 0.f;
-      opt_update(a.opt, lr, wv, g[i], z0, z1);
-      w[i] = wv;
-      if (a.s0) a.s0[i] = z0;
-      if (a.s1) a.s1[i] = z1;
+    // float4 over the chunk (chunk and shard are multiples of 4): one 16-byte load of
+    // the uncached inbox per lane instead of four dependent 4-byte round trips
+    for (long i = c0 + 4 * tid; i < c1; i += 4 * APS_T) {
+      float4 wv = *reinterpret_cast<const float4*>(w + i);
+      const float4 gv = *reinterpret_cast<const float4*>(g + i);
+      float4 z0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 z1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      opt_update(a.opt, lr, wv.x, gv.x, z0.x, z1.x);
+      opt_update(a.opt, lr, wv.y, gv.y, z0.y, z1.y);
+      opt_update(a.opt, lr, wv.z, gv.z, z0.z, z1.z);
+      opt_update(a.opt, lr, wv.w, gv.w, z0.w, z1.w);
+      *reinterpret_cast<float4*>(w + i) = wv;
+      if (a.s0) *reinterpret_cast<float4*>(a.s0 + i) = z0;
+      if (a.s1) *reinterpret_cast<float4*>(a.s1 + i) = z1;
     }
     __syncthreads();
     if (tid == 0) {
@@ -205,17 +218,16 @@ __global__ __launch_bounds__(APS_T) void aps_kernel(ApsArgs a) {
     }
     if (t - s_c > worst) worst = t - s_c;
   }
-  if (tid == 0) atomicMax(a.stale, worst);
+  // (the drain launch has no gradient of its own: t - at there is not a staleness)
+  if (tid == 0 && !a.drain) atomicMax(a.stale, worst);
 
-  // ---- the last workgroup advances this rank's clock
+  // ---- the last workgroup advances this rank's clock (agent-scope RMW / release store)
   __syncthreads();
   if (tid == 0 && !a.drain) {
-    __threadfence();
-    const unsigned prev = atomicAdd(a.state + 1, 1u);
+    const unsigned prev = __hip_atomic_fetch_add(a.state + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (unsigned)gridDim.x - 1) {
-      a.state[1] = 0;
-      a.state[0] = (unsigned)(t + 1);
-      __threadfence();
+      __hip_atomic_store(a.state + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.state, (unsigned)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

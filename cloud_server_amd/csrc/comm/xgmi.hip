@@ -59,7 +59,49 @@ struct XgArgs {
   long rs_lo, rs_sh; char* rs_dst;
   unsigned* seq; unsigned* done; int* err;
   unsigned long long timeout_ticks;
+  // per-block record of the last call (nullable), [XG_MAXB][XG_DIAG] u64:
+  //   {epoch, t_start, t_published, t_waited, status (1 ok / 2 timeout), missing source,
+  //    last flag value seen from it, that source's OWN copy of the flag}
+  // wall_clock64 is one device-wide 100 MHz clock, so ranks sharing a GPU (the one-GPU
+  // multi-process tests) can be lined up block by block after a timeout
+  unsigned long long* diag;
 };
+
+constexpr int XG_DIAG = 8;
+
+__device__ __forceinline__ void xg_note(const XgArgs& a, int k, unsigned long long v) {
+  if (a.diag) a.diag[(long)blockIdx.x * XG_DIAG + k] = v;
+}
+
+// The channel epoch of this call: the device counter + 1, read ONCE per block by thread 0
+// at agent scope (a plain load could hit a stale line in this XCD's L2: the counter is
+// advanced by whichever block finished last, on any XCD) and broadcast through LDS.
+__device__ __forceinline__ unsigned xg_epoch(const XgArgs& a, int* s_abort, unsigned* s_e) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = wall_clock64();
+    *s_abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    *s_e = __hip_atomic_load(a.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (a.diag) {
+      unsigned long long* d = a.diag + (long)blockIdx.x * XG_DIAG;
+      d[0] = *s_e; d[1] = t0; d[2] = 0; d[3] = 0; d[4] = 0; d[5] = 0; d[6] = 0; d[7] = 0;
+    }
+  }
+  __syncthreads();
+  return *s_e;
+}
+
+// The last block to finish advances the epoch for the next call on this channel (agent-
+// scope RMW / release store: visible to every XCD's blocks of the next launch).
+__device__ __forceinline__ void xg_finish(const XgArgs& a, unsigned e) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.seq, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // Byte offset of parity half `par` of a receive buffer [2][world][slot + 32]: every
 // protocol (one-shot slots, two-shot phases, range reduce-scatter) stays inside its half.
@@ -86,6 +128,7 @@ __device__ __forceinline__ void xg_publish(const XgArgs& a, long fidx, unsigned 
     // local memory, where a flag store can stay in this XCD's L2 until the next release
     // (a waiting peer then never sees it: intermittent timeouts in the one-GPU tests)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    xg_note(a, 2, wall_clock64());
   }
 }
 
@@ -96,16 +139,29 @@ __device__ __forceinline__ bool xg_wait(const XgArgs& a, long fidx, unsigned e, 
     const unsigned* f = a.flags[a.rank] + fidx;
     const unsigned long long t0 = wall_clock64();
     for (int r = 0; r < a.world && !*s_abort; ++r) {
-      while (__hip_atomic_load(f + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      unsigned v;
+      while ((v = __hip_atomic_load(f + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != e) {
         if (wall_clock64() - t0 > a.timeout_ticks) {
           __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           *s_abort = 1;
+          // the failure record: who never arrived, what was seen, and what the missing
+          // source's OWN copy of that flag says (it publishes to itself too): e there but
+          // not here = a lost store; not there either = that block never published
+          if (a.diag) {
+            unsigned long long* d = a.diag + (long)blockIdx.x * XG_DIAG;
+            d[3] = wall_clock64(); d[4] = 2; d[5] = (unsigned long long)r; d[6] = v;
+            d[7] = __hip_atomic_load(a.flags[r] + fidx + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (!*s_abort && a.diag) {
+      unsigned long long* d = a.diag + (long)blockIdx.x * XG_DIAG;
+      d[3] = wall_clock64(); d[4] = 1;
+    }
   }
   __syncthreads();
   return !*s_abort;
@@ -189,11 +245,10 @@ __device__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
 
 __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   __shared__ int s_abort;
+  __shared__ unsigned s_e;
   const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
-  if (t == 0) s_abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  __syncthreads();
+  const unsigned e = xg_epoch(a, &s_abort, &s_e);
   if (s_abort) return;
-  const unsigned e = *a.seq + 1u;
   const int par = e & 1u;
   if (a.op == 2) {
     xg_twoshot(a, e, &s_abort);
@@ -214,37 +269,12 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
     for (int p = 0; p < XG_MAXR; ++p)
       if (p < a.world) *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
   }
-  // publish: every wave drains its stores, the barrier, then ONE system-scope release
-  // (one L2 write-back per block, not per wave) before this block's flags go out
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
+  // publish (every wave drains its stores, the barrier, ONE system-scope release per
+  // block, the flags), then wait for every source's flag of this chunk (one lane polls,
+  // bounded) and ONE system-scope acquire for the block (the vector L1 is per CU)
   const long fidx = ((long)par * XG_MAXB + b) * XG_MAXR;
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    for (int p = 0; p < a.world; ++p)
-      __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // flag lines written back (xg_publish)
-  }
-
-  // 2) wait for every source's flag of this chunk (one lane polls all sources, bounded),
-  // then ONE system-scope acquire for the block (the vector L1 is per CU)
-  if (t == 0) {
-    const unsigned* f = a.flags[a.rank] + fidx;
-    const unsigned long long t0 = wall_clock64();
-    for (int r = 0; r < a.world; ++r) {
-      while (__hip_atomic_load(f + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-        if (wall_clock64() - t0 > a.timeout_ticks) {
-          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_abort = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (s_abort) break;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  }
-  __syncthreads();
+  xg_publish(a, fidx, e);
+  xg_wait(a, fidx, e, &s_abort);
 
   // 3) consume from local memory
   if (!s_abort) {
@@ -275,18 +305,8 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
     }
   }
   }
-
   // 4) the last block to finish advances the epoch for the next call on this channel
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    const unsigned prev = atomicAdd(a.done, 1u);
-    if (prev == (unsigned)nb - 1) {
-      *a.done = 0;
-      *a.seq = e;
-      __threadfence();
-    }
-  }
+  xg_finish(a, e);
 }
 
 // op 3: reduce-scatter of a range with GLOBAL ownership (its own kernel: the extra code
@@ -297,11 +317,10 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
 // every rank, the owner sums its units of the range in fixed rank order.
 __global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs a) {
   __shared__ int s_abort;
+  __shared__ unsigned s_e;
   const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
-  if (t == 0) s_abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  __syncthreads();
+  const unsigned e = xg_epoch(a, &s_abort, &s_e);
   if (s_abort) return;
-  const unsigned e = *a.seq + 1u;
   const int par = e & 1u;
   const long units = a.msg_bytes >> 4;
   const long per = (units + nb - 1) / nb;
@@ -330,16 +349,7 @@ __global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs a) {
       *reinterpret_cast<float4*>(a.rs_dst + ((u - own_lo) << 4)) = acc;
     }
   }
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    const unsigned prev = atomicAdd(a.done, 1u);
-    if (prev == (unsigned)nb - 1) {
-      *a.done = 0;
-      *a.seq = e;
-      __threadfence();
-    }
-  }
+  xg_finish(a, e);
 }
 
 }  // namespace csa
@@ -373,6 +383,7 @@ CSA_API int csa_xgmi_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 CSA_API int csa_xgmi_free(void* ptr) { return (int)hipFree(ptr); }
 CSA_API int csa_xgmi_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 CSA_API int csa_xgmi_max_blocks() { return XG_MAXB; }
+CSA_API int csa_xgmi_diag_words() { return XG_DIAG; }
 
 // op 0 = all-gather (dst[r] = src of rank r, rank-major per segment), 1 = fp32 sum all-reduce
 // (src == dst allowed).  Segments are packed back to back into one per-rank message of
@@ -380,7 +391,7 @@ CSA_API int csa_xgmi_max_blocks() { return XG_MAXB; }
 // state = 3 x uint32 on the device: {seq, done, err}.
 CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* const* bufs, void* const* flags,
                          int nseg, void* const* srcs, void* const* dsts, const long* seg_bytes,
-                         unsigned* state, double timeout_s, int nblocks, hipStream_t st) {
+                         unsigned* state, double timeout_s, int nblocks, void* diag, hipStream_t st) {
   if (world < 1 || world > XG_MAXR || rank < 0 || rank >= world || nseg < 1 || nseg > XG_MAXSEG) return -1;
   XgArgs a{};
   a.op = op; a.rank = rank; a.world = world; a.nseg = nseg; a.slot_bytes = slot_bytes;
@@ -402,6 +413,7 @@ CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* con
   }
   a.seq = state; a.done = state + 1; a.err = reinterpret_cast<int*>(state + 2);
   a.timeout_ticks = (unsigned long long)(timeout_s * 1.0e8);   // wall_clock64: 100 MHz
+  a.diag = static_cast<unsigned long long*>(diag);
   const long units = off >> 4;
   // ~8 KB per block: measured 9.6 us vs 16.9 (32 KB) / 52.5 (128 KB) for the 0.9 MB
   // lowrank gather (profiles/r1s4_xgmi_collectives.md)
@@ -418,7 +430,7 @@ CSA_API int csa_xgmi_run(int op, int rank, int world, long slot_bytes, void* con
 // backward produces it (the "ps" strategy: construct_distribute.py:355-357, 413).
 CSA_API int csa_xgmi_reduce_scatter(int rank, int world, long slot_bytes, void* const* bufs, void* const* flags,
                                     const void* src, long lo, long bytes, long shard_bytes, void* dst_shard,
-                                    unsigned* state, double timeout_s, int nblocks, hipStream_t st) {
+                                    unsigned* state, double timeout_s, int nblocks, void* diag, hipStream_t st) {
   if (world < 1 || world > XG_MAXR || rank < 0 || rank >= world) return -1;
   if ((lo & 15) || bytes <= 0 || (bytes & 15) || (shard_bytes & 15) || shard_bytes <= 0) return -2;
   if (((uintptr_t)src & 15) || ((uintptr_t)dst_shard & 15)) return -2;
@@ -435,6 +447,7 @@ CSA_API int csa_xgmi_reduce_scatter(int rank, int world, long slot_bytes, void* 
   }
   a.seq = state; a.done = state + 1; a.err = reinterpret_cast<int*>(state + 2);
   a.timeout_ticks = (unsigned long long)(timeout_s * 1.0e8);
+  a.diag = static_cast<unsigned long long*>(diag);
   const long units = bytes >> 4;
   int nb = nblocks > 0 ? nblocks : (int)((units + 511) / 512);
   nb = nb < 1 ? 1 : (nb > XG_MAXB ? XG_MAXB : nb);

@@ -71,9 +71,21 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
     hipcc = _hipcc()
     objs = [os.path.join(LIBDIR, "obj", os.path.basename(s) + ".o") for s in srcs]
+
+    def compile_one(so) -> None:
+        # per-object stamp: the source, every header (any may be included) and the flags,
+        # so editing one kernel file recompiles that object only
+        src, obj = so
+        ostamp = _hash([src] + hdrs, " ".join(flags))
+        sf = obj + ".stamp"
+        if not force and os.path.exists(obj) and os.path.exists(sf) and open(sf).read().strip() == ostamp:
+            return
+        _run([hipcc, *flags, "-c", src, "-o", obj], verbose)
+        with open(sf, "w") as f:
+            f.write(ostamp)
+
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        list(ex.map(lambda so: _run([hipcc, *flags, "-c", so[0], "-o", so[1]], verbose),
-                    zip(srcs, objs)))
+        list(ex.map(compile_one, zip(srcs, objs)))
     tmp = KERNEL_LIB + ".tmp"
     _run([hipcc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp], verbose)
     os.replace(tmp, KERNEL_LIB)

@@ -21,10 +21,14 @@ One step of rank r at clock t:
 4. **pull**   — every owner's latest published shard into its local copy, waiting only
    until each owner's applied-through clock is >= t - 2s.
 
-So no rank runs more than ``s`` steps ahead of another, and every gradient is computed on
-parameters that contain all pushes older than 2s + 1 clocks: staleness is bounded (and
-measured: ``max_staleness``), never zero-by-barrier.  s = 0 is lockstep (each rank's push
-still applied separately).  At the end ``finish()`` drains: every owner applies every push
+So no rank runs more than ``s`` steps ahead of another.  The staleness of a step is its
+clock minus the applied-through clock of the parameters it pulled (the oldest of its own
+shard's and every pulled shard's): the own shard holds every push through t - s and every
+pulled shard every push through t - 2s, so **max_staleness <= 2s** — the one bound the
+docstring, the kernel's measurement (``async_ps.hip``) and the tests all state.  (The
+gradient of the NEXT clock, t + 1, is computed on those parameters.)  s = 0 is lockstep
+(each rank's push still applied separately).  Staleness is bounded and measured, never
+zero-by-barrier.  At the end ``finish()`` drains: every owner applies every push
 and every rank pulls the final shards, so replicas agree.
 
 Two transports implement the protocol:
@@ -43,7 +47,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import optim_ref
-from .xgmi import _line_up
+from .xgmi import _line_up, max_blocks_from_env, pool_get, pool_put
 
 GRAD, PARAM = 0, 1
 
@@ -196,23 +200,28 @@ class AsyncPSDevice:
         self.r, self.W, self.sh, self.s = rank, world, shard, staleness
         self.opt_id, self.lr, self.device = opt_id, lr, device
         self.R = 2 * staleness + 2
+        # every workgroup of a step waits on its peers' (bounded): CSA_XGMI_BLOCKS caps them
+        # so ranks sharing one GPU keep all their workgroups resident (parallel/xgmi.py)
         self.nb = max(1, min(256, (shard + 4095) // 4096))
+        cap = max_blocks_from_env()
+        if cap:
+            self.nb = max(1, min(self.nb, cap))
         self.timeout_s = timeout_s if timeout_s is not None else float(os.environ.get("CSA_XGMI_TIMEOUT_S", "20"))
         sizes = [self.R * world * shard * 4, self.R * world * self.nb * 4, 2 * shard * 4, 2 * self.nb * 4,
                  2 * self.nb * 4]
         hb = self.lib.csa_xgmi_handle_bytes()
+        self._dev = device.index if device.index is not None else torch.cuda.current_device()
         self._local: List[int] = []
+        self._local_n: List[int] = []
         self._opened: List[int] = []
         handles: Optional[List[bytes]] = []
         with torch.cuda.device(device):
             try:
                 for n in sizes:
-                    p = C.c_void_p()
-                    h = C.create_string_buffer(hb)
-                    if self.lib.csa_xgmi_alloc(n, C.byref(p), h):
-                        raise RuntimeError("async_ps alloc failed")
-                    self._local.append(p.value)
-                    handles.append(h.raw)
+                    ptr, h = pool_get(self.lib, self._dev, n)      # recycled, never hipFree'd
+                    self._local.append(ptr)
+                    self._local_n.append(n)
+                    handles.append(h)
             except Exception:
                 handles = None
             allh: List[Optional[List[bytes]]] = [None] * world
@@ -261,7 +270,6 @@ class AsyncPSDevice:
             _line_up(self.group, self.device)
 
     def _launch(self, flat_grad, flat, slots, drain: int) -> None:
-        lo = self.r * self.sh
         s0 = slots[0, :] if slots.shape[0] > 0 else None
         s1 = slots[1, :] if slots.shape[0] > 1 else None
         rc = self.lib.csa_aps_step(
@@ -269,7 +277,6 @@ class AsyncPSDevice:
             None if s0 is None else s0.data_ptr(), None if s1 is None else s1.data_ptr(), self.opt_id,
             float(self.lr), self.prog.data_ptr(), self.stale.data_ptr(), self.state.data_ptr(), drain,
             self.timeout_s, torch.cuda.current_stream(self.device).cuda_stream)
-        del lo
         if rc:
             raise RuntimeError(f"async_ps step launch failed ({rc})")
 
@@ -279,7 +286,7 @@ class AsyncPSDevice:
     def finish(self, flat: torch.Tensor, slots: torch.Tensor) -> None:
         self._launch(flat, flat, slots, 1)             # (the gradient is not read when draining)
         torch.cuda.synchronize(self.device)
-        self.check()
+        # (no local raise: TrainEngine.finish_async agrees on the error across ranks)
 
     def error(self) -> int:
         return int(self.state[2].item())
@@ -294,7 +301,8 @@ class AsyncPSDevice:
 
     @property
     def applied(self) -> int:
-        return int(self.prog[2].item())
+        """Pushes applied to EVERY chunk of this owner's shard (the slowest workgroup's count)."""
+        return int(self.prog.view(-1, 3)[:, 2].min().item())
 
     @property
     def t(self) -> int:
@@ -309,9 +317,9 @@ class AsyncPSDevice:
             _line_up(self.group, self.device)
         for p in self._opened:
             self.lib.csa_xgmi_close(p)
-        for p in self._local:
-            self.lib.csa_xgmi_free(p)
-        self._local, self._opened = [], []
+        for p, n in zip(self._local, self._local_n):       # back to the process pool
+            pool_put(self._dev, p, n)
+        self._local, self._local_n, self._opened = [], [], []
 
 
 def make_async_ps(eng, lo: int, hi: int):

@@ -36,6 +36,23 @@ class DistContext:
         return self.rank == 0   # reference: is_chief = task_index == 0 (:385)
 
 
+def rccl_env_defaults() -> None:
+    """Environment an RCCL process group of this package is created with (set before
+    ``init_process_group``; explicit user settings win):
+
+    * ``TORCH_NCCL_CUDA_EVENT_CACHE=0`` — RCCL collectives are captured into the step's HIP
+      graphs; with the process-wide event cache a work's end event can be one last
+      recorded inside a capture, which the watchdog may not query (hipErrorCapturedEvent);
+    * ``NCCL_RUNTIME_CONNECT=0`` — every connection set up when a communicator is created,
+      so the first collective of the dedicated capture group
+      (``GradSync._setup_capture_group``) may be one inside a capture;
+    * ``TORCH_NCCL_TRACE_BUFFER_SIZE`` — the flight recorder, whose active list tells when
+      the watchdog has retired that group's one eager collective (``dp.wait_retired``)."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
+    os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")
+
+
 def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
@@ -60,10 +77,7 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 300.0) -> Dis
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = device
-            # RCCL collectives are captured into the step's HIP graphs; with the process-wide
-            # CUDA-event cache a work's end event can be one last recorded inside a capture,
-            # which the watchdog thread may not query (hipErrorCapturedEvent aborts the rank)
-            os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+            rccl_env_defaults()
         dist.init_process_group(**kw)
     return DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
 

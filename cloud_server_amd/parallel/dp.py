@@ -43,6 +43,54 @@ from ..utils.graphs import capture
 DEFAULT_BUCKET_BYTES = 32 << 20   # one bucket covers the sample model's 9.1 MB gradient
 
 
+def wait_retired(group, timeout_s: float = 10.0) -> Optional[bool]:
+    """Block until the process-group watchdog has retired every eager collective of
+    ``group`` (none left in the flight recorder's active list).  True once retired, False
+    on timeout, None where the flight recorder is off (TORCH_NCCL_TRACE_BUFFER_SIZE=0)."""
+    import json
+    import time
+    try:
+        from torch._C._distributed_c10d import _dump_nccl_trace_json
+    except ImportError:  # pragma: no cover
+        return None
+    if int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) <= 0:
+        return None
+    name = dist.distributed_c10d._get_process_group_name(group)
+    t0 = time.perf_counter()
+    while True:
+        try:
+            dump = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
+        except Exception:  # pragma: no cover - dump format / availability
+            return None
+        active = [e for e in dump.get("entries", []) if name in json.dumps(e.get("process_group", ""))]
+        if not active:
+            return True
+        if time.perf_counter() - t0 > timeout_s:
+            return False
+        time.sleep(0.005)
+
+
+_CAP: list = []        # [(default group, capture group, retired)] of this process
+
+
+def capture_group(device: torch.device):
+    """The process's dedicated capture group over all ranks (``GradSync._setup_capture_
+    group``), created collectively on first use per default group — every GradSync (each
+    engine, the strategy tuner's trial engines) shares it — with its connection check
+    retired by the watchdog before any capture uses it.  Returns (group, retired)."""
+    default = dist.distributed_c10d._get_default_group()
+    if _CAP and _CAP[0][0] is default:
+        return _CAP[0][1], _CAP[0][2]
+    g = dist.new_group(backend="nccl", device_id=device)
+    t = torch.ones(1, device=device)
+    dist.all_reduce(t, group=g)
+    if int(t.item()) != dist.get_world_size():
+        raise RuntimeError("capture process group: connection check failed")
+    retired = wait_retired(g)
+    _CAP[:] = [(default, g, retired)]
+    return g, retired
+
+
 class GradSync:
     def __init__(self, ctx: DistContext, numel: int, strategy: str = "allreduce",
                  bucket_bytes: int = DEFAULT_BUCKET_BYTES):
@@ -63,12 +111,47 @@ class GradSync:
         self.xgmi_tuning: dict = {}      # tag -> {"bytes", "xgmi_us", "rccl_us"} (auto mode)
         self._choice: dict = {}
         self.timing: Optional[list] = None   # set by TrainEngine.probe: (start, end) events per call
+        # further poisoned-transport probes (the async_ps device state): () -> nonzero on error
+        self.extra_errors: List = []
         # CSA_DETERMINISTIC=1: every SUM is formed in a fixed rank order — the
         # xGMI kernels (one-/two-shot, range reduce-scatter: fixed-order by construction),
         # or, where they do not apply, an exact all-gather followed by a rank-ordered fold.
         # Bitwise-repeatable and identical on every rank; never RCCL's reductions.
         self.det = os.environ.get("CSA_DETERMINISTIC", "0") == "1"
+        self.cap_group = None
+        self._setup_capture_group()
         self._setup_xgmi()
+
+    # ---- RCCL: captured collectives on their own communicator ----
+    def _setup_capture_group(self) -> None:
+        """RCCL collectives captured into HIP graphs run on a DEDICATED process group.
+
+        The process-group watchdog polls the end event of every EAGER collective until it
+        reaps it; a capture that contains a collective pulls that group's internal RCCL
+        stream into the capture, and querying an event recorded on a stream that is
+        capturing aborts the process (hipErrorCapturedEvent — round 4's intermittent
+        suite abort, profiles/r4_notes.md).  So eager collectives (warm-up steps, the
+        tuner's warm-up, agreement flags) stay on the default group and every collective
+        issued while capturing goes to ``cap_group`` (``_pg``), whose stream therefore never
+        carries an eager event the watchdog is still polling.  The group's communicator is
+        connected eagerly (``device_id``; ``NCCL_RUNTIME_CONNECT=0`` from
+        ``init_distributed`` sets every connection up at creation), and its ONE eager
+        collective — a connection check — is waited on until the watchdog has RETIRED it
+        (the flight recorder's active list, an observable condition, not a timed sleep)."""
+        if not (self.ctx.enabled and self.ctx.backend == "nccl" and dist.is_available() and dist.is_initialized()):
+            return
+        if dist.get_backend() != "nccl":
+            return                   # (the one-GPU multi-process tests: a gloo group, no RCCL)
+        if os.environ.get("CSA_CAPTURE_GROUP", "1") != "1":
+            return
+        self.cap_group, self.cap_group_retired = capture_group(self.ctx.device)
+
+    def _pg(self):
+        """The process group of a data-plane collective issued now: the capture group while
+        the current stream is capturing, else the default group."""
+        if self.cap_group is not None and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return self.cap_group
+        return None
 
     @contextlib.contextmanager
     def _timed(self):
@@ -121,10 +204,13 @@ class GradSync:
         bad = 0
         if self.xgmi is not None:
             bad = int(any(ch.error() for ch in self.xgmi.channels.values()))
+        if any(f() for f in self.extra_errors):
+            bad = 1
         flag = torch.tensor([bad], dtype=torch.int32, device=self.ctx.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
         if flag.item():
-            raise RuntimeError("xGMI collective timed out waiting for a peer on some rank (channel poisoned)")
+            raise RuntimeError("peer-buffer transport timed out waiting for a peer on some rank "
+                               "(xGMI channel / async_ps state poisoned)")
 
     def _xg_channel(self, tag: str, srcs, dsts=None) -> Optional["_xg.XgmiChannel"]:
         """The xGMI channel for call site ``tag``, or None for RCCL.  Decided once per tag,
@@ -177,7 +263,6 @@ class GradSync:
     def _time_paths(self, ch, srcs, dsts) -> Dict[str, float]:
         """µs per call of each candidate (max over ranks): all-reduce sites time the
         one-shot and two-shot xGMI protocols and RCCL; gather sites xGMI and RCCL."""
-        dev = self.ctx.device
         ss = [torch.zeros_like(t) for t in srcs]
         sd = None if dsts is None else [torch.empty_like(d) for d in dsts]
 
@@ -193,13 +278,19 @@ class GradSync:
         def rc():
             for i, t in enumerate(ss):
                 if sd is None:
-                    dist.all_reduce(t)
+                    dist.all_reduce(t, group=self._pg())
                 else:
-                    dist.all_gather_into_tensor(sd[i], t)
+                    dist.all_gather_into_tensor(sd[i], t, group=self._pg())
 
         cands = {"oneshot" if sd is None else "xgmi": one, "rccl": rc}
         if sd is None and self.ctx.world > 2:
             cands["twoshot"] = two
+        return self._time_fns(cands)
+
+    def _time_fns(self, cands) -> Dict[str, float]:
+        """µs per call of each candidate callable (max over ranks): an eager warm-up (RCCL
+        communicator paths), then a HIP graph of 10 calls replayed 3 times."""
+        dev = self.ctx.device
         out = []
         for fn in cands.values():
             side = torch.cuda.Stream(dev)
@@ -260,13 +351,13 @@ class GradSync:
                 elif self.det:
                     self._det_sum(flat_grad[a:b])
                 else:
-                    dist.all_reduce(flat_grad[a:b])
+                    dist.all_reduce(flat_grad[a:b], group=self._pg())
 
     # ---- deterministic fallback (no xGMI channel) ----
     def _det_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape]: every rank's copy of ``t`` (exact: an all-gather moves bits)."""
         out = torch.empty((self.ctx.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
+        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self._pg())
         return out
 
     def _det_sum(self, t: torch.Tensor) -> None:
@@ -282,30 +373,86 @@ class GradSync:
         if not self.ctx.enabled:
             shard_out.copy_(flat_grad)
             return
-        if self.det:
+        if self.det or self.xgmi is not None:
+            # one range covering the buffer: the xGMI range kernel where it was measured
+            # faster (or deterministic mode), else RCCL's reduce-scatter
             self.reduce_scatter_range(flat_grad, shard_out, 0, self.numel)
             return
         with self._timed():
-            dist.reduce_scatter_tensor(shard_out, flat_grad)
+            dist.reduce_scatter_tensor(shard_out, flat_grad, group=self._pg())
+
+    def rs_choice(self, flat_grad: torch.Tensor, shard_out: torch.Tensor, lo: int, hi: int):
+        """The path of the [lo, hi) range reduce-scatter, decided once per range and
+        collectively: the xGMI range kernel if the range fits its alignment rules and —
+        under ``CSA_XGMI=auto`` — it measured faster than RCCL on scratch copies (each as
+        a HIP graph of 10 calls, recorded under ``xgmi_tuning['rs:lo:hi']``); else None
+        (RCCL).  ``CSA_XGMI=1`` and deterministic mode take xGMI whenever it fits."""
+        tag = f"rs:{lo}:{hi}"
+        if tag in self._choice:
+            return self._choice[tag]
+        if self.xgmi is None:
+            return None
+        if torch.cuda.is_current_stream_capturing():
+            if self.det:
+                raise RuntimeError(f"deterministic collective {tag!r} first used inside graph capture")
+            return None
+        sh = self.shard
+        ok = lo % 4 == 0 and hi % 4 == 0 and sh % 4 == 0 and flat_grad.data_ptr() % 16 == 0 \
+            and shard_out.data_ptr() % 16 == 0
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ch = self.xgmi.channel(tag, (hi - lo) * 4) if flag.item() else None
+        if ch is not None and self.xgmi_mode == "auto" and not self.det:
+            sf, so = torch.zeros_like(flat_grad), torch.zeros_like(shard_out)
+            times = self._time_fns({"xgmi": lambda: ch.reduce_scatter_range(sf, lo, hi, sh, so),
+                                    "rccl": lambda: self._rs_rccl(sf, so, lo, hi)})
+            self.xgmi_tuning[tag] = {"bytes": (hi - lo) * 4, "xgmi_us": round(times["xgmi"], 2),
+                                     "rccl_us": round(times["rccl"], 2)}
+            healthy = torch.tensor([0 if ch.error() else 1], dtype=torch.int32, device=self.ctx.device)
+            dist.all_reduce(healthy, op=dist.ReduceOp.MIN)
+            if not healthy.item():
+                self.xgmi_tuning[tag]["error"] = "peer wait timed out"
+                ch.close()
+                del self.xgmi.channels[tag]
+                ch = None
+            elif not times["xgmi"] < times["rccl"]:
+                ch = None
+        self._choice[tag] = ch
+        return ch
+
+    def _rs_rccl(self, flat_grad: torch.Tensor, shard_out: torch.Tensor, lo: int, hi: int) -> None:
+        """RCCL form of the range reduce-scatter: the whole buffer is one reduce-scatter,
+        a partial range one reduce per owner portion."""
+        sh, W, r = self.shard, self.ctx.world, self.ctx.rank
+        if lo == 0 and hi == self.numel and self.ctx.backend != "gloo":
+            dist.reduce_scatter_tensor(shard_out, flat_grad, group=self._pg())
+            return
+        for p in range(W):
+            a, b = max(lo, p * sh), min(hi, (p + 1) * sh)
+            if a >= b:
+                continue
+            part = flat_grad[a:b]
+            if self.ctx.backend == "gloo":
+                buf = part.clone()
+                dist.reduce(buf, dst=p, group=self._pg())
+                if p == r:
+                    shard_out[a - r * sh:b - r * sh].copy_(buf)
+            else:
+                dist.reduce(part, dst=p, group=self._pg())
+                if p == r:
+                    shard_out[a - r * sh:b - r * sh].copy_(part)
 
     def reduce_scatter_range(self, flat_grad: torch.Tensor, shard_out: torch.Tensor, lo: int, hi: int) -> None:
         """The [lo, hi) part of ``reduce_scatter``: every element is summed into its owner's
         shard (owner = index // shard).  Issued per gradient bucket as the backward produces
         it (the HIP program's overlapped ps step); once every bucket covering the buffer has
-        run, ``shard_out`` equals ``reduce_scatter``'s.  xGMI: one launch, each element
-        leaves its GPU at most once; otherwise one RCCL reduce per owner portion."""
+        run, ``shard_out`` equals ``reduce_scatter``'s.  xGMI (where ``rs_choice`` picked
+        it): one launch, each element leaves its GPU at most once; otherwise RCCL."""
         if not self.ctx.enabled:
             shard_out[lo:hi].copy_(flat_grad[lo:hi])
             return
-        sh, W, r = self.shard, self.ctx.world, self.ctx.rank
-        ch = None
-        if self.xgmi is not None and not torch.cuda.is_current_stream_capturing() and f"rs:{lo}:{hi}" not in self._choice:
-            ok = lo % 4 == 0 and hi % 4 == 0 and sh % 4 == 0 and flat_grad.data_ptr() % 16 == 0 \
-                and shard_out.data_ptr() % 16 == 0
-            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            self._choice[f"rs:{lo}:{hi}"] = self.xgmi.channel(f"rs:{lo}:{hi}", (hi - lo) * 4) if flag.item() else None
-        ch = self._choice.get(f"rs:{lo}:{hi}")
+        sh, r = self.shard, self.ctx.rank
+        ch = self.rs_choice(flat_grad, shard_out, lo, hi)
         with self._timed():
             if ch is not None:
                 ch.reduce_scatter_range(flat_grad, lo, hi, sh, shard_out)
@@ -317,20 +464,7 @@ class GradSync:
                 if a < b:
                     shard_out[a - r * sh:b - r * sh].copy_(part[a - lo:b - lo])
                 return
-            for p in range(W):
-                a, b = max(lo, p * sh), min(hi, (p + 1) * sh)
-                if a >= b:
-                    continue
-                part = flat_grad[a:b]
-                if self.ctx.backend == "gloo":
-                    buf = part.clone()
-                    dist.reduce(buf, dst=p)
-                    if p == r:
-                        shard_out[a - r * sh:b - r * sh].copy_(buf)
-                else:
-                    dist.reduce(part, dst=p)
-                    if p == r:
-                        shard_out[a - r * sh:b - r * sh].copy_(part)
+            self._rs_rccl(flat_grad, shard_out, lo, hi)
 
     def all_gather_params(self, flat_param: torch.Tensor) -> None:
         """Every owner's updated shard to every rank (xGMI: one push of the shard to the 7
@@ -346,7 +480,7 @@ class GradSync:
                 ch.all_gather([(flat_param[lo:hi], flat_param)])
                 return
             dist.all_gather_into_tensor(flat_param, flat_param[lo:hi].clone()
-                                        if self.ctx.backend == "gloo" else flat_param[lo:hi])
+                                        if self.ctx.backend == "gloo" else flat_param[lo:hi], group=self._pg())
 
     # ---- lowrank ----
     def all_gather_rows(self, local: torch.Tensor, out: torch.Tensor) -> None:
@@ -354,7 +488,7 @@ class GradSync:
         if not self.ctx.enabled:
             out.copy_(local)
             return
-        dist.all_gather_into_tensor(out, local.contiguous())
+        dist.all_gather_into_tensor(out, local.contiguous(), group=self._pg())
 
     def all_gather_rows_many(self, pairs, tag: str = "gather") -> None:
         """Several ``all_gather_rows`` issued as ONE launch where the xGMI peer-buffer kernel
@@ -370,7 +504,7 @@ class GradSync:
                 ch.all_gather(pairs)
                 return
             for local, out in pairs:
-                dist.all_gather_into_tensor(out, local.contiguous())
+                dist.all_gather_into_tensor(out, local.contiguous(), group=self._pg())
 
     def allreduce_ranges(self, flat: torch.Tensor, ranges, tag: str = "ranges") -> None:
         """Sum-all-reduce the given [lo, hi) slices of ``flat`` (one launch on the xGMI
@@ -386,7 +520,7 @@ class GradSync:
                 if self.det:
                     self._det_sum(flat[lo:hi])
                 else:
-                    dist.all_reduce(flat[lo:hi])
+                    dist.all_reduce(flat[lo:hi], group=self._pg())
 
     def allreduce_tensors(self, tensors, tag: str) -> None:
         """In-place SUM of small fp32 tensors across ranks (SyncBN statistics slabs)."""
@@ -401,7 +535,7 @@ class GradSync:
                 if self.det:
                     self._det_sum(t)
                 else:
-                    dist.all_reduce(t)
+                    dist.all_reduce(t, group=self._pg())
 
     def broadcast_params(self, flat_param: torch.Tensor) -> None:
         """Initial sync from rank 0 (reference: chief runs init_op, construct_distribute.py:379)."""

@@ -57,6 +57,29 @@ def _aligned(t: torch.Tensor) -> bool:
 _POOL: Dict[Tuple[int, int], List[int]] = {}
 
 
+def pool_get(lib, dev: int, nbytes: int) -> Tuple[int, bytes]:
+    """A zeroed uncached peer buffer of ``nbytes`` on device ``dev`` (from the process pool
+    when one is free) and its freshly exported IPC handle."""
+    h = C.create_string_buffer(lib.csa_xgmi_handle_bytes())
+    free = _POOL.get((dev, nbytes))
+    if free:
+        ptr = free.pop()
+        rc = lib.csa_xgmi_reuse(C.c_void_p(ptr), nbytes, h)
+        if rc:
+            raise RuntimeError(f"xgmi buffer reuse failed ({rc})")
+        return ptr, h.raw
+    p = C.c_void_p()
+    rc = lib.csa_xgmi_alloc(nbytes, C.byref(p), h)
+    if rc:
+        raise RuntimeError(f"xgmi alloc failed ({rc})")
+    return p.value, h.raw
+
+
+def pool_put(dev: int, ptr: int, nbytes: int) -> None:
+    """Back to the process pool (never hipFree'd while a peer may still map it)."""
+    _POOL.setdefault((dev, nbytes), []).append(ptr)
+
+
 class XgmiChannel:
     def __init__(self, rank: int, world: int, slot_bytes: int, device: torch.device,
                  group=None, timeout_s: float = 20.0):
@@ -80,22 +103,10 @@ class XgmiChannel:
         with torch.cuda.device(device):
             try:
                 for n in sizes:
-                    h = C.create_string_buffer(hb)
-                    free = _POOL.get((self._dev, n))
-                    if free:
-                        ptr = free.pop()
-                        rc = self.lib.csa_xgmi_reuse(C.c_void_p(ptr), n, h)
-                        if rc:
-                            raise RuntimeError(f"xgmi buffer reuse failed ({rc})")
-                    else:
-                        p = C.c_void_p()
-                        rc = self.lib.csa_xgmi_alloc(n, C.byref(p), h)
-                        if rc:
-                            raise RuntimeError(f"xgmi alloc failed ({rc})")
-                        ptr = p.value
+                    ptr, h = pool_get(self.lib, self._dev, n)
                     self._local.append(ptr)
                     self._local_n.append(n)
-                    handles.append(h.raw)
+                    handles.append(h)
             except Exception:
                 handles = None
             allh: List[Optional[List[bytes]]] = [None] * world
@@ -127,20 +138,36 @@ class XgmiChannel:
         self._bufs = (C.c_void_p * world)(*ptrs[0])
         self._flags = (C.c_void_p * world)(*ptrs[1])
         self.state = torch.zeros(4, dtype=torch.int32, device=device)   # seq, done, err, pad
+        # per-block record of the last call (csrc/comm/xgmi.hip XgArgs::diag), read by
+        # ``diag()`` after a timeout
+        self._dw = self.lib.csa_xgmi_diag_words()
+        self.diag_buf = torch.zeros(nblk * self._dw, dtype=torch.int64, device=device)
         # workgroups per call (0: one per ~8 KB of the per-rank message, at most 256)
         self.nblocks = 0
+        # upper bound on workgroups per call (CSA_XGMI_BLOCKS; 0 = none).  Every block of a
+        # call waits on its peers' blocks, so all ranks' blocks of a call must be resident
+        # at once: ranks that share ONE GPU (the one-GPU multi-process tests) split its
+        # ~1280 slots for 256-thread blocks between them; on a node each rank owns a GPU
+        self.max_blocks = max_blocks_from_env()
         # all-reduce protocol: None = by size (TWO_SHOT_MIN_BYTES); the tuner pins it
         self.protocol: Optional[str] = None
 
     # ---------------------------------------------------------------- calls
+    def blocks_for(self, nbytes: int) -> int:
+        """Workgroups of a call moving ``nbytes`` per rank (0 = the kernel's own choice)."""
+        nb = self.nblocks
+        if self.max_blocks > 0:
+            nb = min(nb if nb > 0 else max(1, (nbytes // 16 + 511) // 512), self.max_blocks)
+        return nb
+
     def _run(self, op: int, srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
         n = len(srcs)
         sb = [s.numel() * s.element_size() for s in srcs]
         rc = self.lib.csa_xgmi_run(
             op, self.rank, self.world, self.slot_bytes, self._bufs, self._flags, n,
             (C.c_void_p * n)(*[s.data_ptr() for s in srcs]), (C.c_void_p * n)(*[d.data_ptr() for d in dsts]),
-            (C.c_long * n)(*sb), self.state.data_ptr(), self.timeout_s, self.nblocks,
-            torch.cuda.current_stream(self.device).cuda_stream)
+            (C.c_long * n)(*sb), self.state.data_ptr(), self.timeout_s, self.blocks_for(sum(sb)),
+            self.diag_buf.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
         if rc:
             raise RuntimeError(f"xgmi collective launch failed ({rc})")
 
@@ -168,7 +195,8 @@ class XgmiChannel:
         rc = self.lib.csa_xgmi_reduce_scatter(
             self.rank, self.world, self.slot_bytes, self._bufs, self._flags, flat.data_ptr(), lo * 4,
             (hi - lo) * 4, shard * 4, shard_out.data_ptr(), self.state.data_ptr(), self.timeout_s,
-            self.nblocks, torch.cuda.current_stream(self.device).cuda_stream)
+            self.blocks_for((hi - lo) * 4), self.diag_buf.data_ptr(),
+            torch.cuda.current_stream(self.device).cuda_stream)
         if rc:
             raise RuntimeError(f"xgmi reduce-scatter launch failed ({rc})")
 
@@ -178,6 +206,38 @@ class XgmiChannel:
 
     def error(self) -> int:
         return int(self.state[2].item())
+
+    def diag(self) -> List[dict]:
+        """Per-block record of the LAST call on this channel (synchronises the device):
+        epoch, wall-clock stamps (device-wide 100 MHz clock), status and — for a block
+        that timed out — the missing source, the flag value it last saw and that source's
+        own copy of the flag.  Blocks that did not take part in the last call are skipped."""
+        torch.cuda.synchronize(self.device)
+        d = self.diag_buf.view(-1, self._dw).cpu().tolist()
+        out = []
+        for b, (e, t0, tp, tw, stt, src, seen, own) in enumerate(d):
+            if t0 == 0:
+                continue
+            rec = {"block": b, "epoch": e, "t_start": t0, "t_pub": tp, "t_wait": tw,
+                   "status": {0: "running", 1: "ok", 2: "timeout"}.get(stt, stt)}
+            if stt == 2:
+                rec.update(missing=src, seen=seen, src_own_copy=own)
+            out.append(rec)
+        return out
+
+    def diag_summary(self) -> dict:
+        """Compact form of ``diag()`` for failure messages: the epochs blocks used, the
+        start / publish window, and every timed-out block's record."""
+        recs = self.diag()
+        if not recs:
+            return {"blocks": 0}
+        starts = [r["t_start"] for r in recs]
+        pubs = [r["t_pub"] for r in recs if r["t_pub"]]
+        return {"blocks": len(recs), "epochs": sorted({r["epoch"] for r in recs}),
+                "t_start": [min(starts), max(starts)], "t_pub": [min(pubs), max(pubs)] if pubs else None,
+                "unpublished": [r["block"] for r in recs if not r["t_pub"]][:16],
+                "timeouts": [r for r in recs if r["status"] == "timeout"][:8],
+                "state": self.state.tolist()}
 
     def check(self) -> None:
         if self.error():
@@ -190,7 +250,7 @@ class XgmiChannel:
         for p in self._opened:
             self.lib.csa_xgmi_close(p)
         for p, n in zip(self._local, self._local_n):       # back to the process pool
-            _POOL.setdefault((self._dev, n), []).append(p)
+            pool_put(self._dev, p, n)
         self._local, self._local_n, self._opened = [], [], []
 
 
@@ -275,6 +335,22 @@ def self_test(comm: XgmiComm) -> bool:
     if ch is not None:
         ch.close()
     return passed
+
+
+def max_blocks_from_env() -> int:
+    """``CSA_XGMI_BLOCKS``: cap on the workgroups of one peer-buffer call (0 / unset: none)."""
+    try:
+        return max(0, int(os.environ.get("CSA_XGMI_BLOCKS", "0")))
+    except ValueError:
+        return 0
+
+
+def shared_gpu_block_cap(world: int, live_channels: int = 1) -> int:
+    """The ``CSA_XGMI_BLOCKS`` that lets ``world`` ranks sharing ONE GPU keep every block of
+    ``live_channels`` concurrent calls resident: half of the chip's ~1280 slots for 256-
+    thread blocks (5 per CU at the kernels' register budget), the other half left to the
+    ranks' own compute kernels running beside them."""
+    return max(8, 640 // (world * max(1, live_channels)) // 8 * 8)
 
 
 def enabled_by_env() -> str:

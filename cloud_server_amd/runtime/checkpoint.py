@@ -85,10 +85,29 @@ def full_slots(eng) -> torch.Tensor:
     return eng.slots
 
 
+def full_params(eng) -> Optional[torch.Tensor]:
+    """The flat parameters every OWNER currently holds, under async_ps (a collective): there
+    a rank's copy of another owner's shard is a pulled one, up to 2s clocks behind, while
+    the optimizer slots saved beside it are that owner's current ones — so the saved
+    parameters are gathered from the owners, as ``full_slots`` gathers the slots.  None for
+    the synchronous strategies (every rank's flat is current)."""
+    if getattr(eng, "aps", None) is None:
+        return None
+    import torch.distributed as dist
+    lo, hi = eng.sync.shard_range()
+    full = torch.empty_like(eng.flat)
+    dist.all_gather_into_tensor(full, eng.flat[lo:hi].contiguous())
+    return full
+
+
 def engine_state(eng) -> Dict[str, Any]:
     """Everything needed to resume an engine exactly where it stopped.  Collective under
-    the "ps" strategy: call on every rank, write on the chief."""
+    the "ps" / "async_ps" strategies: call on every rank, write on the chief."""
     st = eng.model.export_state()
+    full = full_params(eng)
+    if full is not None:
+        for k in eng.model.state.shapes:
+            st[k] = eng.model.state.view(k, full).detach().clone().cpu()
     return {
         "model": st,
         "slots": full_slots(eng).detach().cpu(),

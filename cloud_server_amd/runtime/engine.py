@@ -110,6 +110,10 @@ class TrainEngine:
         if strategy == "async_ps" and self.ctx.enabled:
             from ..parallel.async_ps import make_async_ps
             self.aps = make_async_ps(self, lo, hi)
+            if hasattr(self.aps, "error"):
+                # a timed-out peer wait freezes the device transport (every later launch
+                # returns at once): part of the ranks' agreed health check
+                self.sync.extra_errors.append(self.aps.error)
         self.data = DeviceDataset(train, self.device)
         self.stream = BatchStream(self.data.n, cfg.batch_size, self.device, seed=cfg.seed,
                                   chunk=stream_chunk, rank=self.ctx.rank, world=self.ctx.world)
@@ -370,6 +374,16 @@ class TrainEngine:
             self.sync_device()
             self.aps.finish(self.flat, self.slots)
             self.sync_device()
+            # a timeout anywhere raises on EVERY rank together (never one rank alone)
+            self.sync.check_agreed()
+
+    def close(self) -> None:
+        """Release the peer-buffer transports (collective under data parallelism: every rank
+        calls it; buffers go back to the process pool once every rank's kernels drained)."""
+        if self.aps is not None and hasattr(self.aps, "close"):
+            self.aps.close()
+        if self.sync.xgmi is not None:
+            self.sync.xgmi.close()
 
     def staleness(self) -> int:
         """async_ps: the largest parameter staleness (clocks) any step of this rank saw."""

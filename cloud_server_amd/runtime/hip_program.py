@@ -205,12 +205,13 @@ class HipProgram:
         e = self.e
         # ps (the parameter-server capability): the same suffix buckets are REDUCE-SCATTERED
         # to their owner shards (GradSync.reduce_scatter_range; xGMI: one launch per bucket,
-        # every element leaves its GPU at most once) while the backward continues
-        # (ps overlaps only on the xGMI range reduce-scatter: on RCCL its per-owner reduces
-        # per bucket measured 0.156 ms/step at world 1 against 0.107 for one reduce-scatter
-        # after the backward — profiles/r4_notes.md)
-        self.overlap = (e.ctx.enabled and
-                        (e.sync.strategy == "allreduce" or (e.sync.strategy == "ps" and e.sync.xgmi is not None))
+        # every element leaves its GPU at most once) while the backward continues — only
+        # when EVERY bucket's range reduce-scatter measured faster on the xGMI kernel than
+        # on RCCL (GradSync.rs_choice, decided below): on RCCL the per-owner reduces per
+        # bucket measured 0.156 ms/step at world 1 against 0.107 for one reduce-scatter
+        # after the backward (profiles/r4_notes.md)
+        self.overlap = (e.ctx.enabled and e.sync.strategy in ("allreduce", "ps")
+                        and (e.sync.strategy == "allreduce" or e.sync.xgmi is not None)
                         and os.environ.get("CSA_DP_OVERLAP", "1") == "1")
         self.bucket_at: Dict[object, tuple] = {}
         if not self.overlap:
@@ -234,6 +235,12 @@ class HipProgram:
             if hi - lo >= min_elems or (last and hi > lo):
                 self.bucket_at[key] = (lo, hi)
                 hi = lo
+        if e.sync.strategy == "ps":
+            # every bucket's path decided now (collectively, timed under CSA_XGMI=auto)
+            paths = [e.sync.rs_choice(e.flat_grad, e.grad_shard, lo, hi) for lo, hi in self.bucket_at.values()]
+            if any(ch is None for ch in paths):
+                self.overlap, self.bucket_at = False, {}
+                return
 
     # ------------------------------------------------------------------ DP "lowrank"
     def _plan_lowrank(self) -> None:

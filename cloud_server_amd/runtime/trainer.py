@@ -305,6 +305,10 @@ class JobRun:
             if not action and self.cfg.ckpt_secs > 0 and now - self.t_ckpt >= self.cfg.ckpt_secs:
                 action = "ckpt"         # Supervisor(save_model_secs=60), construct_distribute.py:391
         action = _agree(self.ctx, action)
+        if self.ctx.enabled:
+            # a peer-buffer transport that timed out (xGMI channel, async_ps state) stops
+            # every rank together, at the next control point, not only at the end
+            eng.sync.check_agreed()
         if action == "ckpt":
             with trace_range("csa.ckpt"):
                 self.ckpter.save(self.chief)
@@ -338,6 +342,7 @@ class JobRun:
         if state != "paused":
             self.ckpter.save(chief)
         self.ckpter.wait()
+        eng.close()                   # peer buffers back to the pool (collective)
         if chief:
             write_status(self.model_dir, state=state, step=eng.host_step, final_accuracy=final_acc,
                          backend=eng.backend, fallback=eng.fallback_reason)

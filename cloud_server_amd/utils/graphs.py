@@ -53,32 +53,15 @@ def active_captures() -> int:
     return _active
 
 
-# RCCL watchdog (round 4): the process-group watchdog thread polls the end events of
-# eager collectives until it reaps them, about every 100 ms.  A capture that contains an
-# RCCL collective pulls RCCL's internal stream into the capture, and a query of an event
-# recorded on a stream that is capturing NOW fails (hipErrorCapturedEvent) and aborts the
-# process — seen in the GPU suite whenever a capture began within the watchdog's poll of
-# the warm-up's collectives.  So a capture under an initialised RCCL process group first
-# drains the device and gives the watchdog time to reap every completed eager work.
-_WATCHDOG_DRAIN_S = 0.3
-
-
-def _drain_rccl_watchdog() -> None:
-    import time
-    try:
-        import torch.distributed as dist
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != "nccl":
-            return
-    except Exception:  # pragma: no cover
-        return
-    torch.cuda.synchronize()
-    time.sleep(_WATCHDOG_DRAIN_S)
+# (round 4 drained the device and slept 0.3 s here before every capture under RCCL, to let
+# the process-group watchdog reap eager collectives first; captured collectives now run on
+# a dedicated process group that never carries an eager work the watchdog is polling —
+# parallel/dp.py GradSync._setup_capture_group — so capture needs no wait at all)
 
 
 @contextlib.contextmanager
 def capture(graph: "torch.cuda.CUDAGraph", stream: Optional["torch.cuda.Stream"] = None,
             pool=None) -> Iterator[None]:
-    _drain_rccl_watchdog()
     _enter()
     try:
         kw = {} if stream is None else {"stream": stream}

@@ -39,6 +39,8 @@ def main() -> int:
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
+    from cloud_server_amd.parallel.dist import rccl_env_defaults
+    rccl_env_defaults()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
         cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-4,

@@ -414,7 +414,7 @@ def test_async_ps_gloo_converges_with_bounded_staleness(world, staleness):
     out = _spawn(_train_async, world, staleness, steps)
     for r in range(world):
         flat, stale, first, last, applied = out[r]
-        assert stale <= 2 * staleness + 1, (r, stale)
+        assert stale <= 2 * staleness, (r, stale)         # async_ps.py: max_staleness <= 2s
         assert last < first, (r, first, last)
         assert applied == world * steps, (r, applied)
         torch.testing.assert_close(flat, out[0][0], rtol=0, atol=0)
@@ -431,3 +431,64 @@ def test_distributed_job_async_ps(tmp_path):
     lines = open(os.path.join(mdir, "result.txt")).read().splitlines()
     assert [l.split(",")[0] for l in lines[:3]] == ["step:0", "step:4", "step:8"]
     assert lines[3].startswith("final_accuracy:")
+
+
+def _aps_save(rank, world, port, path, out):
+    """async_ps mid-run checkpoint: rank 1 is slower, so rank 0's copy of rank 1's shard is
+    a stale pull while the saved slots are rank 1's current ones."""
+    import time
+    from cloud_server_amd.parallel.dist import shutdown
+    from cloud_server_amd.runtime import checkpoint as ckpt
+    from cloud_server_amd.runtime.engine import TrainEngine
+    ctx = _init(rank, world, port)
+    cfg = parse_train_config(dict(CFG, options=dict(CFG["options"], batch_size=16, staleness=2)))
+    eng = TrainEngine(cfg, synthetic_mnist(512, seed=1), device="cpu", ctx=ctx, strategy="async_ps")
+    for _ in range(9):
+        if rank == 1:
+            time.sleep(0.02)
+        eng.step()
+    st = ckpt.engine_state(eng)                      # collective
+    lo, hi = eng.sync.shard_range()
+    out[rank] = (eng.flat[lo:hi].clone(), eng.slots.clone(), (lo, hi), eng.flat.clone())
+    if rank == 0:
+        ckpt.save(path, eng.host_step, st)
+    eng.finish_async()
+    shutdown(ctx)
+
+
+def _aps_resume(rank, world, port, path, out):
+    from cloud_server_amd.parallel.dist import shutdown
+    from cloud_server_amd.runtime import checkpoint as ckpt
+    from cloud_server_amd.runtime.engine import TrainEngine
+    ctx = _init(rank, world, port)
+    cfg = parse_train_config(dict(CFG, options=dict(CFG["options"], batch_size=16, staleness=2)))
+    eng = TrainEngine(cfg, synthetic_mnist(512, seed=1), device="cpu", ctx=ctx, strategy="async_ps")
+    ckpt.restore_engine(eng, ckpt.load(ckpt.latest(path)[1]))
+    out[rank] = (eng.flat.clone(), eng.slots.clone(), eng.host_step)
+    eng.finish_async()
+    shutdown(ctx)
+
+
+def test_async_ps_checkpoint_saves_owner_shards_and_resumes(tmp_path):
+    """a mid-run async_ps checkpoint holds every OWNER's current shard (gathered,
+    as the slots are), not the chief's stale pulled copies; a resume puts the same
+    parameters on every rank and each owner's slots back on its shard."""
+    from cloud_server_amd.runtime import checkpoint as ckpt
+    path = str(tmp_path / "m")
+    os.makedirs(path)
+    saved = _spawn(_aps_save, 2, path)
+    obj = ckpt.load(ckpt.latest(path)[1])
+    flat = torch.zeros_like(saved[0][3])
+    for name, o, k in obj["layout"]:
+        flat[o:o + k] = obj["model"][name].reshape(-1)
+    for r in range(2):
+        own, slots, (lo, hi), _ = saved[r]
+        torch.testing.assert_close(flat[lo:hi], own, rtol=0, atol=0)                  # owner's shard
+        torch.testing.assert_close(obj["slots"][:, lo:hi], slots, rtol=0, atol=0)     # owner's slots
+    res = _spawn(_aps_resume, 2, path)
+    for r in range(2):
+        rflat, rslots, step = res[r]
+        lo, hi = saved[r][2]
+        assert step == 9
+        torch.testing.assert_close(rflat, flat, rtol=0, atol=0)
+        torch.testing.assert_close(rslots, obj["slots"][:, lo:hi], rtol=0, atol=0)

@@ -29,6 +29,8 @@ class _DPContext(DistContext):
 def pg():
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from cloud_server_amd.parallel.dist import rccl_env_defaults
+    rccl_env_defaults()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     yield
     # the test's engines (and the RCCL works captured into their graphs) die with this
@@ -178,3 +180,34 @@ def test_capture_never_finalizes_garbage_graphs_while_capturing():
     g.replay()
     torch.cuda.synchronize()
     assert float(x[0]) == 1.0         # captures never execute: only the replay added 1
+
+
+@pytest.mark.parametrize("strategy", ["allreduce", "ps"])
+def test_capture_right_after_eager_collectives(pg, monkeypatch, strategy):
+    """a DP step whose RCCL collectives are captured into the HIP graph is
+    captured IMMEDIATELY after eager collectives on the default group (no device drain,
+    no sleep anywhere in ``capture()``): the captured collectives run on the dedicated
+    capture group, whose stream never carries an eager work the watchdog is polling."""
+    import inspect
+    from cloud_server_amd.utils import graphs
+    assert "sleep" not in inspect.getsource(graphs.capture)
+    monkeypatch.setenv("CSA_XGMI", "0")           # RCCL collectives inside the step graphs
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
+    assert a.sync.cap_group is not None
+    assert a.sync.cap_group_retired is True, a.sync.cap_group_retired   # observed, not timed
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    x = torch.ones(4096, device="cuda:0")
+    for _ in range(8):
+        dist.all_reduce(x)                       # eager works the watchdog still polls
+    a.step(); b.step()                           # warm-up + capture right away
+    for _ in range(8):
+        dist.all_reduce(x)
+    a.prepare_group_graph()                      # every multi-step capture, right away
+    b.prepare_group_graph()
+    a.run_steps(15); b.run_steps(15)
+    torch.cuda.synchronize()
+    assert a.host_step == b.host_step == 16
+    torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
