@@ -81,7 +81,7 @@ __device__ __forceinline__ unsigned xg_epoch(const XgArgs& a, int* s_abort, unsi
     const unsigned long long t0 = wall_clock64();
     *s_abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     *s_e = __hip_atomic_load(a.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    if (a.diag) {
+    if (a.diag && !*s_abort) {       // (a poisoned channel keeps the failing call's record)
       unsigned long long* d = a.diag + (long)blockIdx.x * XG_DIAG;
       d[0] = *s_e; d[1] = t0; d[2] = 0; d[3] = 0; d[4] = 0; d[5] = 0; d[6] = 0; d[7] = 0;
     }

@@ -139,7 +139,9 @@ _SIGS = {
 
 
 def lib_path() -> str:
-    return _build.KERNEL_LIB
+    """The in-tree kernel library (``CSA_KERNEL_LIB`` overrides it: A/B runs of a kernel
+    variant built beside it, e.g. scripts/xgmi_stress.py)."""
+    return os.environ.get("CSA_KERNEL_LIB") or _build.KERNEL_LIB
 
 
 def available() -> bool:
