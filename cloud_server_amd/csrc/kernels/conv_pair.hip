@@ -25,6 +25,7 @@
 // per-layer kernels (conv.hip).
 #include "common.h"
 #include "dense_update.h"
+#include <vector>
 #include <cstdlib>
 #include <algorithm>
 
@@ -59,6 +60,19 @@ struct CPFwdArgs {
   const float* wB; const float* bB; int actB; float alphaB;
   float* y; uint8_t* argmax; float* stat; int nslab;
 };
+
+// Accumulators of LATER launches of the step zeroed by the pair forward's threads (the
+// split-K outputs of the dense forwards, read until the end of the previous step's pair
+// backward): one float4 per thread, no launch of their own (round 5: the fused program's
+// flat optimizer launch is gone, csa_conv_pair_tail_set).
+constexpr int CP_MAXZ = 4;
+struct CPZero { float4* p[CP_MAXZ]; long n4[CP_MAXZ]; int n; };
+
+__device__ __forceinline__ void cp_zero_early(const CPZero& z) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long)gridDim.x * blockDim.x;
+  for (int k = 0; k < z.n; ++k)
+    for (long i = gid; i < z.n4[k]; i += nth) z.p[k][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
 
 // Band tile extents (rows in conv-B-output coordinates and the derived c1 / x rows).
 struct CPBand {
@@ -319,8 +333,9 @@ __device__ __forceinline__ void cp_tables_a(const CPGeom& g, const CPBand& t, in
   }
 }
 
-__global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a) {
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a, CPZero z) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  cp_zero_early(z);
   __shared__ float s_stat[2 * CP_MAXC2];
   __shared__ int s_offA[32], s_offPA[32];
   const CPGeom& g = a.g;
@@ -450,6 +465,7 @@ struct CPBwdArgs {
   float* dscale; float* doffset; float* run_mean; float* run_var; float momentum;
   float* dwA; float* dbA; float* dwB; float* dbB; int stripes;
   const int* tabs; int tab_stride;  // per-band index tables (csa_conv_pair_bwd_tables) or null
+  unsigned* img_tk;                 // tail: +1 per workgroup once its image tile is in LDS (or null)
 };
 
 // LDS carve of the backward (float offsets), shared by the kernel and the host size check.
@@ -728,6 +744,10 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
       }
   }
   __syncthreads();
+  // (every thread's image values are in LDS: this workgroup no longer reads the staged
+  // batch, which the tail's staging workgroups overwrite with the next one)
+  if (a.img_tk && threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.img_tk + (bid % 16) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   CP_STAMP(9);
   // ---- route: dc2 (zero-padded tile) for conv-B-output rows [d2y0, d2y0 + D2H - 1)
   {
@@ -891,21 +911,172 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_kernel(CPBwdArgs a) 
 // of their layer, so they run inside this launch instead of as serial links of the chain.
 // The pair's workgroups come first: the dispatcher deals blocks in index order, so the
 // critical pair blocks all start before any update block takes a slot.
+//
+// Tail (round 5): the rest of the fused program's optimizer launch, as workgroups of this
+// launch.  What that launch still did after horizontal fusion — fold the conv weight-
+// gradient stripes and update the conv and BatchNorm parameters, zero the BN statistic
+// slabs for the next step, stage the next step's batch — depends only on THIS launch's
+// pair workgroups, which finish well before its dense update workgroups (pair chain
+// ~21 us, launch ~28 us: profiles/r4_notes.md).  So, after the update segments:
+//   tail 0            waits until every pair workgroup is done (ticket 0), then folds /
+//                     updates the striped and direct-gradient parameters and zeroes;
+//   tail 1 .. NS      wait until every pair workgroup has its image tile in LDS (ticket
+//                     1), then copy the next batch (rows[cursor]) into the staging buffers.
+// Tail workgroups take slots only after every pair / update workgroup was dispatched, so
+// their (bounded) waits are on workgroups that already run; the last tail workgroup to
+// finish resets the tickets for the next launch.  The head's parameters are updated in
+// the last dense segment's head epilogue and the metric ring is written there too, so the
+// fused program's step has no optimizer launch at all.
+constexpr int CPT_MAXSEG = 8;
+// Tickets: 700 workgroups adding into ONE word serialise at the memory side, and a wave's
+// next vmcnt wait includes its own atomic — so each count is spread over CPT_SPREAD words
+// on separate 64-byte lines (workgroup b adds into word b % CPT_SPREAD; waiters sum them).
+constexpr int CPT_SPREAD = 16, CPT_LINE = 16;         // words, words per line
+constexpr int CPT_TK_WORDS = (2 * CPT_SPREAD + 1) * CPT_LINE;
+static_assert(CPT_SPREAD == 16 && CPT_LINE == 16, "cp_bwd_body spreads the image ticket the same way");
+__host__ __device__ __forceinline__ unsigned* cpt_word(unsigned* tk, int count, int b) {
+  return tk + (count * CPT_SPREAD + (b % CPT_SPREAD)) * CPT_LINE;
+}
+// One parameter workgroup of the tail: elements [base, base + 256) of one parameter tensor
+// (w updated with g = sum_s src[s * ld + i]).  A device table built once at plan time
+// (csa_conv_pair_tail_plan): each workgroup reads its own entry with a uniform address (a
+// scalar load) — per-lane selection among argument arrays made the compiler copy the whole
+// argument struct to scratch in EVERY workgroup of the launch.
+struct CPTailSeg {
+  float* w; float* s0; float* s1; float* src;
+  int S, ld, n, zero, base, pad0, pad1, pad2;
+};
+struct CPTail {
+  int on, param_blocks, stage_blocks;
+  unsigned* tk;                     // [CPT_TK_WORDS]: pair workgroups done | image tiles
+                                    // consumed (CPT_SPREAD words each) | tails done
+  int* err;                         // [1]: a tail wait timed out (nothing of that tail ran)
+  int opt; float lr; const int64_t* step;
+  const CPTailSeg* segs;            // [param_blocks]
+  int nz; float* zp[CP_MAXZ]; int zn[CP_MAXZ];
+  // next batch: out_img[b][..] = img[rows[cursor * B + b]][..] (32-bit words), out_lbl
+  const uint32_t* img; const int64_t* labels; const int64_t* rows; const int64_t* cursor;
+  int B, words; uint32_t* out_img; int64_t* out_lbl;
+};
+
+__device__ __forceinline__ bool cp_tail_wait(const CPTail& t, int k, unsigned want) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = wall_clock64();
+    int ok = 1;
+    // relaxed polls (an acquire per poll invalidates this XCD's L2 every iteration — under
+    // every other workgroup of the launch), ONE acquire once the count is reached
+    for (;;) {
+      unsigned have = 0;
+#pragma unroll
+      for (int j = 0; j < CPT_SPREAD; ++j)
+        have += __hip_atomic_load(cpt_word(t.tk, k, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (have >= want) break;
+      if (wall_clock64() - t0 > 100000000ull) {           // 1 s: never a hung launch
+        __hip_atomic_store(t.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// Tail workgroup k < param_blocks: its table entry's 256 elements; each thread's stripe /
+// parameter / slot loads are issued together (one memory round trip).
+__device__ __forceinline__ void cp_tail_params(const CPTail& t, int k) {
+  const CPTailSeg d = t.segs[k];                       // uniform address: scalar loads
+  const int i = d.base + (int)threadIdx.x;
+  if (i < d.n) {
+    const int nslot = opt_nslots(t.opt);
+    float v[16];
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) v[s2] = d.src[(s2 < d.S ? s2 : 0) * d.ld + i];   // all in flight
+    float wv = d.w[i];
+    float z0 = nslot >= 1 ? d.s0[i] : 0.f, z1 = nslot >= 2 ? d.s1[i] : 0.f;
+    float gsum = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) gsum += s2 < d.S ? v[s2] : 0.f;
+    opt_update(t.opt, opt_step_lr(t.opt, t.lr, t.step), wv, gsum, z0, z1);
+    d.w[i] = wv;
+    if (nslot >= 1) d.s0[i] = z0;
+    if (nslot >= 2) d.s1[i] = z1;
+    if (d.zero)
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2)
+        if (s2 < d.S) d.src[s2 * d.ld + i] = 0.f;
+  }
+  // the statistic slabs, spread over the parameter workgroups
+#pragma unroll
+  for (int z = 0; z < CP_MAXZ; ++z) {
+    if (z >= t.nz) break;
+    for (int j = k * CP_THREADS + (int)threadIdx.x; j < t.zn[z]; j += t.param_blocks * CP_THREADS) t.zp[z][j] = 0.f;
+  }
+}
+
+__device__ __forceinline__ void cp_tail_stage(const CPTail& t, int blk) {
+  const long i = (long)blk * CP_THREADS + threadIdx.x;
+  const long total = (long)t.B * t.words;
+  const int64_t c = *t.cursor;
+  if (i < t.B) t.out_lbl[i] = t.labels[t.rows[c * t.B + i]];
+  if (i >= total) return;
+  const long b = i / t.words, off = i - b * t.words;
+  t.out_img[i] = t.img[t.rows[c * t.B + b] * t.words + off];
+}
+
+__device__ __forceinline__ void cp_tail_body(const CPTail& t, int npair, int k) {
+  if (k < t.param_blocks) {
+    if (cp_tail_wait(t, 0, (unsigned)npair)) cp_tail_params(t, k);
+  } else {
+    if (cp_tail_wait(t, 1, (unsigned)npair)) cp_tail_stage(t, k - t.param_blocks);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned ntail = (unsigned)(t.param_blocks + t.stage_blocks);
+    unsigned* fin = t.tk + 2 * CPT_SPREAD * CPT_LINE;
+    const unsigned prev = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == ntail - 1) {                      // every tail read the tickets: reset them
+      for (int j = 0; j < 2 * CPT_SPREAD; ++j)
+        __hip_atomic_store(t.tk + j * CPT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <bool ONE, int NSLOT>
-__device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs& u, float* smem) {
+__device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs& u, const CPTail& t, float* smem) {
   const int npair = a.g.B * a.g.nbands;
   const int bid = (int)blockIdx.x;
   if (bid < npair) {
     cp_bwd_body<ONE>(a, bid, smem);
+    if (t.on) {
+      // the barrier drains every wave's stripe atomics (device-scope: visible once done);
+      // block 0's plain stores (BN parameter gradients, running statistics) get ONE
+      // release — not 700 L2 write-backs
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        if (bid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(cpt_word(t.tk, 0, bid), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     return;
   }
-  du_segs_body<NSLOT, true>(u, bid - npair, smem);
+  const int nupd = u.start[u.nseg];
+  if (bid < npair + nupd) {
+    du_segs_body<NSLOT, true>(u, bid - npair, smem);
+    return;
+  }
+  cp_tail_body(t, npair, bid - npair - nupd);
 }
 
 template <bool ONE, int NSLOT>
-__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u) {
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u, CPTail t) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  cp_bwd_upd_body<ONE, NSLOT>(a, u, smem);
+  cp_bwd_upd_body<ONE, NSLOT>(a, u, t, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -938,8 +1109,9 @@ struct CPVFwdArgs {
 __host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 1 + g.KAw - 1; }
 
 template <int KBH, int KBW>
-__global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a) {
+__global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z) {
   const CPGeom& g = a.g;
+  cp_zero_early(z);
   __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
   __shared__ int s_koffA[CPV_MAXKA];                    // x-tile offset of conv-A tap k
   __shared__ float s_b[CPV_MAXC1 + CPV_MAXC2];
@@ -1620,7 +1792,15 @@ CSA_API int csa_conv_pair_valu_ok(const int* geom) {
 CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
-                              int nslab, hipStream_t st) {
+                              int nslab, float* const* zero_ptrs, const long* zero_n, int nzero, hipStream_t st) {
+  CPZero z{};
+  if (nzero < 0 || nzero > CP_MAXZ) return -2;
+  for (int k = 0; k < nzero; ++k) {
+    if (((uintptr_t)zero_ptrs[k] & 15) || (zero_n[k] & 3)) return -2;
+    z.p[k] = reinterpret_cast<float4*>(zero_ptrs[k]);
+    z.n4[k] = zero_n[k] / 4;
+  }
+  z.n = nzero;
   CPFwdArgs a{};
   if (!cp_geom(geom, a.g) || cp_lds(a.g, false) > CP_LDS_MAX) return -1;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
@@ -1628,30 +1808,38 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
   a.nslab = nslab < 1 ? 1 : nslab;
   if (cpv_ok(a.g)) {
     CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab};
-    if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
-    else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v);
+    if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z);
+    else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z);
     return (int)hipGetLastError();
   }
   static bool attr = hipFuncSetAttribute((const void*)conv_pair_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
   hipLaunchKernelGGL(conv_pair_fwd_kernel, dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CP_THREADS),
-                     cp_lds(a.g, false), st, a);
+                     cp_lds(a.g, false), st, a, z);
   return (int)hipGetLastError();
 }
 
+// The tail of the next carrying launch on this thread (csa_conv_pair_tail_set), like the
+// deferred dense segments: host state consumed by that launch.
+static thread_local CPTail g_cp_tail{};
+
 template <bool ONE, int NSLOT>
-static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const DUSegs& u, size_t lds, hipStream_t st) {
+static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const DUSegs& u, const CPTail& t, size_t lds, hipStream_t st) {
   static const bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_upd_kernel<ONE, NSLOT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
-  const unsigned blocks = (unsigned)(a.g.B * a.g.nbands + u.start[u.nseg]);
-  hipLaunchKernelGGL((conv_pair_bwd_upd_kernel<ONE, NSLOT>), dim3(blocks), dim3(CP_THREADS), lds, st, a, u);
+  const unsigned blocks = (unsigned)(a.g.B * a.g.nbands + u.start[u.nseg] + (t.on ? t.param_blocks + t.stage_blocks : 0));
+  hipLaunchKernelGGL((conv_pair_bwd_upd_kernel<ONE, NSLOT>), dim3(blocks), dim3(CP_THREADS), lds, st, a, u, t);
   return (int)hipGetLastError();
 }
 
-// The MFMA pair backward carrying the deferred dense update segments taken for it.
-static int cp_launch_bwd_upd(const CPBwdArgs& a, const DUSegs& u, hipStream_t st) {
+// The MFMA pair backward carrying the deferred dense update segments taken for it (and the
+// tail, when one was set for this launch).
+static int cp_launch_bwd_upd(CPBwdArgs a, const DUSegs& u, hipStream_t st) {
+  const CPTail t = g_cp_tail;
+  g_cp_tail = CPTail{};
+  if (t.on) a.img_tk = cpt_word(t.tk, 1, 0);
   size_t lds = cp_lds(a.g, true);
   const size_t dl = du_lds_floats(u.seg[0].M, 4) * sizeof(float);
   for (int s = 1; s < u.nseg; ++s)
@@ -1659,10 +1847,65 @@ static int cp_launch_bwd_upd(const CPBwdArgs& a, const DUSegs& u, hipStream_t st
   if (dl > lds) lds = dl;
   const int ns = opt_nslots(u.seg[0].opt);
   const bool one = cp_bwd_one_batch(a);
-  if (ns == 0) return one ? cp_launch_bwd_upd_t<true, 0>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 0>(a, u, lds, st);
-  if (ns == 1) return one ? cp_launch_bwd_upd_t<true, 1>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 1>(a, u, lds, st);
-  return one ? cp_launch_bwd_upd_t<true, 2>(a, u, lds, st) : cp_launch_bwd_upd_t<false, 2>(a, u, lds, st);
+  if (ns == 0) return one ? cp_launch_bwd_upd_t<true, 0>(a, u, t, lds, st) : cp_launch_bwd_upd_t<false, 0>(a, u, t, lds, st);
+  if (ns == 1) return one ? cp_launch_bwd_upd_t<true, 1>(a, u, t, lds, st) : cp_launch_bwd_upd_t<false, 1>(a, u, t, lds, st);
+  return one ? cp_launch_bwd_upd_t<true, 2>(a, u, t, lds, st) : cp_launch_bwd_upd_t<false, 2>(a, u, t, lds, st);
 }
+
+// Tail plan: the parameter table of the tail's parameter workgroups, written to the device
+// buffer `table` (at least csa_conv_pair_tail_table_bytes(n, nseg)).  Parameter k < nseg:
+// w[k][i] updated with sum_s src[k][s * ld[k] + i] (S[k] <= 16 rows; zero[k]: the rows are
+// re-zeroed, their only reader is this fold).  Returns the parameter workgroup count.
+CSA_API long csa_conv_pair_tail_table_bytes(const int* n, int nseg) {
+  long blocks = 0;
+  for (int k = 0; k < nseg; ++k) blocks += (n[k] + CP_THREADS - 1) / CP_THREADS;
+  return blocks * (long)sizeof(CPTailSeg);
+}
+
+CSA_API int csa_conv_pair_tail_plan(void* table, int opt, int nseg, float* const* w, float* const* s0,
+                                    float* const* s1, float* const* src, const int* S, const int* ld, const int* n,
+                                    const int* zero) {
+  if (!table || nseg < 1 || nseg > CPT_MAXSEG) return -1;
+  const int ns = opt_nslots(opt);
+  std::vector<CPTailSeg> segs;
+  for (int k = 0; k < nseg; ++k) {
+    if (!w[k] || !src[k] || S[k] < 1 || S[k] > 16 || n[k] < 1 || ld[k] < n[k]) return -2;
+    if ((ns >= 1 && !s0[k]) || (ns >= 2 && !s1[k])) return -2;
+    for (int base = 0; base < n[k]; base += CP_THREADS)
+      segs.push_back(CPTailSeg{w[k], s0[k], s1[k], src[k], S[k], ld[k], n[k], zero[k], base, 0, 0, 0});
+  }
+  if (hipMemcpy(table, segs.data(), segs.size() * sizeof(CPTailSeg), hipMemcpyHostToDevice) != hipSuccess) return -3;
+  return (int)segs.size();
+}
+
+// Tail of the NEXT pair backward launched by this thread (it must carry deferred dense
+// segments: the MFMA carrier): `param_blocks` workgroups over the planned table, nz <= 4
+// float regions zeroed, the next batch staged when out_img != null (imsz % 4 == 0).
+// tk: 3 zeroed uints, err: 1 int (device).
+CSA_API int csa_conv_pair_tail_set(unsigned* tk, int* err, int opt, float lr, const int64_t* step,
+                                   const void* table, int param_blocks, int nz, float* const* zp, const long* zn,
+                                   const uint8_t* img, const int64_t* labels, const int64_t* rows,
+                                   const int64_t* cursor, int B, long imsz, uint8_t* out_img, int64_t* out_lbl) {
+  if (!tk || !err || !step || !table || param_blocks < 1 || nz < 0 || nz > CP_MAXZ) return -1;
+  CPTail t{};
+  t.on = 1; t.tk = tk; t.err = err; t.opt = opt; t.lr = lr; t.step = step;
+  t.segs = static_cast<const CPTailSeg*>(table); t.param_blocks = param_blocks;
+  t.nz = nz;
+  for (int k = 0; k < nz; ++k) { t.zp[k] = zp[k]; t.zn[k] = (int)zn[k]; }
+  if (out_img) {
+    if (imsz % 4 || B < 1 || !img || !labels || !rows || !cursor || !out_lbl) return -3;
+    t.img = reinterpret_cast<const uint32_t*>(img); t.labels = labels; t.rows = rows; t.cursor = cursor;
+    t.B = B; t.words = (int)(imsz / 4);
+    t.out_img = reinterpret_cast<uint32_t*>(out_img); t.out_lbl = out_lbl;
+    const long total = (long)B * t.words > B ? (long)B * t.words : B;
+    t.stage_blocks = (int)((total + CP_THREADS - 1) / CP_THREADS);
+  }
+  g_cp_tail = t;
+  return 0;
+}
+
+CSA_API int csa_conv_pair_tail_pending() { return g_cp_tail.on; }
+CSA_API int csa_conv_pair_tail_ticket_words() { return CPT_TK_WORDS; }
 
 __global__ __launch_bounds__(CP_THREADS) void cp_bwd_tables_kernel(CPGeom g, int* out, int stride) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1749,12 +1992,14 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
     if (!vattr) return -3;
     if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_bwd_kernel<2, 2>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
     else hipLaunchKernelGGL((cpv_bwd_kernel<3, 3>), grid, dim3(CPV_T), cpv_bwd_lds_max(a.g), st, a);
+    if (g_cp_tail.on) return -7;                                // a tail needs the MFMA carrier
     DUSegs u;                                                   // deferred updates on their own
     if (du_take(u) > 0) return du_flush_segs(u, st);
     return (int)hipGetLastError();
   }
   DUSegs u;
   if (du_take(u) > 0) return cp_launch_bwd_upd(a, u, st);
+  if (g_cp_tail.on) return -7;
   if (cp_bwd_one_batch(a))
     hipLaunchKernelGGL(conv_pair_bwd_kernel<true>, grid, dim3(CP_THREADS), cp_lds(a.g, true), st, a);
   else

@@ -53,6 +53,9 @@ struct DUArgs {
   const float* hrl; const int* hrc;   // [M] per-row loss / correct
   float* ring_loss; int* ring_correct; int ring; float ldiv;
   int hact; float halpha;   // the head's input transform: the head reads act(hy)
+  // head parameters updated IN PLACE by the epilogue (round 5, the pair-backward tail
+  // program: no flat optimizer launch) instead of storing dWh / dbh into hgw / hgb
+  float* hw; float* hb; float* hs0w; float* hs1w; float* hs0b; float* hs1b;
 };
 
 constexpr int DU_HNC = 10;           // head classes
@@ -176,7 +179,16 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
     } else {
       for (int m = 0; m < M; ++m) v = fmaf(act_fwd(a.hy[(long)m * a.N + n], a.hact, a.halpha), s_d[m * DU_HNC + j], v);
     }
-    a.hgw[(long)n * DU_HNC + j] = v;
+    if (a.hw) {                                            // in-place update (shared rule)
+      const long k = (long)n * DU_HNC + j;
+      float w = a.hw[k], z0 = a.hs0w ? a.hs0w[k] : 0.f, z1 = a.hs1w ? a.hs1w[k] : 0.f;
+      opt_update(a.opt, opt_step_lr(a.opt, a.lr, a.step), w, v, z0, z1);
+      a.hw[k] = w;
+      if (a.hs0w) a.hs0w[k] = z0;
+      if (a.hs1w) a.hs1w[k] = z1;
+    } else {
+      a.hgw[(long)n * DU_HNC + j] = v;
+    }
   }
   if (last_block) {                                        // dbh and the step's metrics
     const int lane = t & 63, w = t >> 6;
@@ -184,7 +196,15 @@ __device__ __forceinline__ void du_head_finish(const DUArgs& a, DUHead& h, float
       if (lane < DU_HNC) {
         float v = 0.f;
         for (int m = 0; m < M; ++m) v += s_d[m * DU_HNC + lane];
-        a.hgb[lane] = v;
+        if (a.hb) {
+          float wb = a.hb[lane], z0 = a.hs0b ? a.hs0b[lane] : 0.f, z1 = a.hs1b ? a.hs1b[lane] : 0.f;
+          opt_update(a.opt, opt_step_lr(a.opt, a.lr, a.step), wb, v, z0, z1);
+          a.hb[lane] = wb;
+          if (a.hs0b) a.hs0b[lane] = z0;
+          if (a.hs1b) a.hs1b[lane] = z1;
+        } else {
+          a.hgb[lane] = v;
+        }
       }
     } else if (w == 1) {
       float l = lane < M ? a.hrl[lane] : 0.f;

@@ -288,6 +288,17 @@ CSA_API int csa_dense_update_defer(const float* dY, float* W, float* bias, int M
 
 CSA_API int csa_dense_update_pending() { return g_du_def.n; }
 
+// The deferred head segment updates the head's parameters in place (w [K][10], b [10] and
+// their optimizer slots) instead of storing dWh / dbh: the pair-backward tail program.
+CSA_API int csa_dense_update_head_params(float* hw, float* hb, float* hs0w, float* hs1w, float* hs0b, float* hs1b) {
+  if (g_du_def.head < 0 || !hw || !hb) return -1;
+  DUArgs& a = g_du_def.seg[g_du_def.head];
+  const int ns = opt_nslots(a.opt);
+  if ((ns >= 1 && (!hs0w || !hs0b)) || (ns >= 2 && (!hs1w || !hs1b))) return -2;
+  a.hw = hw; a.hb = hb; a.hs0w = hs0w; a.hs1w = hs1w; a.hs0b = hs0b; a.hs1b = hs1b;
+  return 0;
+}
+
 namespace csa {
 int du_take(DUSegs& out) {
   out = DUSegs{};

@@ -78,7 +78,13 @@ _SIGS = {
     "csa_conv_pair_ok": (I, [P]),
     "csa_cp_debug": (I, [P]),
     "csa_head_debug": (I, [P]),
-    "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P]),
+    "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P, P, I, P]),
+    "csa_conv_pair_tail_table_bytes": (L, [P, I]),
+    "csa_conv_pair_tail_plan": (I, [P, I, I, P, P, P, P, P, P, P, P]),
+    "csa_conv_pair_tail_set": (I, [P, P, I, F, P, P, I, I, P, P, P, P, P, P, I, L, P, P]),
+    "csa_conv_pair_tail_pending": (I, []),
+    "csa_conv_pair_tail_ticket_words": (I, []),
+    "csa_dense_update_head_params": (I, [P, P, P, P, P, P]),
     "csa_conv_pair_valu_ok": (I, [P]),
     "csa_conv_pair_grid": (I, [P]),
     "csa_set_deterministic": (None, [I]),

@@ -187,6 +187,7 @@ class HipProgram:
         self._plan_stage()
         self._plan_grad_buckets()
         self.opt_segments = self._opt_segments()
+        self._plan_tail()
 
     # ------------------------------------------------------------------ DP overlap
     def _plan_grad_buckets(self) -> None:
@@ -486,6 +487,118 @@ class HipProgram:
             self.head_row and last.kind == "dense" and last.fused and len(self.units) > 2
             and not last.in_tf.has_bn
             and self.lib.csa_head_dgrad_ok(self.B, last.layer.spec.hidden, last.layer.in_shape.numel))
+
+    # ------------------------------------------------------------------ pair-backward tail
+    def _plan_tail(self) -> None:
+        """Round 5: the one-GPU fused program without an optimizer launch.
+
+        After horizontal fusion the flat optimizer launch only updated the conv pair's
+        (striped) and the BatchNorm's parameters, zeroed the next step's accumulators and
+        staged the next batch — 8.1 us of a ~88 us step (profiles/r4_step_trace.md).  Now:
+
+        * the conv / BN updates, the statistic-slab zeroing and the batch staging run as
+          TAIL workgroups of the pair backward launch (``csa_conv_pair_tail_set``), which
+          wait (bounded) for the pair workgroups — done ~7 us before that launch's dense
+          update workgroups;
+        * the head's parameters are updated in place by the last dense segment's head
+          epilogue (``csa_dense_update_head_params``), which also writes the metric ring;
+        * the dense forwards' split-K outputs, read until the end of the pair backward, are
+          zeroed by the NEXT step's pair forward threads (its zero list).
+
+        Applies to the horizontal-fusion program with the staged batch and the row head
+        when every other parameter and accumulator is one of those (``CSA_PAIR_TAIL=0``
+        restores the optimizer launch)."""
+        self.tail = False
+        self.fwd_zero: List[torch.Tensor] = []
+        if not (getattr(self, "hfuse", False) and getattr(self, "staged", False) and self.head_row
+                and self.pair is not None and os.environ.get("CSA_PAIR_TAIL", "1") == "1"):
+            return
+        e = self.e
+        ua, ub = self.units[0], self.units[1]
+        if not (ua.wg_stripes > 1 and ub.wg_stripes == ua.wg_stripes and not getattr(ua, "row_fold", False)
+                and ua.wg_stripes <= 16):
+            return
+        nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
+        offs = self.model.state.offsets
+        fused = {f"{u.layer.name}.{p}" for u in self.units if u.kind == "dense" and u.fused for p in ("weight", "bias")}
+        params = []           # (name, src tensor, S, ld, zero)
+        for u, acc, nm in ((ua, ua.dw_acc, "weight"), (ua, ua.db_acc, "bias"), (ub, ub.dw_acc, "weight"),
+                           (ub, ub.db_acc, "bias")):
+            if acc is not None:
+                params.append((f"{u.layer.name}.{nm}", acc, u.wg_stripes, acc.shape[1], 1))
+        if nt.has_bn:
+            for pn in ("scale", "offset"):
+                n = f"{nt.norm.name}.{pn}"
+                params.append((n, self.gviews[n], 1, self.gviews[n].numel(), 0))
+        rest = set(offs) - fused - {p[0] for p in params} - {"head.weight", "head.bias"}
+        if rest or len(params) > 8:
+            return                      # parameters the tail does not know about
+        # zero regions: the BN statistic slabs (read by every pair workgroup) in the tail,
+        # the dense split-K outputs at the next pair forward; anything else: no tail
+        slabs = []
+        for u in self.units:
+            if u.in_tf.has_bn:
+                slabs += [u.in_tf.slab.view(-1), u.in_tf.bwd_slab.view(-1)]
+        ys = [u.y.view(-1) for u in self.units if u.kind == "dense" and u.splits_fwd > 1]
+        regions = self.zero_regions + self.zero_early
+        ptrs = {t.data_ptr() for t in slabs} | {t.data_ptr() for t in ys}
+        if any(r.data_ptr() not in ptrs for r in regions) or len(slabs) > 4 or len(ys) > 4:
+            return
+        if any(t.numel() % 4 or t.data_ptr() % 16 for t in ys):
+            return
+        sl = e.slots
+        s0 = sl[0] if sl.shape[0] > 0 else None
+        s1 = sl[1] if sl.shape[0] > 1 else None
+
+        def slot(s, name):
+            return None if s is None else s[offs[name]:]
+
+        self.tail_params = [(self.views[n], slot(s0, n), slot(s1, n), src, S, ld, self.views[n].numel(), z)
+                            for n, src, S, ld, z in params]
+        self.tail_zero = [t for t in slabs if any(r.data_ptr() == t.data_ptr() for r in regions)]
+        self.fwd_zero = [t for t in ys if any(r.data_ptr() == t.data_ptr() for r in regions)]
+        self.head_params = (self.views["head.weight"], self.views["head.bias"], slot(s0, "head.weight"),
+                            slot(s1, "head.weight"), slot(s0, "head.bias"), slot(s1, "head.bias"))
+        self.tail_tk = torch.zeros(int(self.lib.csa_conv_pair_tail_ticket_words()), dtype=torch.int32,
+                                   device=e.device)                           # spread tickets
+        self.tail_err = torch.zeros(1, dtype=torch.int32, device=e.device)
+        # the parameter workgroups' table (one entry per 256 elements of a parameter)
+        tp = self.tail_params
+        n = len(tp)
+        P = C.c_void_p
+        ns = (C.c_int * 8)(*[t[6] for t in tp])
+        nbytes = int(self.lib.csa_conv_pair_tail_table_bytes(ns, n))
+        self.tail_table = torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=e.device)
+        torch.cuda.synchronize(e.device)
+        self.tail_blocks = int(self.lib.csa_conv_pair_tail_plan(
+            K.ptr(self.tail_table), e.opt_id, n, (P * 8)(*[t[0].data_ptr() for t in tp]),
+            (P * 8)(*[K.ptr(t[1]) for t in tp]), (P * 8)(*[K.ptr(t[2]) for t in tp]),
+            (P * 8)(*[t[3].data_ptr() for t in tp]), (C.c_int * 8)(*[t[4] for t in tp]),
+            (C.c_int * 8)(*[t[5] for t in tp]), ns, (C.c_int * 8)(*[t[7] for t in tp])))
+        if self.tail_blocks < 1:
+            raise RuntimeError(f"conv_pair_tail_plan failed: {self.tail_blocks}")
+        self.tail = True
+
+    def _tail_set(self) -> None:
+        """Record the tail of this step's pair backward launch (host state, like the
+        deferred dense segments) and switch the head segment to in-place updates."""
+        e, lib = self.e, self.lib
+        hw, hb, hs0w, hs1w, hs0b, hs1b = self.head_params
+        self._rc(lib.csa_dense_update_head_params(K.ptr(hw), K.ptr(hb), K.ptr(hs0w), K.ptr(hs1w), K.ptr(hs0b),
+                                                  K.ptr(hs1b)), "dense_update_head_params")
+        P = C.c_void_p
+        rc = lib.csa_conv_pair_tail_set(
+            K.ptr(self.tail_tk), K.ptr(self.tail_err), e.opt_id, float(e.lr), K.ptr(e.dstep),
+            K.ptr(self.tail_table), self.tail_blocks,
+            len(self.tail_zero), (P * 4)(*[t.data_ptr() for t in self.tail_zero]),
+            (C.c_long * 4)(*[t.numel() for t in self.tail_zero]),
+            K.ptr(e.data.images), K.ptr(e.data.labels), K.ptr(e.stream.rows), K.ptr(e.stream.cursor), self.B,
+            self.stage_img.shape[1], K.ptr(self.stage_img), K.ptr(self.stage_lbl))
+        self._rc(rc, "conv_pair_tail_set")
+
+    def tail_error(self) -> int:
+        """Nonzero when a tail workgroup's bounded wait timed out (its work did not run)."""
+        return int(self.tail_err.item()) if getattr(self, "tail", False) else 0
 
     # ------------------------------------------------------------------ deterministic mode
     def _check_det(self) -> None:
@@ -867,6 +980,8 @@ class HipProgram:
         for r in self.zero_regions + self.zero_early + self.stripe_bufs:
             r.zero_()
         self.e.flat_grad.zero_()
+        if getattr(self, "tail", False):
+            self.tail_tk.zero_()            # (an aborted launch must not leave tickets behind)
 
     # ------------------------------------------------------------------ batch staging
     def _plan_stage(self) -> None:
@@ -1155,6 +1270,11 @@ class HipProgram:
                 main.wait_stream(self.lr_side)
         else:
             e.after_backward_sync()
+        if getattr(self, "tail", False):
+            # the pair backward's tail did the optimizer launch's work
+            if lib.csa_dense_update_pending() or lib.csa_conv_pair_tail_pending():
+                raise RuntimeError("pair-backward tail / deferred updates not consumed")
+            return
         self._optimizer(st)
 
     # ------------------------------------------------------------------ forward
@@ -1180,13 +1300,18 @@ class HipProgram:
             nt = self.units[2].in_tf if len(self.units) > 2 else self.head_tf
             oslab = nt.slab if nt.has_bn and not self._eval_bn else None
             simg, srows, scur = self._batch_src()
+            # (the tail program: the dense split-K outputs of this step, zeroed by the pair
+            # forward's threads — not when predicting, which zeroes them itself)
+            fz = [] if getattr(self, "_predicting", False) else getattr(self, "fwd_zero", [])
             self._rc(lib.csa_conv_pair_fwd(
                 K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
                 K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
                 _act_id(ua.act), _alpha(ua.act),
                 K.ptr(V[f"{ub.layer.name}.weight"]), K.ptr(V.get(f"{ub.layer.name}.bias")) if ub.layer.spec.bias else None,
                 _act_id(ub.act), _alpha(ub.act), K.ptr(ub.y), K.ptr(ub.argmax), K.ptr(oslab),
-                nt.prod_rows if self.det else self.lib.csa_conv_fwd_nslab(None, None), st), "conv_pair_fwd")
+                nt.prod_rows if self.det else self.lib.csa_conv_fwd_nslab(None, None),
+                (C.c_void_p * 4)(*[t.data_ptr() for t in fz]), (C.c_long * 4)(*[t.numel() for t in fz]), len(fz),
+                st), "conv_pair_fwd")
             if oslab is not None and self.det:
                 self._row_fold(oslab, nt.prod_rows, oslab.shape[1] * oslab.shape[2], oslab, 0, st)
             if oslab is not None and self.sync_bn:
@@ -1392,6 +1517,8 @@ class HipProgram:
             rm = getattr(self.model, f"bn{nt.norm.index}_mean")
             rv = getattr(self.model, f"bn{nt.norm.index}_var")
         simg, srows, scur = self._batch_src()
+        if getattr(self, "tail", False):
+            self._tail_set()
         self._rc(lib.csa_conv_pair_bwd(
             K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
             K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
