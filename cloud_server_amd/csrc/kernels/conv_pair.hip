@@ -1111,7 +1111,6 @@ __host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 
 template <int KBH, int KBW>
 __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z) {
   const CPGeom& g = a.g;
-  cp_zero_early(z);
   __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
   __shared__ int s_koffA[CPV_MAXKA];                    // x-tile offset of conv-A tap k
   __shared__ float s_b[CPV_MAXC1 + CPV_MAXC2];
@@ -1289,6 +1288,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z) 
       else atomicAdd(&row[tid], acc);
     }
   }
+  cp_zero_early(z);                   // (at the end: stores in front would delay the loads)
   CP_STAMP(4);
 }
 

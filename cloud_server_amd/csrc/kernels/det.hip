@@ -62,9 +62,70 @@ __global__ __launch_bounds__(RF_COLS * RF_SL) void rows_fold_kernel(const float*
     for (int r = r0; r < r1; ++r) const_cast<float*>(src)[(long)r * ld + j] = 0.f;
 }
 
+// Several folds in ONE launch (the data-parallel program folds the conv pair's four striped
+// gradients into the flat gradient before their bucket is exchanged: four launches of a
+// couple of µs each were serial links of the step).  Block b belongs to the job whose
+// block range holds it; the job is chosen by uniform selects of named fields (no argument
+// arrays indexed at run time: those are copied to scratch by every workgroup).
+struct RFJob { const float* src; long ld; long n; float* dst; int R; int zero; int blk0; int pad; };
+struct RFMulti { RFJob j0, j1, j2, j3; int njobs; };
+
+__global__ __launch_bounds__(RF_COLS * RF_SL) void rows_fold_multi_kernel(RFMulti a) {
+  __shared__ float s_part[RF_SL][RF_COLS];
+  const int b = blockIdx.x;
+  RFJob J = a.j0;
+  if (a.njobs > 1 && b >= a.j1.blk0) J = a.j1;
+  if (a.njobs > 2 && b >= a.j2.blk0) J = a.j2;
+  if (a.njobs > 3 && b >= a.j3.blk0) J = a.j3;
+  const int c = threadIdx.x % RF_COLS, sl = threadIdx.x / RF_COLS;
+  const long j = (long)(b - J.blk0) * RF_COLS + c;
+  const int per = (J.R + RF_SL - 1) / RF_SL;
+  const int r0 = sl * per, r1 = min(J.R, r0 + per);
+  const long jj = j < J.n ? j : J.n - 1;
+  float acc = 0.f;
+  for (int r = r0; r < r1; r += RF_U) {
+    float v[RF_U];
+#pragma unroll
+    for (int u = 0; u < RF_U; ++u) v[u] = J.src[(long)min(r + u, r1 - 1) * J.ld + jj];
+#pragma unroll
+    for (int u = 0; u < RF_U; ++u) pin(v[u]);
+#pragma unroll
+    for (int u = 0; u < RF_U; ++u)
+      if (r + u < r1) acc += v[u];
+  }
+  s_part[sl][c] = acc;
+  __syncthreads();
+  if (sl == 0 && j < J.n) {
+    float t = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < RF_SL; ++s2) t += s_part[s2][c];
+    J.dst[j] = t;
+  }
+  if (J.zero && j < J.n)
+    for (int r = r0; r < r1; ++r) const_cast<float*>(J.src)[(long)r * J.ld + j] = 0.f;
+}
+
 }  // namespace csa
 
 using namespace csa;
+
+// Up to 4 csa_rows_fold jobs as one launch (same arithmetic, same fixed order).
+CSA_API int csa_rows_fold_multi(int njobs, const float* const* src, const long* ld, const int* R, const long* n,
+                                float* const* dst, const int* zero_src, hipStream_t st) {
+  if (njobs < 1 || njobs > 4) return -1;
+  RFMulti a{};
+  RFJob* js[4] = {&a.j0, &a.j1, &a.j2, &a.j3};
+  int blk = 0;
+  for (int k = 0; k < njobs; ++k) {
+    if (!src[k] || !dst[k] || R[k] < 1 || n[k] < 1 || ld[k] < n[k]) return -1;
+    if (zero_src[k] && dst[k] >= src[k] && dst[k] < src[k] + (long)R[k] * ld[k]) return -2;
+    *js[k] = RFJob{src[k], ld[k], n[k], dst[k], R[k], zero_src[k], blk, 0};
+    blk += (int)((n[k] + RF_COLS - 1) / RF_COLS);
+  }
+  a.njobs = njobs;
+  hipLaunchKernelGGL(rows_fold_multi_kernel, dim3((unsigned)blk), dim3(RF_COLS * RF_SL), 0, st, a);
+  return (int)hipGetLastError();
+}
 
 CSA_API void csa_set_deterministic(int on) { g_csa_det = on ? 1 : 0; }
 CSA_API int csa_deterministic() { return g_csa_det; }

@@ -339,6 +339,7 @@ class HipProgram:
             else:
                 self.e.sync.allreduce(self.e.flat_grad, b[0], b[1])
 
+
     # ------------------------------------------------------------------ fused updates
     def _plan_fused(self) -> None:
         """On one GPU the dense weight gradients feed nothing but the optimizer: such a
@@ -1531,11 +1532,18 @@ class HipProgram:
             min(ua.wg_stripes, ub.wg_stripes), K.ptr(self.pair_tabs), st), "conv_pair_bwd")
         self._sync_bn_param_grads(nt)
         if ua.row_fold:
+            # the pair's (up to) four striped gradients into the flat gradient: ONE launch
+            jobs = []
             for u in (ua, ub):
                 lp = u.layer
-                self._row_fold(u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"], 1, st)
+                jobs.append((u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], G[f"{lp.name}.weight"]))
                 if u.db_acc is not None:
-                    self._row_fold(u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"], 1, st)
+                    jobs.append((u.db_acc, u.wg_stripes, u.db_acc.shape[1], G[f"{lp.name}.bias"]))
+            n = len(jobs)
+            self._rc(lib.csa_rows_fold_multi(
+                n, (C.c_void_p * 4)(*[j[0].data_ptr() for j in jobs]), (C.c_long * 4)(*[j[2] for j in jobs]),
+                (C.c_int * 4)(*[j[1] for j in jobs]), (C.c_long * 4)(*[j[2] for j in jobs]),
+                (C.c_void_p * 4)(*[j[3].data_ptr() for j in jobs]), (C.c_int * 4)(*([1] * n)), st), "rows_fold_multi")
 
     def _conv_det_folds(self, u: Unit, tf, st) -> None:
         """Deterministic mode, after a conv unit's backward: its BN-backward rows (one per
@@ -1697,6 +1705,11 @@ class HipProgram:
         return segs
 
     def _optimizer(self, st) -> None:
+        """The flat optimizer launch: the update of every parameter no fused kernel updated
+        plus the step's side jobs (accumulator zeroing, folds, metrics, cursor, staging).
+        (Round 5 measured per-bucket updates on the DP side stream, each right after its
+        bucket's exchange: 0.137 against 0.102 ms/step at world 1 — the graph's branches
+        serialised behind them: profiles/r5_notes.md.)"""
         e, lib = self.e, self.lib
         lo, hi = e.sync.shard_range()
         s0 = e.slots[0] if e.slots.shape[0] > 0 else None
@@ -1711,8 +1724,9 @@ class HipProgram:
             w, g = e.flat[lo:hi], e.grad_shard
         else:
             w, g = e.flat, e.flat_grad
-        zp = (C.c_void_p * 16)(*[r.data_ptr() for r in self.zero_regions])
-        zn = (C.c_long * 16)(*[r.numel() for r in self.zero_regions])
+        zregs = self.zero_regions
+        zp = (C.c_void_p * 16)(*[r.data_ptr() for r in zregs])
+        zn = (C.c_long * 16)(*[r.numel() for r in zregs])
         folds = []          # striped conv weight gradients / head partials -> summed inside the update
         offs = self.model.state.offsets
         for u in self.units:
@@ -1766,7 +1780,7 @@ class HipProgram:
         self._rc(lib.csa_optimizer2s(
             e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), slo, shi, len(segs),
             0 if self.ps_mode else 1, float(e.lr), K.ptr(e.dstep),
-            zp, zn, len(self.zero_regions), fo, fn, fs, fS, fl, fz, len(folds), klo, khi, len(keep),
+            zp, zn, len(zregs), fo, fn, fs, fS, fl, fz, len(folds), klo, khi, len(keep),
             *met, *cursor_args, *stage, st), "optimizer")
         if getattr(self, "hfuse", False) and lib.csa_dense_update_pending():
             raise RuntimeError("deferred dense updates were not consumed by the pair backward")
