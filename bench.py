@@ -147,7 +147,8 @@ def main() -> int:
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     # auto: "lowrank" data parallelism when world > 1 (dense weight gradients from
     # all-gathered GEMM operands instead of an 8 MB all-reduce; parallel/dp.py), else plain
-    ap.add_argument("--strategy", default="auto", choices=["auto", "allreduce", "ps", "lowrank"])
+    ap.add_argument("--strategy", default="auto",
+                    choices=["auto", "allreduce", "allreduce:hf", "ps", "ps:hf", "lowrank"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--optimizer", default="AdagradOptimizer")
     ap.add_argument("--jobs", type=int, default=1, help="independent jobs packed on one GPU")

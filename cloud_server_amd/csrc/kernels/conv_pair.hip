@@ -944,8 +944,8 @@ __host__ __device__ __forceinline__ unsigned* cpt_word(unsigned* tk, int count, 
 // argument struct to scratch in EVERY workgroup of the launch.
 struct CPTailSeg {
   float* w; float* s0; float* s1; float* src;
-  int S, ld, n, zero, base, pad0, pad1, pad2;
-};
+  int S, ld, n, zero, base, store, pad1, pad2;   // store: w[i] = the sum (a gradient fold,
+};                                               // data parallel: exchanged before the update)
 struct CPTail {
   int on, param_blocks, stage_blocks;
   unsigned* tk;                     // [CPT_TK_WORDS]: pair workgroups done | image tiles
@@ -1001,10 +1001,14 @@ __device__ __forceinline__ void cp_tail_params(const CPTail& t, int k) {
     float gsum = 0.f;
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) gsum += s2 < d.S ? v[s2] : 0.f;
-    opt_update(t.opt, opt_step_lr(t.opt, t.lr, t.step), wv, gsum, z0, z1);
-    d.w[i] = wv;
-    if (nslot >= 1) d.s0[i] = z0;
-    if (nslot >= 2) d.s1[i] = z1;
+    if (d.store) {
+      d.w[i] = gsum;
+    } else {
+      opt_update(t.opt, opt_step_lr(t.opt, t.lr, t.step), wv, gsum, z0, z1);
+      d.w[i] = wv;
+      if (nslot >= 1) d.s0[i] = z0;
+      if (nslot >= 2) d.s1[i] = z1;
+    }
     if (d.zero)
 #pragma unroll
       for (int s2 = 0; s2 < 16; ++s2)
@@ -1864,15 +1868,15 @@ CSA_API long csa_conv_pair_tail_table_bytes(const int* n, int nseg) {
 
 CSA_API int csa_conv_pair_tail_plan(void* table, int opt, int nseg, float* const* w, float* const* s0,
                                     float* const* s1, float* const* src, const int* S, const int* ld, const int* n,
-                                    const int* zero) {
+                                    const int* zero, int store) {
   if (!table || nseg < 1 || nseg > CPT_MAXSEG) return -1;
-  const int ns = opt_nslots(opt);
+  const int ns = store ? 0 : opt_nslots(opt);
   std::vector<CPTailSeg> segs;
   for (int k = 0; k < nseg; ++k) {
     if (!w[k] || !src[k] || S[k] < 1 || S[k] > 16 || n[k] < 1 || ld[k] < n[k]) return -2;
     if ((ns >= 1 && !s0[k]) || (ns >= 2 && !s1[k])) return -2;
     for (int base = 0; base < n[k]; base += CP_THREADS)
-      segs.push_back(CPTailSeg{w[k], s0[k], s1[k], src[k], S[k], ld[k], n[k], zero[k], base, 0, 0, 0});
+      segs.push_back(CPTailSeg{w[k], s0[k], s1[k], src[k], S[k], ld[k], n[k], zero[k], base, store ? 1 : 0, 0, 0});
   }
   if (hipMemcpy(table, segs.data(), segs.size() * sizeof(CPTailSeg), hipMemcpyHostToDevice) != hipSuccess) return -3;
   return (int)segs.size();

@@ -288,6 +288,17 @@ CSA_API int csa_dense_update_defer(const float* dY, float* W, float* bias, int M
 
 CSA_API int csa_dense_update_pending() { return g_du_def.n; }
 
+// The LAST deferred segment in gradient mode (data parallel): its weight / bias gradients
+// are stored whole into gW / gb (the flat gradient, exchanged before the optimizer) instead
+// of updating W / b.  Defer it with the slot-free rule (opt 0): no slot is read.
+CSA_API int csa_dense_update_grad_mode(float* gW, float* gb) {
+  if (g_du_def.n < 1 || !gW || !gb) return -1;
+  DUArgs& a = g_du_def.seg[g_du_def.n - 1];
+  if (opt_nslots(a.opt) != 0) return -2;
+  a.gW = gW; a.gb = gb;
+  return 0;
+}
+
 // The deferred head segment updates the head's parameters in place (w [K][10], b [10] and
 // their optimizer slots) instead of storing dWh / dbh: the pair-backward tail program.
 CSA_API int csa_dense_update_head_params(float* hw, float* hb, float* hs0w, float* hs1w, float* hs0b, float* hs1b) {

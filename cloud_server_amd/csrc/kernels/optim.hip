@@ -39,6 +39,12 @@ struct KeepList { long lo[MAXK], hi[MAXK]; int count; };
 
 struct SegList { long lo[MAXSEG]; long start4[MAXSEG + 1]; int count; };
 
+// The fast path's segments (no folds): flat [lo, lo + 4 n) with a per-segment rule for the
+// gradient — zero it after reading (an accumulator) or keep it (stored whole every step) —
+// instead of a per-element search of the keep list.
+constexpr int MAXFS = 32;
+struct FastSegs { long lo4[MAXFS]; long start4[MAXFS + 1]; int zero[MAXFS]; int count; };
+
 struct MetricFold {        // head partials -> ring[(step - 1) % ring]
   const float* loss; const int* corr; int parts; float div;
   float* ring_loss; int* ring_correct; int ring;
@@ -77,6 +83,8 @@ struct OptArgs {
   int64_t* cursor;                 // batch-stream cursor: += 1 (mod cursor_wrap) per step
   long cursor_wrap;
   BatchStage stage;                // next step's batch gathered by the trailing blocks
+  int fast;                        // no folds: the FastSegs loop (two float4 per thread in flight)
+  FastSegs fs;
 };
 
 constexpr int MAXS = 16;   // stripes / partial rows per folded gradient
@@ -128,6 +136,46 @@ __constant__ long long* g_opt_dbg = nullptr;
   do {                                                                                       \
     if (g_opt_dbg && threadIdx.x == 0) g_opt_dbg[blockIdx.x * 4 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
+
+// The launch's side jobs after the update: zero the next step's accumulators, write the
+// metric ring, advance the cursor.
+__device__ __forceinline__ void opt_duties(const OptArgs& a, long tid, long nth) {
+  // zero accumulators for the next step
+  for (int z = 0; z < a.z.count; ++z) {
+    float* p = a.z.p[z];
+    const long n = a.z.n[z];
+    for (long i = tid; i < n; i += nth) p[i] = 0.f;
+  }
+  OPT_STAMP(2);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (a.met.parts > 0) {
+      // MAXS partials' loads in flight together per round (a serial load -> add loop is one
+      // memory round trip per partial on the critical path of the whole step)
+      float ls = 0.f;
+      int nc = 0;
+      for (int p0 = 0; p0 < a.met.parts; p0 += MAXS) {
+        float lv[MAXS];
+        int cv[MAXS];
+#pragma unroll
+        for (int p = 0; p < MAXS; ++p) {
+          const int pp = p0 + p < a.met.parts ? p0 + p : 0;
+          lv[p] = a.met.loss[pp];
+          cv[p] = a.met.corr[pp];
+        }
+#pragma unroll
+        for (int p = 0; p < MAXS; ++p)
+          if (p0 + p < a.met.parts) { ls += lv[p]; nc += cv[p]; }
+      }
+      const int pos = (int)((*a.step - 1) % a.met.ring);
+      a.met.ring_loss[pos] = ls / a.met.div;
+      a.met.ring_correct[pos] = nc;
+    }
+    if (a.cursor) {
+      const int64_t c = *a.cursor + 1;
+      *a.cursor = (a.cursor_wrap > 0 && c >= a.cursor_wrap) ? 0 : c;
+    }
+  }
+}
 
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   OPT_STAMP(0);
@@ -204,41 +252,70 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     if (nslot >= 2) s14[i] = s1;
   }
   OPT_STAMP(1);
-  // zero accumulators for the next step
-  for (int z = 0; z < a.z.count; ++z) {
-    float* p = a.z.p[z];
-    const long n = a.z.n[z];
-    for (long i = tid; i < n; i += nth) p[i] = 0.f;
+  opt_duties(a, tid, nth);
+  OPT_STAMP(3);
+}
+
+// No folds (the data-parallel programs): a streaming update over FastSegs, two float4s of
+// every operand in flight per thread, then the same side jobs.  Its own kernel: inside
+// optim_kernel the extra live registers cut that kernel's occupancy to two waves per SIMD.
+__global__ __launch_bounds__(256) void optim_fast_kernel(OptArgs a) {
+  OPT_STAMP(0);
+  const int nmain = (int)gridDim.x - a.stage.blocks;
+  if ((int)blockIdx.x >= nmain) {
+    stage_gather(a.stage, (int)blockIdx.x - nmain);
+    OPT_STAMP(3);
+    return;
   }
-  OPT_STAMP(2);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (a.met.parts > 0) {
-      // MAXS partials' loads in flight together per round (a serial load -> add loop is one
-      // memory round trip per partial on the critical path of the whole step)
-      float ls = 0.f;
-      int nc = 0;
-      for (int p0 = 0; p0 < a.met.parts; p0 += MAXS) {
-        float lv[MAXS];
-        int cv[MAXS];
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long nth = (long)nmain * blockDim.x;
+  const float lr = opt_step_lr(a.opt, a.lr, a.step);
+  float4* w4 = (float4*)a.w;
+  const float4* g4 = (const float4*)a.g;
+  float4* s04 = (float4*)a.s0;
+  float4* s14 = (float4*)a.s1;
+  const int nslot = opt_nslots(a.opt);
+  {
+    // streaming update: each thread keeps two float4s of every operand in flight (the loop
+    // below was one dependent round trip per float4 with a per-element keep search)
+    const long m4 = a.fs.start4[a.fs.count];
+    for (long t0 = tid; t0 < m4; t0 += 2 * nth) {
+      long idx[2];
+      int zg[2];
+      bool ok[2];
+      float4 w[2], g[2], s0[2], s1[2];
 #pragma unroll
-        for (int p = 0; p < MAXS; ++p) {
-          const int pp = p0 + p < a.met.parts ? p0 + p : 0;
-          lv[p] = a.met.loss[pp];
-          cv[p] = a.met.corr[pp];
-        }
-#pragma unroll
-        for (int p = 0; p < MAXS; ++p)
-          if (p0 + p < a.met.parts) { ls += lv[p]; nc += cv[p]; }
+      for (int u = 0; u < 2; ++u) {
+        const long t = t0 + u * nth;
+        ok[u] = t < m4;
+        const long tc = ok[u] ? t : m4 - 1;
+        int k = 0;
+        for (int j = 1; j < a.fs.count; ++j) k = tc >= a.fs.start4[j] ? j : k;
+        idx[u] = a.fs.lo4[k] + (tc - a.fs.start4[k]);
+        zg[u] = a.fs.zero[k];
+        w[u] = w4[idx[u]];
+        g[u] = g4[idx[u]];
+        s0[u] = nslot >= 1 ? s04[idx[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s1[u] = nslot >= 2 ? s14[idx[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      const int pos = (int)((*a.step - 1) % a.met.ring);
-      a.met.ring_loss[pos] = ls / a.met.div;
-      a.met.ring_correct[pos] = nc;
-    }
-    if (a.cursor) {
-      const int64_t c = *a.cursor + 1;
-      *a.cursor = (a.cursor_wrap > 0 && c >= a.cursor_wrap) ? 0 : c;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (!ok[u]) continue;
+        float* wp = (float*)&w[u];
+        const float* gp = (const float*)&g[u];
+        float* sp0 = (float*)&s0[u];
+        float* sp1 = (float*)&s1[u];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) opt_update(a.opt, lr, wp[j], gp[j], sp0[j], sp1[j]);
+        w4[idx[u]] = w[u];
+        if (nslot >= 1) s04[idx[u]] = s0[u];
+        if (nslot >= 2) s14[idx[u]] = s1[u];
+        if (a.gz && zg[u]) reinterpret_cast<float4*>(a.gz)[idx[u]] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
+  OPT_STAMP(1);
+  opt_duties(a, tid, nth);
   OPT_STAMP(3);
 }
 
@@ -372,6 +449,31 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
     a.fold.hi = fold_off[i] + fold_n[i] > a.fold.hi ? fold_off[i] + fold_n[i] : a.fold.hi;
   }
   a.met = MetricFold{met_loss, met_corr, met_parts, met_div, ring_loss, ring_correct, ring};
+  // fast path: no folds -> split the segments at the keep ranges' edges (float4 units)
+  if (nfold == 0) {
+    FastSegs f{};
+    bool fits = true;
+    f.start4[0] = 0;
+    for (int i = 0; i < a.seg.count && fits; ++i) {
+      long x = a.seg.lo[i], end = a.seg.lo[i] + 4 * (a.seg.start4[i + 1] - a.seg.start4[i]);
+      while (x < end && fits) {
+        // the piece [x, y) lies wholly inside a keep range (zero = 0) or wholly outside (1)
+        int inside = -1;
+        long y = end;
+        for (int q = 0; q < nkeep; ++q) {
+          if (x >= keep_lo[q] && x < keep_hi[q]) { inside = q; y = y < keep_hi[q] ? y : keep_hi[q]; }
+          else if (keep_lo[q] > x && keep_lo[q] < y) y = keep_lo[q];
+        }
+        if (f.count >= MAXFS) { fits = false; break; }
+        f.lo4[f.count] = x / 4;
+        f.zero[f.count] = inside < 0 ? 1 : 0;
+        f.start4[f.count + 1] = f.start4[f.count] + (y - x) / 4;
+        ++f.count;
+        x = y;
+      }
+    }
+    if (fits && f.count > 0) { a.fast = 1; a.fs = f; }
+  }
   const long n4 = a.seg.start4[a.seg.count];
   long zmax = 0;
   for (int i = 0; i < nzero; ++i) zmax = zero_ns[i] > zmax ? zero_ns[i] : zmax;
@@ -384,7 +486,15 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   a.stage = make_stage(st_img, st_labels, st_rows, st_cursor, st_B, st_imsz, st_out_img, st_out_lbl);
-  hipLaunchKernelGGL(optim_kernel, dim3(blocks + a.stage.blocks), dim3(256), 0, st, a);
+  if (a.fast) {
+    // half the threads: each keeps two float4s of every operand in flight
+    const long fwork = ((a.fs.start4[a.fs.count] + 1) / 2) > zmax ? (a.fs.start4[a.fs.count] + 1) / 2 : zmax;
+    int fb = (int)((fwork + 255) / 256);
+    fb = fb > cap ? cap : (fb < 1 ? 1 : fb);
+    hipLaunchKernelGGL(optim_fast_kernel, dim3(fb + a.stage.blocks), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(optim_kernel, dim3(blocks + a.stage.blocks), dim3(256), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -80,7 +80,8 @@ _SIGS = {
     "csa_head_debug": (I, [P]),
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P, P, I, P]),
     "csa_conv_pair_tail_table_bytes": (L, [P, I]),
-    "csa_conv_pair_tail_plan": (I, [P, I, I, P, P, P, P, P, P, P, P]),
+    "csa_conv_pair_tail_plan": (I, [P, I, I, P, P, P, P, P, P, P, P, I]),
+    "csa_dense_update_grad_mode": (I, [P, P]),
     "csa_conv_pair_tail_set": (I, [P, P, I, F, P, P, I, I, P, P, P, P, P, P, I, L, P, P]),
     "csa_conv_pair_tail_pending": (I, []),
     "csa_conv_pair_tail_ticket_words": (I, []),

@@ -76,11 +76,15 @@ def lowrank_worth_trying(cfg, world: int) -> bool:
     return t_gemm <= t_links
 
 
-def default_candidates(cfg, world: int) -> Tuple[str, ...]:
+def default_candidates(cfg, world: int, gpu: bool = False) -> Tuple[str, ...]:
     """lowrank where it can win, allreduce, and ps (the parameter-server capability:
     bucketed reduce-scatter to owner shards overlapped with the backward, owner-side
-    optimizer, xGMI all-gather — construct_distribute.py:355-357, 413)."""
-    base = ("allreduce", "ps")
+    optimizer, xGMI all-gather — construct_distribute.py:355-357, 413), each also as its
+    ":hf" program: the one-GPU step's structure (dense weight gradients inside the pair
+    backward launch, fewer and shorter launches) at the price of one exchange after the
+    backward instead of buckets overlapped with it — which wins depends on the link time
+    (``gpu``: the ":hf" programs exist on the HIP program only)."""
+    base = ("allreduce", "allreduce:hf", "ps", "ps:hf") if gpu else ("allreduce", "ps")
     return (("lowrank",) + base) if lowrank_worth_trying(cfg, world) else base
 
 
@@ -91,7 +95,7 @@ def pick_strategy(cfg, ds, ctx: DistContext, candidates: Optional[Sequence[str]]
     if not ctx.enabled:
         return "allreduce", {}
     if candidates is None:
-        candidates = default_candidates(cfg, ctx.world)
+        candidates = default_candidates(cfg, ctx.world, gpu=ctx.device.type == "cuda")
     candidates = tuple(candidates)
     if len(candidates) == 1:
         return candidates[0], {}

@@ -85,6 +85,11 @@ class TrainEngine:
         (``runtime.multijob``): its HIP program uses the packed launch profile."""
         self.cfg = cfg
         self.packed = packed
+        # "<strategy>:hf" — the data-parallel program with the one-GPU step's structure
+        # (dense weight gradients formed inside the pair backward launch, no bucket overlap);
+        # the start-up tuner times it against the overlapped program (parallel/strategy.py)
+        strategy, _, variant = strategy.partition(":")
+        self.dp_variant = variant
         if deterministic_mode() and strategy == "lowrank" and ctx is not None and ctx.enabled:
             # same exact DP math; its gathered-operand GEMMs have no fixed-order variant
             strategy = "allreduce"

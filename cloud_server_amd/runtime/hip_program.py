@@ -211,8 +211,11 @@ class HipProgram:
         # on RCCL (GradSync.rs_choice, decided below): on RCCL the per-owner reduces per
         # bucket measured 0.156 ms/step at world 1 against 0.107 for one reduce-scatter
         # after the backward (profiles/r4_notes.md)
+        # (the ":hf" program forms every dense gradient inside the pair backward launch:
+        # nothing is ready early, one exchange after the backward)
         self.overlap = (e.ctx.enabled and e.sync.strategy in ("allreduce", "ps")
                         and (e.sync.strategy == "allreduce" or e.sync.xgmi is not None)
+                        and not getattr(self, "dp_hf", False)
                         and os.environ.get("CSA_DP_OVERLAP", "1") == "1")
         self.bucket_at: Dict[object, tuple] = {}
         if not self.overlap:
@@ -471,13 +474,18 @@ class HipProgram:
         # (not in the packed profile: there the other jobs' kernels already fill the CUs the
         # pair backward leaves idle, and K = 4 / 8 packs measured 1.10 / 1.12 M samples/s with
         # the deferred updates against 1.17 / 1.23 M without — profiles/r4_multitenant.md)
-        if (self.forward_only or not self.fused or self.det or self.pair is None or self.packed
+        # data parallel ("<strategy>:hf"): the same split in GRADIENT mode — the deferred
+        # segments store dW / db whole into the flat gradient, the pair backward's tail folds
+        # the conv stripes into it, then the exchange and the flat optimizer follow
+        self.dp_hf = bool(self.fused_grad and getattr(self.e, "dp_variant", "") == "hf"
+                          and self.e.sync.strategy in ("allreduce", "ps"))
+        if (self.forward_only or not (self.fused or self.dp_hf) or self.det or self.pair is None or self.packed
                 or os.environ.get("CSA_HFUSE", "1") != "1"):
+            self.dp_hf = False
             return
         dense = [u for u in self.units if u.kind == "dense" and u.fused]
-        if not dense or len(dense) > 4:
-            return
-        if any(u.layer.spec.hidden % 128 for u in dense):
+        if not dense or len(dense) > 4 or any(u.layer.spec.hidden % 128 for u in dense):
+            self.dp_hf = False
             return
         self.hfuse = True
         # the last dense layer's input gradient rides in the head launch (csa_head_dgrad:
@@ -510,7 +518,11 @@ class HipProgram:
         when every other parameter and accumulator is one of those (``CSA_PAIR_TAIL=0``
         restores the optimizer launch)."""
         self.tail = False
+        self.tail_update = False
         self.fwd_zero: List[torch.Tensor] = []
+        if getattr(self, "dp_hf", False):
+            self._plan_tail_fold()
+            return
         if not (getattr(self, "hfuse", False) and getattr(self, "staged", False) and self.head_row
                 and self.pair is not None and os.environ.get("CSA_PAIR_TAIL", "1") == "1"):
             return
@@ -575,19 +587,58 @@ class HipProgram:
             K.ptr(self.tail_table), e.opt_id, n, (P * 8)(*[t[0].data_ptr() for t in tp]),
             (P * 8)(*[K.ptr(t[1]) for t in tp]), (P * 8)(*[K.ptr(t[2]) for t in tp]),
             (P * 8)(*[t[3].data_ptr() for t in tp]), (C.c_int * 8)(*[t[4] for t in tp]),
-            (C.c_int * 8)(*[t[5] for t in tp]), ns, (C.c_int * 8)(*[t[7] for t in tp])))
+            (C.c_int * 8)(*[t[5] for t in tp]), ns, (C.c_int * 8)(*[t[7] for t in tp]), 0))
         if self.tail_blocks < 1:
             raise RuntimeError(f"conv_pair_tail_plan failed: {self.tail_blocks}")
+        self.tail = self.tail_update = True
+
+    def _plan_tail_fold(self) -> None:
+        """The ":hf" data-parallel program's tail: fold the pair's weight-gradient stripes
+        into the flat gradient (stored sums, no update) before the exchange — the optimizer
+        launch after the exchange keeps the updates, zeroing and staging."""
+        e = self.e
+        ua, ub = self.units[0], self.units[1]
+        if not (getattr(ua, "tail_fold", False) and ua.wg_stripes > 1 and ua.wg_stripes <= 16):
+            raise Unsupported("data-parallel :hf program: the pair stripes need the tail fold")
+        G = self.gviews
+        jobs = []
+        for u in (ua, ub):
+            lp = u.layer
+            jobs.append((G[f"{lp.name}.weight"].view(-1), u.dw_acc, u.wg_stripes, u.dw_acc.shape[1]))
+            if u.db_acc is not None:
+                jobs.append((G[f"{lp.name}.bias"].view(-1), u.db_acc, u.wg_stripes, u.db_acc.shape[1]))
+        self.tail_tk = torch.zeros(int(self.lib.csa_conv_pair_tail_ticket_words()), dtype=torch.int32,
+                                   device=e.device)
+        self.tail_err = torch.zeros(1, dtype=torch.int32, device=e.device)
+        P = C.c_void_p
+        n = len(jobs)
+        ns = (C.c_int * 8)(*[j[0].numel() for j in jobs])
+        nbytes = int(self.lib.csa_conv_pair_tail_table_bytes(ns, n))
+        self.tail_table = torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=e.device)
+        torch.cuda.synchronize(e.device)
+        self.tail_blocks = int(self.lib.csa_conv_pair_tail_plan(
+            K.ptr(self.tail_table), 0, n, (P * 8)(*[j[0].data_ptr() for j in jobs]), (P * 8)(), (P * 8)(),
+            (P * 8)(*[j[1].data_ptr() for j in jobs]), (C.c_int * 8)(*[j[2] for j in jobs]),
+            (C.c_int * 8)(*[j[3] for j in jobs]), ns, (C.c_int * 8)(*([1] * n)), 1))
+        if self.tail_blocks < 1:
+            raise RuntimeError(f"conv_pair_tail_plan failed: {self.tail_blocks}")
+        self.tail_zero = []
         self.tail = True
 
     def _tail_set(self) -> None:
         """Record the tail of this step's pair backward launch (host state, like the
         deferred dense segments) and switch the head segment to in-place updates."""
         e, lib = self.e, self.lib
+        P = C.c_void_p
+        if not self.tail_update:           # the ":hf" data-parallel fold: nothing else
+            self._rc(lib.csa_conv_pair_tail_set(
+                K.ptr(self.tail_tk), K.ptr(self.tail_err), 0, 0.0, K.ptr(e.dstep), K.ptr(self.tail_table),
+                self.tail_blocks, 0, (P * 4)(), (C.c_long * 4)(), None, None, None, None, 0, 0, None, None),
+                "conv_pair_tail_set")
+            return
         hw, hb, hs0w, hs1w, hs0b, hs1b = self.head_params
         self._rc(lib.csa_dense_update_head_params(K.ptr(hw), K.ptr(hb), K.ptr(hs0w), K.ptr(hs1w), K.ptr(hs0b),
                                                   K.ptr(hs1b)), "dense_update_head_params")
-        P = C.c_void_p
         rc = lib.csa_conv_pair_tail_set(
             K.ptr(self.tail_tk), K.ptr(self.tail_err), e.opt_id, float(e.lr), K.ptr(e.dstep),
             K.ptr(self.tail_table), self.tail_blocks,
@@ -911,7 +962,11 @@ class HipProgram:
                 # backward took 37 us instead of 25)
                 # — and every conv unit's in deterministic mode (one stripe per wgrad workgroup)
                 in_pair = self.pair is not None and k < 2
-                u.row_fold = self.det or (in_pair and self.e.ctx.enabled)
+                # (":hf": the pair backward's tail folds the stripes into the flat gradient)
+                u.tail_fold = in_pair and getattr(self, "dp_hf", False)
+                u.row_fold = self.det or (in_pair and self.e.ctx.enabled and not u.tail_fold)
+                if u.tail_fold:
+                    S = self.WGRAD_STRIPES
                 if u.row_fold:
                     if not self.det:
                         S = self.WGRAD_STRIPES
@@ -925,7 +980,7 @@ class HipProgram:
                     fold_budget -= nf
                 u.wg_stripes = S
                 nw = self.gviews[f"{lp.name}.weight"].numel()
-                if S > 1:       # zeroed by the optimizer's fold (their only reader)
+                if S > 1:       # zeroed by the fold that reads them (their only reader)
                     u.dw_acc = torch.zeros(S, nw, device=self.e.device)
                     u.db_acc = torch.zeros(S, lp.spec.cout, device=self.e.device) if lp.spec.bias else None
                     self.stripe_bufs += [t for t in (u.dw_acc, u.db_acc) if t is not None]
@@ -1272,10 +1327,10 @@ class HipProgram:
         else:
             e.after_backward_sync()
         if getattr(self, "tail", False):
-            # the pair backward's tail did the optimizer launch's work
             if lib.csa_dense_update_pending() or lib.csa_conv_pair_tail_pending():
                 raise RuntimeError("pair-backward tail / deferred updates not consumed")
-            return
+            if self.tail_update:
+                return                      # the pair backward's tail did the optimizer's work
         self._optimizer(st)
 
     # ------------------------------------------------------------------ forward
@@ -1637,12 +1692,21 @@ class HipProgram:
         if self.hfuse:
             # weight gradient + update deferred into the pair backward launch; the input
             # gradient (+ transform backward + BN statistics) now
-            rc = lib.csa_dense_update_defer(
-                K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
-                B, fin, fout, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
-                K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
-                K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
-                1.0, *head)
+            if self.dp_hf:
+                # gradient mode: dW / db stored whole into the flat gradient (slot-free rule)
+                G = self.gviews
+                rc = lib.csa_dense_update_defer(
+                    K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
+                    B, fin, fout, K.ptr(xw), 0, 0.0, K.ptr(e.dstep), None, None, None, None, 1.0, *head)
+                if rc >= 0:
+                    rc = lib.csa_dense_update_grad_mode(K.ptr(G[f"{lp.name}.weight"]), K.ptr(G[f"{lp.name}.bias"]))
+            else:
+                rc = lib.csa_dense_update_defer(
+                    K.ptr(u.dy), K.ptr(self.views[f"{lp.name}.weight"]), K.ptr(self.views[f"{lp.name}.bias"]),
+                    B, fin, fout, K.ptr(xw), e.opt_id, float(e.lr), K.ptr(e.dstep),
+                    K.ptr(s0[ow:]) if s0 is not None else None, K.ptr(s1[ow:]) if s1 is not None else None,
+                    K.ptr(s0[ob:]) if s0 is not None else None, K.ptr(s1[ob:]) if s1 is not None else None,
+                    1.0, *head)
             if rc < 0:
                 raise RuntimeError(f"dense_update_defer failed: {rc}")
             if prev is not None and not (self.head_dgrad and u is self.units[-1]):
@@ -1730,7 +1794,8 @@ class HipProgram:
         folds = []          # striped conv weight gradients / head partials -> summed inside the update
         offs = self.model.state.offsets
         for u in self.units:
-            if u.kind == "conv" and u.wg_stripes > 1 and not getattr(u, "row_fold", False):
+            if (u.kind == "conv" and u.wg_stripes > 1 and not getattr(u, "row_fold", False)
+                    and not getattr(u, "tail_fold", False)):
                 lp = u.layer
                 folds.append((offs[f"{lp.name}.weight"], u.dw_acc.shape[1], u.dw_acc, u.wg_stripes, u.dw_acc.shape[1], 1))
                 if u.db_acc is not None:

@@ -211,3 +211,31 @@ def test_capture_right_after_eager_collectives(pg, monkeypatch, strategy):
     torch.cuda.synchronize()
     assert a.host_step == b.host_step == 16
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
+
+
+@pytest.mark.parametrize("strategy", ["allreduce:hf", "ps:hf"])
+def test_hf_programs_match_single_gpu(pg, monkeypatch, strategy):
+    """the data-parallel program with the one-GPU step's structure — fc2's
+    input gradient in the head launch, fc1's input gradient alone, both dense weight
+    gradients formed in GRADIENT mode as extra workgroups of the pair backward (stored whole
+    into the flat gradient), the conv stripes folded by that launch's tail — then the
+    exchange and the flat optimizer; world 1 must reproduce the single-GPU step."""
+    monkeypatch.setenv("CSA_XGMI", "0")
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
+    assert a.backend == "hip", a.fallback_reason
+    p = a.program
+    assert p.dp_hf and p.hfuse and p.head_dgrad and p.tail and not p.tail_update and not p.overlap
+    assert a.sync.strategy == strategy.split(":")[0]
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for _ in range(4):
+        a.step(); b.step()
+    a.run_steps(16); b.run_steps(16)
+    torch.cuda.synchronize()
+    assert a.host_step == b.host_step == 20 and int(a.dstep.item()) == 20
+    assert p.tail_error() == 0
+    torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
+    ma, mb = a.metrics_since(0), b.metrics_since(0)
+    assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
