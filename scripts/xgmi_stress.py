@@ -35,7 +35,15 @@ def worker(rank, world, port, steps, strategy, q):
         ctx = DistContext(rank=rank, world=world, local_rank=0, backend="nccl", device=dev)
         eng = TrainEngine(cfg, synthetic_mnist(4000, seed=0), device="cuda:0", ctx=ctx, backend="hip",
                           strategy=strategy)
-        assert eng.sync.xgmi is not None and eng.program.overlap, (eng.sync.xgmi_reason, eng.program.overlap)
+        if strategy == "async_ps":
+            assert eng.aps is not None and type(eng.aps).__name__ == "AsyncPSDevice"
+        else:
+            assert eng.sync.xgmi is not None and eng.program.overlap, (eng.sync.xgmi_reason, eng.program.overlap)
+
+        def poisoned() -> bool:
+            if eng.aps is not None:
+                return bool(eng.aps.error())
+            return any(c.error() for c in eng.sync.xgmi.channels.values())
         eng.step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -50,13 +58,20 @@ def worker(rank, world, port, steps, strategy, q):
             done += n
             torch.cuda.synchronize()
             chunks.append(round((time.perf_counter() - tc) * 1e3 / n, 3))
-            if any(c.error() for c in eng.sync.xgmi.channels.values()):
+            if poisoned():
                 bad = True
                 break
         dt = time.perf_counter() - t0
         res = {"ok": not bad, "steps": done, "ms_per_step": round(dt * 1e3 / max(done - 1, 1), 3),
-               "chunk_ms": chunks,
-               "blocks": {t: c.blocks_for(c.slot_bytes) for t, c in eng.sync.xgmi.channels.items()}}
+               "chunk_ms": chunks}
+        if eng.aps is not None:
+            res.update(staleness=eng.staleness(), aps_blocks=eng.aps.nb)
+            eng.finish_async()
+            eng.close()
+            dist.destroy_process_group()
+            q.put((rank, res))
+            return
+        res["blocks"] = {t: c.blocks_for(c.slot_bytes) for t, c in eng.sync.xgmi.channels.items()}
         if bad:
             res["timeouts"] = {t: c.diag_summary() for t, c in eng.sync.xgmi.channels.items()}
             os.makedirs("gpurun_out", exist_ok=True)
