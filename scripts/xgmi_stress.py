@@ -18,7 +18,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def worker(rank, world, port, steps, strategy, q):
+def worker(rank, world, port, steps, strategy, q, chunk=25):
     import torch
     import torch.distributed as dist
     os.environ.update(CSA_XGMI="1", LOCAL_WORLD_SIZE=str(world), HSA_ENABLE_IPC_MODE_LEGACY="0")
@@ -38,7 +38,8 @@ def worker(rank, world, port, steps, strategy, q):
         if strategy == "async_ps":
             assert eng.aps is not None and type(eng.aps).__name__ == "AsyncPSDevice"
         else:
-            assert eng.sync.xgmi is not None and eng.program.overlap, (eng.sync.xgmi_reason, eng.program.overlap)
+            assert eng.sync.xgmi is not None, eng.sync.xgmi_reason
+            assert eng.program.overlap or os.environ.get("CSA_DP_OVERLAP") == "0"
 
         def poisoned() -> bool:
             if eng.aps is not None:
@@ -51,7 +52,7 @@ def worker(rank, world, port, steps, strategy, q):
         bad = False
         chunks = []                          # ms per step of each 25-step chunk
         while done < steps:
-            n = min(25, steps - done)
+            n = min(chunk, steps - done)
             tc = time.perf_counter()
             for _ in range(n):
                 eng.step()
@@ -90,12 +91,13 @@ def main() -> int:
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--strategy", default="allreduce")
+    ap.add_argument("--chunk", type=int, default=25, help="steps enqueued between host syncs")
     a = ap.parse_args()
     import torch.multiprocessing as mp
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, a.world, port, a.steps, a.strategy, q)) for r in range(a.world)]
+    ps = [ctx.Process(target=worker, args=(r, a.world, port, a.steps, a.strategy, q, a.chunk)) for r in range(a.world)]
     for p in ps:
         p.start()
     res = {}
