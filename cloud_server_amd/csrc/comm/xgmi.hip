@@ -69,6 +69,35 @@ struct XgArgs {
 
 constexpr int XG_DIAG = 8;
 
+// native 16-byte vectors for the per-rank register arrays (HIP's uint4 / float4 classes
+// kept those arrays in scratch)
+typedef unsigned xu4 __attribute__((ext_vector_type(4)));
+typedef float xf4 __attribute__((ext_vector_type(4)));
+
+// Element i of a kernarg pointer table without indexing it dynamically: a runtime index
+// into the by-value XgArgs made the compiler copy the struct to scratch in every lane
+// (144 B/lane; a scratch-using spinning kernel beside another process's queue is what the
+// round-5 stall traces point at).  With a uniform i this is a chain of scalar selects.
+template <class T>
+__device__ __forceinline__ T xg_pick(T const (&v)[XG_MAXR], int i) {
+  T x = v[0];
+#pragma unroll
+  for (int k = 1; k < XG_MAXR; ++k)
+    if (i == k) x = v[k];
+  return x;
+}
+
+// The segment holding byte `off` of the packed message (per lane: unrolled selects, no
+// dynamic index into the kernarg segment table).
+struct XgPos { const char* src; char* dst; long so; long bytes; };
+__device__ __forceinline__ XgPos xg_pos(const XgArgs& a, long off) {
+  XgPos p{a.seg[0].src, a.seg[0].dst, off - a.seg[0].off, a.seg[0].bytes};
+#pragma unroll
+  for (int k = 1; k < XG_MAXSEG; ++k)
+    if (k < a.nseg && off >= a.seg[k].off) p = XgPos{a.seg[k].src, a.seg[k].dst, off - a.seg[k].off, a.seg[k].bytes};
+  return p;
+}
+
 __device__ __forceinline__ void xg_note(const XgArgs& a, int k, unsigned long long v) {
   if (a.diag) a.diag[(long)blockIdx.x * XG_DIAG + k] = v;
 }
@@ -109,21 +138,15 @@ __host__ __device__ __forceinline__ long xg_par_base(const XgArgs& a, int par) {
   return (long)par * ((long)a.world * a.slot_bytes + 32L * a.world);
 }
 
-__device__ __forceinline__ int xg_find(const XgArgs& a, long off) {
-  int s = 0;
-#pragma unroll 1
-  for (int k = 1; k < a.nseg; ++k) s = off >= a.seg[k].off ? k : s;
-  return s;
-}
-
 // Publish this block's stores of one phase, then raise its flags (value e) in every rank.
 __device__ __forceinline__ void xg_publish(const XgArgs& a, long fidx, unsigned e) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    for (int p = 0; p < a.world; ++p)
-      __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int p = 0; p < XG_MAXR; ++p)
+      if (p < a.world) __hip_atomic_store(a.flags[p] + fidx + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // write the flag lines back too: ranks sharing ONE GPU map each other's buffers as
     // local memory, where a flag store can stay in this XCD's L2 until the next release
     // (a waiting peer then never sees it: intermittent timeouts in the one-GPU tests)
@@ -136,7 +159,7 @@ __device__ __forceinline__ void xg_publish(const XgArgs& a, long fidx, unsigned 
 // false (and poisons the channel) on timeout.  Every thread must call.
 __device__ __forceinline__ bool xg_wait(const XgArgs& a, long fidx, unsigned e, int* s_abort) {
   if (threadIdx.x == 0) {
-    const unsigned* f = a.flags[a.rank] + fidx;
+    const unsigned* f = xg_pick(a.flags, a.rank) + fidx;
     const unsigned long long t0 = wall_clock64();
     for (int r = 0; r < a.world && !*s_abort; ++r) {
       unsigned v;
@@ -150,7 +173,7 @@ __device__ __forceinline__ bool xg_wait(const XgArgs& a, long fidx, unsigned e, 
           if (a.diag) {
             unsigned long long* d = a.diag + (long)blockIdx.x * XG_DIAG;
             d[3] = wall_clock64(); d[4] = 2; d[5] = (unsigned long long)r; d[6] = v;
-            d[7] = __hip_atomic_load(a.flags[r] + fidx + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            d[7] = __hip_atomic_load(xg_pick(a.flags, r) + fidx + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
           break;
         }
@@ -168,18 +191,21 @@ __device__ __forceinline__ bool xg_wait(const XgArgs& a, long fidx, unsigned e, 
 }
 
 __device__ __forceinline__ const char* xg_src(const XgArgs& a, long off) {
-  const XgSeg& s = a.seg[xg_find(a, off)];
-  return s.src + (off - s.off);
+  const XgPos p = xg_pos(a, off);
+  return p.src + p.so;
 }
 
 __device__ __forceinline__ char* xg_dst(const XgArgs& a, long off) {
-  const XgSeg& s = a.seg[xg_find(a, off)];
-  return s.dst + (off - s.off);
+  const XgPos p = xg_pos(a, off);
+  return p.dst + p.so;
 }
 
-// Two-shot fp32 sum all-reduce (op 2): see the header comment.
-__device__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
-  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x, W = a.world;
+// Two-shot fp32 sum all-reduce (op 2): see the header comment.  W = a.world as a template
+// parameter: the per-rank register arrays then have constant bounds (with a runtime bound
+// the compiler kept them in scratch, 144 B/lane).
+template <int W>
+__device__ __forceinline__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
+  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
   const int par = e & 1u;
   const long units = a.msg_bytes >> 4;
   const long S = (units + W - 1) / W;                 // 16-byte units per shard
@@ -198,12 +224,11 @@ __device__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
   // phase 1: my contribution to shard p -> rank p's slot [my rank]
   for (long v = v0 + t; v < v1; v += blockDim.x) {
 #pragma unroll
-    for (int p = 0; p < XG_MAXR; ++p) {
-      if (p >= W) break;
+    for (int p = 0; p < W; ++p) {
       const long u = p * S + v;
       if (u < units) {
-        const uint4 x = *reinterpret_cast<const uint4*>(xg_src(a, u << 4));
-        *reinterpret_cast<uint4*>(a.buf[p] + area0 + (long)a.rank * shard + (v << 4)) = x;
+        const xu4 x = *reinterpret_cast<const xu4*>(xg_src(a, u << 4));
+        *reinterpret_cast<xu4*>(a.buf[p] + area0 + (long)a.rank * shard + (v << 4)) = x;
       }
     }
   }
@@ -211,48 +236,41 @@ __device__ void xg_twoshot(const XgArgs& a, unsigned e, int* s_abort) {
   if (!xg_wait(a, f1, e, s_abort)) return;
 
   // reduce my shard's sub-chunk (fixed rank order), push the sum to every rank's slot [me]
-  const char* mine0 = a.buf[a.rank] + area0;
+  const char* mine0 = xg_pick(a.buf, a.rank) + area0;
   for (long v = v0 + t; v < v1; v += blockDim.x) {
     const long u = (long)a.rank * S + v;
     if (u >= units) break;
-    float4 x[XG_MAXR];
+    xf4 x[W];
 #pragma unroll
-    for (int r = 0; r < XG_MAXR; ++r)
-      if (r < W) x[r] = *reinterpret_cast<const float4*>(mine0 + (long)r * shard + (v << 4));
-    float4 acc = x[0];
+    for (int r = 0; r < W; ++r) x[r] = *reinterpret_cast<const xf4*>(mine0 + (long)r * shard + (v << 4));
+    xf4 acc = x[0];
 #pragma unroll
-    for (int r = 1; r < XG_MAXR; ++r)
-      if (r < W) { acc.x += x[r].x; acc.y += x[r].y; acc.z += x[r].z; acc.w += x[r].w; }
+    for (int r = 1; r < W; ++r) { acc += x[r]; }
 #pragma unroll
-    for (int p = 0; p < XG_MAXR; ++p)
-      if (p < W) *reinterpret_cast<float4*>(a.buf[p] + area1 + (long)a.rank * shard + (v << 4)) = acc;
+    for (int p = 0; p < W; ++p)
+      *reinterpret_cast<xf4*>(a.buf[p] + area1 + (long)a.rank * shard + (v << 4)) = acc;
   }
   xg_publish(a, f2, e);
   if (!xg_wait(a, f2, e, s_abort)) return;
 
   // phase 2 consume: every owner's reduced sub-chunk -> the output
-  const char* mine1 = a.buf[a.rank] + area1;
+  const char* mine1 = xg_pick(a.buf, a.rank) + area1;
   for (long v = v0 + t; v < v1; v += blockDim.x) {
-    uint4 x[XG_MAXR];
+    xu4 x[W];
 #pragma unroll
-    for (int r = 0; r < XG_MAXR; ++r)
-      if (r < W && r * S + v < units) x[r] = *reinterpret_cast<const uint4*>(mine1 + (long)r * shard + (v << 4));
+    for (int r = 0; r < W; ++r)           // in the buffer for every r (v < S); only the stores are guarded
+      x[r] = *reinterpret_cast<const xu4*>(mine1 + (long)r * shard + (v << 4));
 #pragma unroll
-    for (int r = 0; r < XG_MAXR; ++r)
-      if (r < W && r * S + v < units) *reinterpret_cast<uint4*>(xg_dst(a, (r * S + v) << 4)) = x[r];
+    for (int r = 0; r < W; ++r)
+      if (r * S + v < units) *reinterpret_cast<xu4*>(xg_dst(a, (r * S + v) << 4)) = x[r];
   }
 }
 
-__global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
-  __shared__ int s_abort;
-  __shared__ unsigned s_e;
+// One-shot all-gather / all-reduce (ops 0 / 1) for W = a.world ranks.
+template <int W>
+__device__ __forceinline__ void xg_oneshot(const XgArgs& a, unsigned e, int* s_abort) {
   const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
-  const unsigned e = xg_epoch(a, &s_abort, &s_e);
-  if (s_abort) return;
   const int par = e & 1u;
-  if (a.op == 2) {
-    xg_twoshot(a, e, &s_abort);
-  } else {
   // this block's chunk of the packed per-rank message, in 16-byte units
   const long units = a.msg_bytes >> 4;
   const long per = (units + nb - 1) / nb;
@@ -263,47 +281,64 @@ __global__ __launch_bounds__(256) void xgmi_kernel(XgArgs a) {
   // 1) push: load each 16 B once, store it into every rank's slot [rank] (own included)
   for (long u = u0 + t; u < u1; u += blockDim.x) {
     const long off = u << 4;
-    const XgSeg& s = a.seg[xg_find(a, off)];
-    const uint4 v = *reinterpret_cast<const uint4*>(s.src + (off - s.off));
+    const xu4 v = *reinterpret_cast<const xu4*>(xg_src(a, off));
 #pragma unroll
-    for (int p = 0; p < XG_MAXR; ++p)
-      if (p < a.world) *reinterpret_cast<uint4*>(a.buf[p] + my_slot + off) = v;
+    for (int p = 0; p < W; ++p) *reinterpret_cast<xu4*>(a.buf[p] + my_slot + off) = v;
   }
   // publish (every wave drains its stores, the barrier, ONE system-scope release per
   // block, the flags), then wait for every source's flag of this chunk (one lane polls,
   // bounded) and ONE system-scope acquire for the block (the vector L1 is per CU)
   const long fidx = ((long)par * XG_MAXB + b) * XG_MAXR;
   xg_publish(a, fidx, e);
-  xg_wait(a, fidx, e, &s_abort);
-
   // 3) consume from local memory
-  if (!s_abort) {
-    const char* mine = a.buf[a.rank] + xg_par_base(a, par);
+  if (xg_wait(a, fidx, e, s_abort)) {
+    const char* mine = xg_pick(a.buf, a.rank) + xg_par_base(a, par);
     for (long u = u0 + t; u < u1; u += blockDim.x) {
       const long off = u << 4;
-      const XgSeg& s = a.seg[xg_find(a, off)];
-      const long so = off - s.off;
+      const XgPos s = xg_pos(a, off);
+      const long so = s.so;
       if (a.op == 0) {           // all-gather: out is rank-major [world][seg.bytes]
-        uint4 v[XG_MAXR];
+        xu4 v[W];
 #pragma unroll
-        for (int r = 0; r < XG_MAXR; ++r)
-          if (r < a.world) v[r] = *reinterpret_cast<const uint4*>(mine + (long)r * a.slot_bytes + off);
+        for (int r = 0; r < W; ++r) v[r] = *reinterpret_cast<const xu4*>(mine + (long)r * a.slot_bytes + off);
 #pragma unroll
-        for (int r = 0; r < XG_MAXR; ++r)
-          if (r < a.world) *reinterpret_cast<uint4*>(s.dst + (long)r * s.bytes + so) = v[r];
+        for (int r = 0; r < W; ++r) *reinterpret_cast<xu4*>(s.dst + (long)r * s.bytes + so) = v[r];
       } else {                   // all-reduce (fp32 sum), rank order fixed -> bitwise identical on all ranks
-        float4 v[XG_MAXR];
+        xf4 v[W];
 #pragma unroll
-        for (int r = 0; r < XG_MAXR; ++r)
-          if (r < a.world) v[r] = *reinterpret_cast<const float4*>(mine + (long)r * a.slot_bytes + off);
-        float4 acc = v[0];
+        for (int r = 0; r < W; ++r) v[r] = *reinterpret_cast<const xf4*>(mine + (long)r * a.slot_bytes + off);
+        xf4 acc = v[0];
 #pragma unroll
-        for (int r = 1; r < XG_MAXR; ++r)
-          if (r < a.world) { acc.x += v[r].x; acc.y += v[r].y; acc.z += v[r].z; acc.w += v[r].w; }
-        *reinterpret_cast<float4*>(s.dst + so) = acc;
+        for (int r = 1; r < W; ++r) { acc += v[r]; }
+        *reinterpret_cast<xf4*>(s.dst + so) = acc;
       }
     }
   }
+}
+
+template <int W>
+__device__ __forceinline__ void xg_body(const XgArgs& a, unsigned e, int* s_abort) {
+  if (a.op == 2) xg_twoshot<W>(a, e, s_abort);
+  else xg_oneshot<W>(a, e, s_abort);
+}
+
+__global__ __launch_bounds__(256) void xgmi_kernel(XgArgs) {
+  // the arguments are read in place from the kernarg segment: through the by-value
+  // parameter the compiler copied the whole struct into scratch in every lane (488 B)
+  const XgArgs& a = *(const XgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  __shared__ int s_abort;
+  __shared__ unsigned s_e;
+  const unsigned e = xg_epoch(a, &s_abort, &s_e);
+  if (s_abort) return;
+  switch (a.world) {
+    case 1: xg_body<1>(a, e, &s_abort); break;
+    case 2: xg_body<2>(a, e, &s_abort); break;
+    case 3: xg_body<3>(a, e, &s_abort); break;
+    case 4: xg_body<4>(a, e, &s_abort); break;
+    case 5: xg_body<5>(a, e, &s_abort); break;
+    case 6: xg_body<6>(a, e, &s_abort); break;
+    case 7: xg_body<7>(a, e, &s_abort); break;
+    default: xg_body<8>(a, e, &s_abort); break;
   }
   // 4) the last block to finish advances the epoch for the next call on this channel
   xg_finish(a, e);
@@ -335,7 +370,7 @@ __global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs a) {
   const long fidx = ((long)par * XG_MAXB + b) * XG_MAXR;
   xg_publish(a, fidx, e);
   if (xg_wait(a, fidx, e, &s_abort)) {
-    const char* mine = a.buf[a.rank] + xg_par_base(a, par);
+    const char* mine = xg_pick(a.buf, a.rank) + xg_par_base(a, par);
     // my units of this block's chunk: [max(u0, own_lo), min(u1, own_hi))
     const long own_lo = (long)a.rank * a.rs_sh - a.rs_lo, own_hi = own_lo + a.rs_sh;
     const long c0 = u0 > own_lo ? u0 : own_lo, c1 = u1 < own_hi ? u1 : own_hi;

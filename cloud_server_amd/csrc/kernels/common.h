@@ -25,6 +25,10 @@ extern thread_local int g_csa_det;
 // Packed profile (det.hip, host state): a process that packs several jobs onto one GPU
 // prefers launch shapes with less CU-time per job-step over the lowest latency alone.
 extern thread_local int g_csa_packed;
+// Shared-GPU profile (det.hip, host state): several ranks of one job run on ONE GPU (the
+// multi-process tests); no launch may depend on a 16-wave workgroup being placed while a
+// peer rank's kernel spins in a peer wait.
+extern thread_local int g_csa_shared;
 
 __device__ __forceinline__ float act_fwd(float x, int act, float alpha) {
   switch (act) {

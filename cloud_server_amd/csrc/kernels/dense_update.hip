@@ -37,7 +37,6 @@
 // and written once (32 MB) — instead of the split-K backward pair (dW written) plus the
 // flat optimizer pass (dW, W, acc re-read).
 #include "dense_update.h"
-#include <cstdlib>
 
 namespace csa {
 
@@ -81,12 +80,16 @@ CSA_API int csa_dense_bwd_update_slabs(int K) {
 }
 
 // Column blocks per row group the launcher picks: one 1024-thread block when the row groups
-// fill the chip (fc1: 245) and N <= 512, else 128-column blocks of 256 threads.
+// fill the chip (fc1: 245) and N <= 512 (one process per GPU), else 128-column blocks of
+// 256 threads.
 static int du_cs(int K, int N) {
   const int groups = (K + DU_FT - 1) / DU_FT;
   // packed profile: always 128-column blocks (256 threads, 33 KB LDS: four per CU beside
   // other jobs' kernels): K = 4 805.5k vs 743.0k samples/s (profiles/r2_multitenant.md)
-  const int minb = g_csa_packed ? (1 << 30) : 128;
+  // ranks sharing ONE GPU (g_csa_shared): a 16-wave workgroup of one process was seen
+  // not to be placed for as long as another process's kernel spun in a peer wait (the
+  // round-5 world-2 stall: profiles/r5_notes.md); 256-thread blocks always were
+  const int minb = (g_csa_packed || g_csa_shared) ? (1 << 30) : 128;
   if (N <= 512 && groups >= minb) return 1;
   return (N + 127) / 128;
 }

@@ -22,6 +22,7 @@ namespace csa {
 
 thread_local int g_csa_det = 0;
 thread_local int g_csa_packed = 0;
+thread_local int g_csa_shared = 0;
 
 constexpr int RF_COLS = 64;      // columns per workgroup
 constexpr int RF_SL = 4;         // row slices per column (one per wave)
@@ -131,6 +132,8 @@ CSA_API void csa_set_deterministic(int on) { g_csa_det = on ? 1 : 0; }
 CSA_API int csa_deterministic() { return g_csa_det; }
 CSA_API void csa_set_packed(int on) { g_csa_packed = on ? 1 : 0; }
 CSA_API int csa_packed() { return g_csa_packed; }
+CSA_API void csa_set_shared_gpu(int on) { g_csa_shared = on ? 1 : 0; }
+CSA_API int csa_shared_gpu() { return g_csa_shared; }
 
 CSA_API int csa_rows_fold(const float* src, long ld, int R, long n, float* dst, int zero_src, hipStream_t st) {
   if (!src || !dst || R < 1 || n < 1 || ld < n) return -1;

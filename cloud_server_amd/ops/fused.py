@@ -92,6 +92,8 @@ _SIGS = {
     "csa_deterministic": (I, []),
     "csa_set_packed": (None, [I]),
     "csa_packed": (I, []),
+    "csa_set_shared_gpu": (None, [I]),
+    "csa_shared_gpu": (I, []),
     "csa_rows_fold": (I, [P, L, I, L, P, I, P]),
     "csa_rows_fold_multi": (I, [I, P, P, P, P, P, P, P]),
     "csa_conv_pair_bwd": (I, [P, P, P, P, P, P, I, F, P, I, I, F, P, P, P, P, I, F, F, P, P, P, I, P, P, P, P, F,

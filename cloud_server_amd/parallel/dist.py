@@ -98,6 +98,21 @@ def all_reduce_max(ctx: DistContext, value: float) -> float:
     return float(t.item())
 
 
+def ranks_share_gpu(ctx: DistContext, device: torch.device) -> bool:
+    """True when another rank of this job drives the same physical GPU (the one-GPU
+    multi-process tests; a node runs one rank per GPU).  Ranks compare PCI locations, so a
+    launcher that narrows each rank's visible devices is not mistaken for sharing.  Called
+    by every rank at engine construction (one small all-gather)."""
+    if not ctx.enabled or device.type != "cuda" or not dist.is_initialized():
+        return False
+    p = torch.cuda.get_device_properties(device)
+    me = (int(getattr(p, "pci_domain_id", 0)), int(getattr(p, "pci_bus_id", 0)),
+          int(getattr(p, "pci_device_id", 0)), str(getattr(p, "uuid", "")))
+    seen = [None] * ctx.world
+    dist.all_gather_object(seen, me)
+    return sum(1 for x in seen if x == me) > 1
+
+
 def shutdown(ctx: DistContext) -> None:
     if ctx.enabled and dist.is_initialized():
         dist.destroy_process_group()

@@ -30,7 +30,7 @@ from ..data.stream import BatchStream, DeviceDataset
 from ..models.cnn import DigitNet, build_model, loss_fn
 from ..models.dsl import TrainConfig
 from ..ops import optim_ref
-from ..parallel.dist import DistContext
+from ..parallel.dist import DistContext, ranks_share_gpu
 from ..parallel.dp import GradSync
 from ..utils.tracing import trace_range
 from ..utils.graphs import capture
@@ -95,6 +95,10 @@ class TrainEngine:
             strategy = "allreduce"
         self.ctx = ctx or DistContext(device=torch.device(device))
         self.device = torch.device(device)
+        # CSA_SHARED_GPU_PROFILE=0 keeps the one-rank-per-GPU launch shapes even when ranks
+        # share a device (reproduces the round-5 world-2 stall: scripts/xgmi_stress.py)
+        self.shared_gpu = (ranks_share_gpu(self.ctx, self.device)
+                           and os.environ.get("CSA_SHARED_GPU_PROFILE", "1") != "0")
         self.model: DigitNet = build_model(cfg, self.device, pad_multiple=self.ctx.world,
                                            dense_last=strategy == "lowrank")
         self.model.train()

@@ -132,6 +132,9 @@ class HipProgram:
         # packed profile (engines built to run as branches of one multi-job graph): launch
         # shapes with less CU-time per step (conv_pair.hip, dense_update.hip)
         self.packed = bool(getattr(eng, "packed", False))
+        # shared-GPU profile (several ranks of this job on ONE device): no 16-wave
+        # workgroups (dense_update.hip du_cs; profiles/r5_notes.md, the world-2 stall)
+        self.shared_gpu = bool(getattr(eng, "shared_gpu", False))
         with self._det_scope():
             self._init_plan(eng, forward_only)
 
@@ -140,13 +143,16 @@ class HipProgram:
 
         class _Scope:
             def __enter__(self_):
-                self_.prev = (int(prog.lib.csa_deterministic()), int(prog.lib.csa_packed()))
+                self_.prev = (int(prog.lib.csa_deterministic()), int(prog.lib.csa_packed()),
+                              int(prog.lib.csa_shared_gpu()))
                 prog.lib.csa_set_deterministic(1 if prog.det else 0)
                 prog.lib.csa_set_packed(1 if prog.packed else 0)
+                prog.lib.csa_set_shared_gpu(1 if prog.shared_gpu else 0)
 
             def __exit__(self_, *exc):
                 prog.lib.csa_set_deterministic(self_.prev[0])
                 prog.lib.csa_set_packed(self_.prev[1])
+                prog.lib.csa_set_shared_gpu(self_.prev[2])
                 return False
         return _Scope()
 

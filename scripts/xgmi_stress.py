@@ -50,21 +50,37 @@ def worker(rank, world, port, steps, strategy, q, chunk=25):
         t0 = time.perf_counter()
         done = 1
         bad = False
+        import faulthandler
+        os.makedirs("gpurun_out", exist_ok=True)
+        hang_fh = open(f"gpurun_out/xgmi_stress_host_{world}_{rank}.txt", "w")
+        slow_host = []                       # (step, host call, seconds) of calls > 0.1 s
         chunks = []                          # ms per step of each 25-step chunk
         while done < steps:
             n = min(chunk, steps - done)
             tc = time.perf_counter()
-            for _ in range(n):
+            for i in range(n):
+                # a host call that blocks > 0.5 s leaves its Python stack in the dump file
+                faulthandler.dump_traceback_later(0.5, file=hang_fh)
+                th = time.perf_counter()
                 eng.step()
+                faulthandler.cancel_dump_traceback_later()
+                w = time.perf_counter() - th
+                if w > 0.1:
+                    slow_host.append((done + i, "step", round(w, 3)))
             done += n
+            faulthandler.dump_traceback_later(0.5, file=hang_fh)
+            th = time.perf_counter()
             torch.cuda.synchronize()
+            faulthandler.cancel_dump_traceback_later()
+            if time.perf_counter() - th > 0.1:
+                slow_host.append((done, "sync", round(time.perf_counter() - th, 3)))
             chunks.append(round((time.perf_counter() - tc) * 1e3 / n, 3))
             if poisoned():
                 bad = True
                 break
         dt = time.perf_counter() - t0
         res = {"ok": not bad, "steps": done, "ms_per_step": round(dt * 1e3 / max(done - 1, 1), 3),
-               "chunk_ms": chunks}
+               "chunk_ms": chunks, "slow_host": slow_host}
         if eng.aps is not None:
             res.update(staleness=eng.staleness(), aps_blocks=eng.aps.nb)
             eng.finish_async()
@@ -92,7 +108,16 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--strategy", default="allreduce")
     ap.add_argument("--chunk", type=int, default=25, help="steps enqueued between host syncs")
+    ap.add_argument("--rank", type=int, default=-1,
+                    help="run ONE rank in this process (with --port), e.g. each under its own profiler")
+    ap.add_argument("--port", type=int, default=0)
     a = ap.parse_args()
+    if a.rank >= 0:
+        class _Q:
+            def put(self, item):
+                print(json.dumps({"rank": item[0], "res": item[1]}), flush=True)
+        worker(a.rank, a.world, a.port, a.steps, a.strategy, _Q(), a.chunk)
+        return 0
     import torch.multiprocessing as mp
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     ctx = mp.get_context("spawn")

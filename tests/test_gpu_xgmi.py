@@ -181,6 +181,9 @@ def _worker_ps(rank: int, world: int, port: int, q, phases=(("ps1", "ps"), ("ps2
             assert eng.backend == "hip", eng.fallback_reason
             assert eng.sync.xgmi is not None, eng.sync.xgmi_reason
             assert eng.program.det and eng.sync.det
+            # ranks share this GPU: the shared-GPU launch profile (no 16-wave workgroups)
+            # must be on, or a rank's fc1 update can starve beside a peer's spinning wait
+            assert eng.shared_gpu and eng.program.shared_gpu
             # both strategies overlap their buckets with the backward (the all-reduce
             # reference included: VERDICT r4 — no CSA_DP_OVERLAP=0 escape)
             assert eng.program.overlap and eng.program.bucket_at
