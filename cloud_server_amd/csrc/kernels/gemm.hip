@@ -271,7 +271,7 @@ template <int WM, int WN, int WK, class LA, class LB, class EPI>
 __device__ __forceinline__ void gemm_body(LA la, LB lb, EPI epi, int M, int N, int K,
                                           int k_per_split, const BNRef& bn, int bn_on,
                                           float* bn_slab_out, int slab_C, int GX, int GY, int GZ,
-                                          int bid, int nblk, float* lds) {
+                                          int bid, int nblk, float* lds, int det = 0) {
   static_assert(WM * WN * WK == 4, "4 waves per workgroup");
   const TileId tid = gemm_tile(GX, GY, GZ, bid, nblk);
   if (!tid.valid) return;                 // whole workgroup: grid padding
@@ -380,10 +380,39 @@ __device__ __forceinline__ void gemm_body(LA la, LB lb, EPI epi, int M, int N, i
       int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
       epi(m0 + row, n0 + (lane & 31), acc[i], first, s_acc, aux[i]);
     }
-    epi.flush(n0 + (lane & 31), s_acc);
+    if (!det) epi.flush(n0 + (lane & 31), s_acc);
   }
   GEMM_STAMP(7);
   if (EPI::NEEDS_LDS && bn_slab_out) {
+    if (det) {
+      // deterministic mode: no float atomics.  Every lane's {sum dz, sum dz*xhat} goes to
+      // LDS (the stage area: every operand / split-K read is behind the barrier), one
+      // thread per statistic folds them in (wave, lane) order, and the workgroup writes
+      // its OWN slab row (csa_dense_dgrad_slabs: one per workgroup; folded in row order)
+      float* s_det = lds;
+      __syncthreads();
+      if (wk == 0) {
+        if constexpr (EPI::NEEDS_LDS) {
+          s_det[wmn * 128 + 2 * lane] = epi.sd;
+          s_det[wmn * 128 + 2 * lane + 1] = epi.sdx;
+        }
+      }
+      __syncthreads();
+      const int slab_row = (tid.z * GY + tid.y) * GX + tid.x;
+      for (int i = threadIdx.x; i < 2 * slab_C; i += blockDim.x) {
+        const int ch = i < slab_C ? i : i - slab_C, which = i < slab_C ? 0 : 1;
+        float v = 0.f;
+        for (int w = 0; w < WM * WN; ++w) {
+          const int nw = tid.x * 32 * WN + (w % WN) * 32;
+          for (int l = 0; l < 64; ++l) {
+            const int f = nw + (l & 31);
+            if (f < N && f % slab_C == ch) v += s_det[w * 128 + 2 * l + which];
+          }
+        }
+        bn_slab_out[(size_t)slab_row * 2 * slab_C + i] = v;
+      }
+      return;
+    }
     // fold into one of BN_SLAB_ROWS rows (atomics; the caller zeroes the slab every step),
     // so a consumer reduces 16 rows instead of one per workgroup
     __syncthreads();
@@ -398,10 +427,11 @@ template <int WM, int WN, int WK, class LA, class LB, class EPI>
 struct GemmProblem {
   LA la; LB lb; EPI epi; int M, N, K, kps; BNRef bn; int bn_on; float* slab_out; int slab_C;
   int GX, GY, GZ;
+  int det;                             // deterministic mode: exclusive BN slab rows, no atomics
   __host__ __device__ int nblocks() const { return (GX * GY * GZ + 7) / 8 * 8; }
   __device__ __forceinline__ void run(int bid, float* lds) const {
     gemm_body<WM, WN, WK>(la, lb, epi, M, N, K, kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ, bid,
-                          nblocks(), lds);
+                          nblocks(), lds, det);
   }
 };
 
@@ -450,6 +480,7 @@ static Plan plan_gemm(int M, int N, int K, bool allow_split) {
 
 static int grid_slabs(const Plan& p, int M, int N) {
   const int g = ((N + 32 * p.wn - 1) / (32 * p.wn)) * ((M + 32 * p.wm - 1) / (32 * p.wm)) * p.splits;
+  if (g_csa_det) return g;                 // deterministic mode: one exclusive row per workgroup
   return g < BN_SLAB_ROWS ? g : BN_SLAB_ROWS;
 }
 
@@ -460,7 +491,8 @@ static int with_problem(const Plan& p, LA la, LB lb, EPI epi, int M, int N, int 
   const int GX = (N + 32 * p.wn - 1) / (32 * p.wn), GY = (M + 32 * p.wm - 1) / (32 * p.wm);
   const int GZ = p.splits;
 #define CSA_P(WM, WN, WK) \
-  return f(GemmProblem<WM, WN, WK, LA, LB, EPI>{la, lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ})
+  return f(GemmProblem<WM, WN, WK, LA, LB, EPI>{la, lb, epi, M, N, K, p.kps, bn, bn_on, slab_out, slab_C, GX, GY, GZ, \
+                                                g_csa_det})
   if (p.wm == 2 && p.wn == 2) CSA_P(2, 2, 1);
   if (p.wm == 1 && p.wn == 2) CSA_P(1, 2, 2);
   CSA_P(1, 1, 4);
@@ -629,7 +661,7 @@ CSA_API int csa_dense_bwd(const float* dY, const float* W, float* dX, int M, int
   auto go = [&](auto ed, int bn_on, float* so, int sc) {
     using ED = decltype(ed);
     const GemmProblem<1, 1, 4, LoadRowMajor<true>, LoadRowMajor<true>, ED> a{
-        la, lb, ed, M, Kin, Nout, pd.kps, bn, bn_on, so, sc, GX, GY, pd.splits};
+        la, lb, ed, M, Kin, Nout, pd.kps, bn, bn_on, so, sc, GX, GY, pd.splits, g_csa_det};
     auto launch = [&](auto law) {
       return with_problem(pw, law, lbw, ew, Mg, Nout, M, BNRef{}, 0, nullptr, 0, [&](auto b) {
         hipLaunchKernelGGL((gemm_pair_kernel<decltype(a), decltype(b)>),

@@ -979,7 +979,9 @@ CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, c
   // dW/db are ACCUMULATED (the caller zeroes them every step); ws = int[4] zeroed once
   const size_t rows_lds =
       ((size_t)RG * NCLS + 4 * 256 + 8 + (size_t)K * NCLS + (size_t)RG * (K + 1)) * sizeof(float);
-  if (K % 4 == 0 && rows_lds <= HEAD_LDS_MAX && ws) {
+  // deterministic mode: the single-workgroup generic kernel (fixed-order sums, plain
+  // stores; the row-group kernel accumulates dW with atomics)
+  if (K % 4 == 0 && rows_lds <= HEAD_LDS_MAX && ws && !g_csa_det) {
     if (rows_lds > 64 * 1024) {
       static bool attr_set = hipFuncSetAttribute((const void*)head_rows_kernel,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -989,6 +991,13 @@ CSA_API int csa_head(const float* h, int M, int K, int in_act, float in_alpha, c
     hipLaunchKernelGGL(head_rows_kernel, dim3((M + RG - 1) / RG), dim3(RT), rows_lds, st, a, ws);
   } else {
     const size_t base = ((size_t)M * NCLS + 32) * sizeof(float);
+    if (base > 64 * 1024) {
+      if (base > HEAD_LDS_MAX) return -4;
+      static bool attr_g = hipFuncSetAttribute((const void*)head_generic_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)HEAD_LDS_MAX) == hipSuccess;
+      if (!attr_g) return -3;
+    }
     hipLaunchKernelGGL(head_generic_kernel, dim3(1), dim3(HT), base, st, a);
   }
   return (int)hipGetLastError();

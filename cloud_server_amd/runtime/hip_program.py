@@ -668,10 +668,11 @@ class HipProgram:
         in row order by the finalize kernels), gather-form pools (overlapping pools are never
         fused), gconv units (implicit GEMM without split-K), fused dense backward + update
         units (exclusive BN-backward rows, fixed-order column-block hand-off), materialised-
-        gradient dense units and dense forwards (no split-K), and the row-per-workgroup or
-        partial-row heads.  What remains — a materialised-gradient dense unit reading a
-        BatchNorm'd input, and the atomic head — raises Unsupported, and the engine runs the
-        step on eager PyTorch with its deterministic algorithms instead."""
+        gradient dense units and dense forwards (no split-K; a BatchNorm'd input's backward
+        statistics go to one exclusive slab row per GEMM workgroup, folded in (wave, lane)
+        order: gemm.hip), and the row-per-workgroup, partial-row or single-workgroup generic
+        heads (head.hip csa_head picks the generic kernel: fixed-order sums, plain stores).
+        Only async_ps data parallelism stays outside (pushes applied in arrival order)."""
         e = self.e
         # data parallel: every collective of the step is fixed-order (GradSync.det: the xGMI
         # kernels or an exact all-gather + rank-ordered fold), the stripes are exclusive rows
@@ -680,14 +681,6 @@ class HipProgram:
         if e.ctx.enabled and e.sync.strategy not in ("allreduce", "ps"):
             # (async_ps applies pushes in arrival order: nondeterministic by definition)
             raise Unsupported(f"deterministic mode: {e.sync.strategy} data parallelism")
-        for u in self.units:
-            # materialised-gradient dense units are fixed-order without split-K, except for
-            # the BatchNorm-backward statistics their input-gradient epilogue adds atomically
-            if u.kind == "dense" and not u.fused and u.in_tf.has_bn:
-                raise Unsupported(f"deterministic mode: dense unit {u.layer.name} (BatchNorm input, "
-                                  "materialised gradient) has no fixed-order variant")
-        if not (self.head_row or self.head_rg):
-            raise Unsupported("deterministic mode: head outside the row-per-workgroup / partial-row family")
 
     def _row_fold(self, t: torch.Tensor, rows: int, width: int, dst: torch.Tensor, zero_src: int, st) -> None:
         """dst[:width] = fixed-order sum of the first ``rows`` rows of ``t`` (row stride width)."""
@@ -1245,6 +1238,7 @@ class HipProgram:
                         K.ptr(u.dy), K.ptr(V[f"{lp.name}.weight"]), K.ptr(prev.dy), B, fin, fout,
                         K.ptr(xf), in_act, in_alpha, *self._bn_args_c(tf), K.ptr(tf.bwd_slab), st),
                         "slabs:dense_dgrad")
+                    self._dense_det_fold(u, st)
                 if u in self.lr_units:          # global wgrad formed after the gathers
                     if k == self.lr_first:
                         self._lowrank_wgrads()
@@ -1655,7 +1649,17 @@ class HipProgram:
             1.0, st)
         if rc < 0:
             raise RuntimeError(f"dense_bwd failed: {rc}")
+        if rc > 0:
+            self._dense_det_fold(u, st)
         return rc > 0
+
+    def _dense_det_fold(self, u: Unit, st) -> None:
+        """Deterministic mode, after a materialised-gradient dense unit's input gradient: its
+        BN-backward rows (one per GEMM workgroup, gemm.hip) to row 0 in row order."""
+        tf = u.in_tf
+        if self.det and tf.has_bn:
+            self._row_fold(tf.bwd_slab, tf.bwd_prod_rows, tf.bwd_slab.shape[1] * tf.bwd_slab.shape[2],
+                           tf.bwd_slab, 0, st)
 
     def _dd_wgrad_update(self, u: Unit, x: torch.Tensor, dy: torch.Tensor, M: int, act, st) -> None:
         """Weight gradient X^T dY over ``M`` rows with the optimizer update of W / b applied

@@ -208,3 +208,56 @@ def test_deterministic_hip_every_lowering_bitwise(monkeypatch, name):
         a, b = e_det.model.state.view(k, g_det), e_det.model.state.view(k, g_ref)
         scale = b.abs().max().item() + 1e-6
         assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6 + 1e-5 * gmax, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [80, 300])
+def test_deterministic_hip_large_batch_bitwise(monkeypatch, batch):
+    """the last two eager fallbacks of deterministic mode are gone.
+    Batch 80: the dense layers take the materialised-gradient GEMMs (the fused backward +
+    update covers M <= 64), fc1 reading a BatchNorm'd input — its backward statistics go to
+    exclusive slab rows, folded in order (gemm.hip).  Batch 300: beyond the partial-row head
+    (M <= 256), the single-workgroup generic head.  The HIP program stays on, two graph runs
+    and an eager run are bitwise equal, and one step's gradients match the fp32 reference."""
+    from test_hip_step import CASES, _cfg
+
+    monkeypatch.setenv("CSA_DETERMINISTIC", "1")
+    try:
+        runs = []
+        for mode in ("graph", "graph", "eager"):
+            cfg = _cfg(CASES["sample"], optimizer="AdamOptimizer", lr=1e-3, batch=batch)
+            eng = TrainEngine(cfg, synthetic_mnist(700, seed=5), device="cuda:0", backend="hip",
+                              use_graph=mode == "graph")
+            assert eng.backend == "hip" and eng.program.det, eng.fallback_reason
+            if batch == 80:
+                assert any(u.kind == "dense" and not u.fused and u.in_tf.has_bn for u in eng.program.units)
+            else:
+                assert not (eng.program.head_row or eng.program.head_rg)
+            for _ in range(6):
+                eng.step()
+            eng.sync_device()
+            runs.append((eng.flat.clone(), eng.slots.clone(), eng.metrics_since(0)["loss"]))
+        for i in (1, 2):
+            assert torch.equal(runs[0][0], runs[i][0]), f"run {i}: params differ"
+            assert torch.equal(runs[0][1], runs[i][1]), f"run {i}: optimizer slots differ"
+            assert runs[0][2] == runs[i][2]
+
+        def grads(backend):
+            cfg = _cfg(CASES["sample"], batch=batch)
+            eng = TrainEngine(cfg, synthetic_mnist(600, seed=13), device="cuda:0", backend=backend,
+                              use_graph=False)
+            w0 = eng.flat.clone()
+            eng.step()
+            eng.sync_device()
+            return eng, (w0 - eng.flat) / cfg.effective_lr
+
+        e_det, g_det = grads("hip")
+        assert e_det.program.det
+        _, g_ref = grads("torch")
+    finally:
+        torch.use_deterministic_algorithms(False)
+    gmax = g_ref.abs().max().item()
+    for k in e_det.model.state.shapes:
+        a, b = e_det.model.state.view(k, g_det), e_det.model.state.view(k, g_ref)
+        scale = b.abs().max().item() + 1e-6
+        assert (a - b).abs().max().item() <= 3e-3 * scale + 1e-6 + 1e-5 * gmax, k
