@@ -179,6 +179,10 @@ def main() -> int:
     # run_steps: exactly K steps; on one GPU groups of CSA_GRAPH_STEPS steps replay one
     # multi-step graph and the remainder the k/2, k/4, .. 2-step graphs (runtime/engine.py)
     eng.step()                          # capture + first step (the single-step graph's first replay)
+    if args.steps <= 64 and os.environ.get("CSA_BENCH_ONE_GRAPH", "1") == "1":
+        # a short timed loop (the driver's K = 20) is ONE K-step graph replay: no gaps
+        # between graph launches inside the timed region (K real steps either way)
+        eng.extra_group_sizes = [args.steps]
     eng.prepare_group_graph()           # every multi-step graph captured AND replayed once
                                         # (state restored): no first launch in the timed loop
     eng.run_steps(max(args.warmup - 1, 0))

@@ -161,6 +161,9 @@ class TrainEngine:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.graph = None
         self.graph_k = None      # CSA_GRAPH_STEPS steps captured in one graph (run_steps)
+        # further multi-step graph sizes to capture beside k, k/2, .. (a known loop length:
+        # bench.py's K timed steps replay as ONE graph, no inter-graph gaps)
+        self.extra_group_sizes: List[int] = []
         self.graphs_k: Dict[int, object] = {}   # every multi-step size (group_sizes)
         self.warmed = False      # _warm_up ran (a packed host re-captures without it)
 
@@ -256,7 +259,7 @@ class TrainEngine:
         single-step graph (RCCL kernels, or the xGMI peer-buffer kernels whose channel
         sequence numbers live on the device), so k steps capture the same way; the
         per-call-site path choice is made eagerly at warm-up, before any capture."""
-        k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        k = int(os.environ.get("CSA_GRAPH_STEPS", "32"))
         if self.ctx.enabled and os.environ.get("CSA_DP_GRAPH_STEPS", "1") != "1":
             return 1
         return k if (self.use_graph and k > 1) else 1
@@ -269,6 +272,8 @@ class TrainEngine:
         while k > 1:
             sizes.append(k)
             k //= 2
+        if self.group_steps() > 1:
+            sizes = sorted(set(sizes) | {n for n in self.extra_group_sizes if n > 1}, reverse=True)
         return sizes
 
     def _snapshot(self):
@@ -334,9 +339,10 @@ class TrainEngine:
 
     def run_steps(self, n: int) -> None:
         """``n`` training steps.  With a captured single-GPU program, groups of
-        ``CSA_GRAPH_STEPS`` (default 8) steps replay ONE graph holding that many steps:
+        ``CSA_GRAPH_STEPS`` (default 32) steps replay ONE graph holding that many steps:
         one launch instead of k.  Bench on MI355X (scripts/gpu_sweep.sh): 0.108 ms/step
-        ungrouped, 0.1045 at k = 4, 0.1035 at k = 8, 0.1034 at k = 16.  The remainder
+        ungrouped, 0.1045 at k = 4, 0.1035 at k = 8, 0.1034 at k = 16; round 5 (scripts/
+        gpu_r5x.sh, 2000 steps): 0.08293 at k = 8, 0.08261 at 16, 0.08234 at 32.  The remainder
         ``n mod k`` replays the k/2, k/4, .. 2-step graphs, so at most one step runs as a
         single-step replay.  Groups never straddle a half of the batch row table
         (BatchStream.can_group); exactly ``n`` steps execute."""

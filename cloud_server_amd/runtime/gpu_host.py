@@ -176,7 +176,7 @@ def serve(spool: str, device: str, backend: str = "auto", idle_exit_s: float = 0
             continue                      # re-pack without them before stepping
         # 8 steps of every job in one multi-step graph launch when no job has a hook inside
         # them (PackedJobs.run_steps; 2.4x a lone job's throughput at 4 jobs)
-        k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        k = int(os.environ.get("CSA_GRAPH_STEPS", "32"))
         group = pack.graph is not None and k > 1 and all(j.groupable(k) for j in jobs.values())
         # a launch that may capture (new pack, first multi-step launch) waits for a build
         # in flight; plain replays run alongside it

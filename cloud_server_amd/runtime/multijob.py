@@ -72,7 +72,7 @@ class PackedJobs:
         restored afterwards (see TrainEngine.prepare_group_graph): a timed loop then never
         pays the capture or the graph's first launch."""
         import os
-        k = k or int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        k = k or int(os.environ.get("CSA_GRAPH_STEPS", "32"))
         if not self.cuda or k <= 1 or self.graph is None or self.graph_k is not None:
             return
         self._capture_group(k)
@@ -89,7 +89,7 @@ class PackedJobs:
         graph where every job's group stays inside one half of its row table (see
         TrainEngine.run_steps), single packed steps otherwise."""
         import os
-        k = int(os.environ.get("CSA_GRAPH_STEPS", "8"))
+        k = int(os.environ.get("CSA_GRAPH_STEPS", "32"))
         while n > 0:
             if (self.cuda and k > 1 and n >= k and self.graph is not None
                     and all(e.stream.can_group(k) for e in self.engines)):

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 5: kernel traces of the step with and without the pair-backward tail.
+# Round 5: packed K = 8 at k = 32 with 4 / 6 / 8 hardware queues per process.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-for t in 0 1; do
-  cd /tmp && CSA_PAIR_TAIL=$t timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r5h_prof$t -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 500 --warmup 50 > $GRAFT_REPO_ROOT/gpurun_out/r5h_b$t.json 2>/dev/null || exit 6
-  cd $GRAFT_REPO_ROOT; f=$(find gpurun_out/r5h_prof$t -name "*kernel_stats.csv" | head -1); echo "== tail=$t $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r5h_b$t.json)"; head -12 "$f" | cut -d, -f1-4 | cut -c1-150
+for q in 4 6 8; do
+  GPU_MAX_HW_QUEUES=$q timeout -k 10 150 python3 bench.py --jobs 8 --steps 2048 --warmup 256 > gpurun_out/r5h_q$q.json 2>> gpurun_out/r5h.err || exit 3
+  echo "hwq=$q jobs=8 $(grep -o '"value": [0-9.]*' gpurun_out/r5h_q$q.json)"
 done

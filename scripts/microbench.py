@@ -45,10 +45,12 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=50)
+    ap.add_argument("--packed", action="store_true", help="the packed (multi-tenant) launch profile")
     a = ap.parse_args()
     cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer",
                                   options={"batch_size": a.batch}))
-    eng = TrainEngine(cfg, synthetic_mnist(6000), device="cuda", backend="hip", use_graph=False)
+    eng = TrainEngine(cfg, synthetic_mnist(6000), device="cuda", backend="hip", use_graph=False,
+                      packed=a.packed)
     for _ in range(3):
         eng.step()
     rec = Recorder(eng.program.lib)
@@ -56,6 +58,8 @@ def main() -> int:
     eng.step()
     torch.cuda.synchronize()
     eng.program.lib = rec.lib
+    if a.packed:
+        rec.lib.csa_set_packed(1)       # replays outside the program's scope keep its shapes
     total = 0.0
     rows = []
     if os.environ.get("MB_GEMM"):

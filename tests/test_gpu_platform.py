@@ -205,7 +205,7 @@ def test_node_status_reports_gpus_on_device():
     print("gpu0 fields:", sorted(g))
 
 
-def test_packed_run_steps_equal_single_packed_steps():
+def test_packed_run_steps_equal_single_packed_steps(monkeypatch):
     """PackedJobs.run_steps(n) (8-step multi-job graphs, groups never crossing a half of a
     job's row table: stream_chunk 12 forces half switches inside the run) == n single
     packed steps: same host/device step, cursor, per-step batches and weights (gpu_host's
@@ -216,6 +216,9 @@ def test_packed_run_steps_equal_single_packed_steps():
     from cloud_server_amd.models.dsl import parse_train_config
     from cloud_server_amd.runtime.engine import TrainEngine
     from cloud_server_amd.runtime.multijob import PackedJobs
+
+    # 8-step groups: they fit the 12-step row-table chunks (the default 32 would not group)
+    monkeypatch.setenv("CSA_GRAPH_STEPS", "8")
 
     def engs():
         out = []
