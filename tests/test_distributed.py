@@ -115,6 +115,25 @@ def _spawn(fn, world, *args):
     return dict(out)
 
 
+def _share_gpu(rank, world, port, buses, out):
+    """ranks_share_gpu with faked device properties: each rank reports PCI bus buses[rank]."""
+    from types import SimpleNamespace
+    from cloud_server_amd.parallel import dist as D
+    ctx = _init(rank, world, port)
+    props = SimpleNamespace(pci_domain_id=0, pci_bus_id=buses[rank], pci_device_id=0, uuid=f"gpu{buses[rank]}")
+    torch.cuda.get_device_properties = lambda dev=None: props
+    out[rank] = D.ranks_share_gpu(ctx, torch.device("cuda", 0))
+    D.shutdown(ctx)
+
+
+@pytest.mark.parametrize("buses,want", [((3, 3), True), ((3, 4), False)])
+def test_ranks_share_gpu_compares_pci_locations(buses, want):
+    """The shared-GPU launch profile (profiles/r5_notes.md) is chosen only when another
+    rank of the job drives the SAME physical GPU: ranks all-gather their PCI locations."""
+    out = _spawn(_share_gpu, 2, buses)
+    assert out == {0: want, 1: want}
+
+
 def test_collectives_world2():
     out = _spawn(_collectives, 2)
     assert out == {0: True, 1: True}
