@@ -68,10 +68,69 @@ struct CPFwdArgs {
 constexpr int CP_MAXZ = 4;
 struct CPZero { float4* p[CP_MAXZ]; long n4[CP_MAXZ]; int n; };
 
-__device__ __forceinline__ void cp_zero_early(const CPZero& z) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long)gridDim.x * blockDim.x;
+__device__ __forceinline__ void cp_zero_early(const CPZero& z, int nblk) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long)nblk * blockDim.x;
   for (int k = 0; k < z.n; ++k)
     for (long i = gid; i < z.n4[k]; i += nth) z.p[k][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Deferred dense-parameter update (round 5, data-parallel programs).  Under data
+// parallelism the dense weight gradients exist whole in the flat gradient and are exchanged
+// after the backward, so the flat optimizer launch that follows the exchange was a serial
+// 11.5 us stream over every parameter (profiles/r5_dp_trace.md).  The dense layers'
+// parameters are only read again by the NEXT step's dense forwards, which come after this
+// launch: their update rides as extra workgroups of the next step's pair forward (1 % of
+// HBM busy), gated by a device flag that the (now small) optimizer launch raises once the
+// exchanged gradient is in place.  A host flush (csa_opt_carry_flush) applies a pending
+// update at every point that reads the parameters between steps.
+constexpr int CP_MAXCS = 4;
+struct CPOptCarry {
+  int blocks;                          // extra workgroups (0: no carry)
+  int opt; float lr; const int64_t* step;
+  float* w; const float* g; float* s0; float* s1;
+  const unsigned* pending;             // 1: the exchanged gradient awaits its update
+  int count; long lo4[CP_MAXCS]; long start4[CP_MAXCS + 1];   // flat spans, float4 units
+};
+
+// Workgroup k of nblk: a grid-stride streaming update, one float4 of each operand per
+// thread and iteration (the carrying forward keeps its occupancy; ~1 000 workgroups keep
+// 12 MB in flight).  Segment lookup by unrolled selects (no per-lane index into the
+// argument struct).
+__device__ __forceinline__ void cp_opt_carry(const CPOptCarry& c, int k, int nblk) {
+  __shared__ unsigned s_pend;
+  if (threadIdx.x == 0) s_pend = __hip_atomic_load(c.pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (!s_pend) return;
+  const int nslot = opt_nslots(c.opt);
+  const float lr = opt_step_lr(c.opt, c.lr, c.step);
+  const long m4 = c.start4[c.count];
+  const long nth = (long)nblk * blockDim.x;
+  float4* w4 = reinterpret_cast<float4*>(c.w);
+  const float4* g4 = reinterpret_cast<const float4*>(c.g);
+  float4* s04 = reinterpret_cast<float4*>(c.s0);
+  float4* s14 = reinterpret_cast<float4*>(c.s1);
+  for (long t = (long)k * blockDim.x + threadIdx.x; t < m4; t += nth) {
+    long lo = c.lo4[0], st = 0;
+#pragma unroll
+    for (int q = 1; q < CP_MAXCS; ++q)
+      if (q < c.count && t >= c.start4[q]) { lo = c.lo4[q]; st = c.start4[q]; }
+    const long i = lo + (t - st);
+    float4 w = w4[i];
+    const float4 g = g4[i];
+    float4 z0 = nslot >= 1 ? s04[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 z1 = nslot >= 2 ? s14[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    opt_update(c.opt, lr, w.x, g.x, z0.x, z1.x);
+    opt_update(c.opt, lr, w.y, g.y, z0.y, z1.y);
+    opt_update(c.opt, lr, w.z, g.z, z0.z, z1.z);
+    opt_update(c.opt, lr, w.w, g.w, z0.w, z1.w);
+    w4[i] = w;
+    if (nslot >= 1) s04[i] = z0;
+    if (nslot >= 2) s14[i] = z1;
+  }
+}
+
+__global__ __launch_bounds__(256) void cp_opt_carry_kernel(CPOptCarry c) {
+  cp_opt_carry(c, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Band tile extents (rows in conv-B-output coordinates and the derived c1 / x rows).
@@ -335,7 +394,7 @@ __device__ __forceinline__ void cp_tables_a(const CPGeom& g, const CPBand& t, in
 
 __global__ __launch_bounds__(CP_THREADS) void conv_pair_fwd_kernel(CPFwdArgs a, CPZero z) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  cp_zero_early(z);
+  cp_zero_early(z, (int)gridDim.x);
   __shared__ float s_stat[2 * CP_MAXC2];
   __shared__ int s_offA[32], s_offPA[32];
   const CPGeom& g = a.g;
@@ -1112,9 +1171,16 @@ struct CPVFwdArgs {
 
 __host__ __device__ inline int cpv_txw(const CPGeom& g) { return g.W2 + g.KBw - 1 + g.KAw - 1; }
 
-template <int KBH, int KBW>
-__global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z) {
+template <int KBH, int KBW, bool CARRY>
+__global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, CPOptCarry oc) {
   const CPGeom& g = a.g;
+  // CARRY: the deferred dense update's workgroups follow the pair's (its own instantiation:
+  // the update's registers stay out of the plain forward)
+  const int npair = CARRY ? (int)gridDim.x - oc.blocks : (int)gridDim.x;
+  if (CARRY && (int)blockIdx.x >= npair) {
+    cp_opt_carry(oc, (int)blockIdx.x - npair, oc.blocks);
+    return;
+  }
   __shared__ float s_w[CPV_UW * CPV_T];                 // [wA (KA x C1) | wB (KB x C2)]
   __shared__ int s_koffA[CPV_MAXKA];                    // x-tile offset of conv-A tap k
   __shared__ float s_b[CPV_MAXC1 + CPV_MAXC2];
@@ -1288,11 +1354,11 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z) 
       float acc = 0.f;
       for (int sl = 0; sl < nsl; ++sl) acc += s_sp[sl * cols + tid];
       float* row = a.stat + (size_t)(blockIdx.x % a.nslab) * 2 * g.C2;
-      if (a.nslab >= (int)gridDim.x) row[tid] = acc;           // one row per workgroup
+      if (a.nslab >= npair) row[tid] = acc;                    // one row per workgroup
       else atomicAdd(&row[tid], acc);
     }
   }
-  cp_zero_early(z);                   // (at the end: stores in front would delay the loads)
+  cp_zero_early(z, npair);            // (at the end: stores in front would delay the loads)
   CP_STAMP(4);
 }
 
@@ -1793,6 +1859,50 @@ CSA_API int csa_conv_pair_valu_ok(const int* geom) {
   return cp_geom(geom, g) && cpv_ok(g) ? 1 : 0;
 }
 
+// The deferred dense update (CPOptCarry) the NEXT csa_conv_pair_fwd on this thread carries
+// (host state, like the tail of the carrying backward); csa_opt_carry_flush applies the same
+// update standalone.  Spans [lo, hi) of the flat buffer, float4-aligned.
+static thread_local CPOptCarry g_cp_carry{};
+
+static int cp_carry_make(CPOptCarry& c, int opt, float lr, const int64_t* step, float* w, const float* g, float* s0,
+                         float* s1, const unsigned* pending, int nseg, const long* seg_lo, const long* seg_hi,
+                         int blocks) {
+  c = CPOptCarry{};
+  if (nseg < 1 || nseg > CP_MAXCS || !w || !g || !pending || blocks < 1) return -1;
+  if (opt_nslots(opt) >= 1 && !s0) return -1;
+  if (opt_nslots(opt) >= 2 && !s1) return -1;
+  c.opt = opt; c.lr = lr; c.step = step; c.w = w; c.g = g; c.s0 = s0; c.s1 = s1; c.pending = pending;
+  c.count = nseg;
+  c.start4[0] = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (seg_lo[i] % 4 || seg_hi[i] % 4 || seg_hi[i] <= seg_lo[i]) return -1;
+    c.lo4[i] = seg_lo[i] / 4;
+    c.start4[i + 1] = c.start4[i] + (seg_hi[i] - seg_lo[i]) / 4;
+  }
+  c.blocks = blocks;
+  return 0;
+}
+
+CSA_API int csa_conv_pair_fwd_carry(int opt, float lr, const int64_t* step, float* w, const float* g, float* s0,
+                                    float* s1, const unsigned* pending, int nseg, const long* seg_lo,
+                                    const long* seg_hi, int blocks) {
+  return cp_carry_make(g_cp_carry, opt, lr, step, w, g, s0, s1, pending, nseg, seg_lo, seg_hi, blocks);
+}
+
+// Apply a pending deferred update now (a no-op on the device when none is pending), then
+// clear the flag: every host read of the parameters between steps goes through this.
+CSA_API int csa_opt_carry_flush(int opt, float lr, const int64_t* step, float* w, const float* g, float* s0,
+                                float* s1, unsigned* pending, int nseg, const long* seg_lo, const long* seg_hi,
+                                int blocks, hipStream_t st) {
+  CPOptCarry c;
+  const int rc = cp_carry_make(c, opt, lr, step, w, g, s0, s1, pending, nseg, seg_lo, seg_hi, blocks);
+  if (rc) return rc;
+  hipLaunchKernelGGL(cp_opt_carry_kernel, dim3((unsigned)blocks), dim3(256), 0, st, c);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemsetAsync(pending, 0, sizeof(unsigned), st);
+}
+
 CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB,
                               const float* bB, int actB, float alphaB, float* y, uint8_t* argmax, float* stat,
@@ -1805,6 +1915,8 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
     z.n4[k] = zero_n[k] / 4;
   }
   z.n = nzero;
+  const CPOptCarry oc = g_cp_carry;
+  g_cp_carry = CPOptCarry{};
   CPFwdArgs a{};
   if (!cp_geom(geom, a.g) || cp_lds(a.g, false) > CP_LDS_MAX) return -1;
   a.img = img; a.idx = idx; a.cursor = cursor; a.wA = wA; a.bA = bA; a.actA = actA; a.alphaA = alphaA;
@@ -1812,10 +1924,17 @@ CSA_API int csa_conv_pair_fwd(const int* geom, const uint8_t* img, const int64_t
   a.nslab = nslab < 1 ? 1 : nslab;
   if (cpv_ok(a.g)) {
     CPVFwdArgs v{a.g, img, idx, cursor, wA, bA, actA, alphaA, wB, bB, actB, alphaB, y, argmax, stat, a.nslab};
-    if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z);
-    else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3>), dim3((unsigned)(a.g.B * a.g.nbands)), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z);
+    const unsigned grid = (unsigned)(a.g.B * a.g.nbands + oc.blocks);
+    if (oc.blocks) {
+      if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2, true>), dim3(grid), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z, oc);
+      else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3, true>), dim3(grid), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z, oc);
+    } else {
+      if (a.g.KBh == 2) hipLaunchKernelGGL((cpv_fwd_kernel<2, 2, false>), dim3(grid), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z, oc);
+      else hipLaunchKernelGGL((cpv_fwd_kernel<3, 3, false>), dim3(grid), dim3(CPV_T), cpv_fwd_lds(a.g), st, v, z, oc);
+    }
     return (int)hipGetLastError();
   }
+  if (oc.blocks) return -7;                        // only the VALU forward carries the update
   static bool attr = hipFuncSetAttribute((const void*)conv_pair_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;

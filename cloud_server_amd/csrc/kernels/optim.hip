@@ -85,7 +85,8 @@ struct OptArgs {
   BatchStage stage;                // next step's batch gathered by the trailing blocks
   int fast;                        // no folds: the FastSegs loop (two float4 per thread in flight)
   FastSegs fs;
-};
+  unsigned* set_pending;           // data parallel: raise the deferred dense update's flag
+};                                 // (csa_conv_pair_fwd_carry: the next pair forward applies it)
 
 constexpr int MAXS = 16;   // stripes / partial rows per folded gradient
 
@@ -179,6 +180,7 @@ __device__ __forceinline__ void opt_duties(const OptArgs& a, long tid, long nth)
 
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   OPT_STAMP(0);
+  if (a.set_pending && blockIdx.x == 0 && threadIdx.x == 0) *a.set_pending = 1u;
   const int nmain = (int)gridDim.x - a.stage.blocks;
   if ((int)blockIdx.x >= nmain) {
     stage_gather(a.stage, (int)blockIdx.x - nmain);
@@ -261,6 +263,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
 // optim_kernel the extra live registers cut that kernel's occupancy to two waves per SIMD.
 __global__ __launch_bounds__(256) void optim_fast_kernel(OptArgs a) {
   OPT_STAMP(0);
+  if (a.set_pending && blockIdx.x == 0 && threadIdx.x == 0) *a.set_pending = 1u;
   const int nmain = (int)gridDim.x - a.stage.blocks;
   if ((int)blockIdx.x >= nmain) {
     stage_gather(a.stage, (int)blockIdx.x - nmain);
@@ -365,6 +368,11 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
                             const int64_t* st_cursor, int st_B, long st_imsz, uint8_t* st_out_img,
                             int64_t* st_out_lbl, hipStream_t st);
 
+// The flag the NEXT csa_optimizer2s launch on this thread raises (host state, consumed by
+// that call): the data-parallel programs' deferred dense update (conv_pair.hip CPOptCarry).
+static thread_local unsigned* g_opt_set_pending = nullptr;
+CSA_API void csa_optimizer_set_pending(unsigned* flag) { g_opt_set_pending = flag; }
+
 // A network whose first unit reads no raw images (a dense / standalone norm / pool first
 // layer) takes its float input [B][D] = images[rows[cursor]] / 255 from this one launch
 // (was index_select + to(float) + mul: three torch kernels per step).  One thread per
@@ -419,6 +427,8 @@ CSA_API int csa_optimizer2s(int opt, float* w, float* g, float* s0, float* s1, l
   if (st_out_img && (st_imsz % 4 || st_B <= 0)) return -1;
   if (n % 4 || nzero > MAXZ || nfold > MAXF || nkeep > MAXK || nseg > MAXSEG) return -1;
   OptArgs a{};
+  a.set_pending = g_opt_set_pending;
+  g_opt_set_pending = nullptr;
   a.keep.count = nkeep;
   for (int i = 0; i < nkeep; ++i) {
     if (keep_lo[i] % 4 || keep_hi[i] % 4) return -1;

@@ -47,7 +47,7 @@ def rccl_env_defaults() -> None:
       so the first collective of the dedicated capture group
       (``GradSync._setup_capture_group``) may be one inside a capture;
     * ``TORCH_NCCL_TRACE_BUFFER_SIZE`` — the flight recorder, whose active list tells when
-      the watchdog has retired that group's one eager collective (``dp.wait_retired``)."""
+      the watchdog has retired that group's one eager collective (``utils.graphs.wait_retired``)."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
     os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")

@@ -38,36 +38,9 @@ import torch.distributed as dist
 from ..utils.tracing import trace_range
 from .dist import DistContext
 from . import xgmi as _xg
-from ..utils.graphs import capture
+from ..utils.graphs import capture, wait_retired
 
 DEFAULT_BUCKET_BYTES = 32 << 20   # one bucket covers the sample model's 9.1 MB gradient
-
-
-def wait_retired(group, timeout_s: float = 10.0) -> Optional[bool]:
-    """Block until the process-group watchdog has retired every eager collective of
-    ``group`` (none left in the flight recorder's active list).  True once retired, False
-    on timeout, None where the flight recorder is off (TORCH_NCCL_TRACE_BUFFER_SIZE=0)."""
-    import json
-    import time
-    try:
-        from torch._C._distributed_c10d import _dump_nccl_trace_json
-    except ImportError:  # pragma: no cover
-        return None
-    if int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) <= 0:
-        return None
-    name = dist.distributed_c10d._get_process_group_name(group)
-    t0 = time.perf_counter()
-    while True:
-        try:
-            dump = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
-        except Exception:  # pragma: no cover - dump format / availability
-            return None
-        active = [e for e in dump.get("entries", []) if name in json.dumps(e.get("process_group", ""))]
-        if not active:
-            return True
-        if time.perf_counter() - t0 > timeout_s:
-            return False
-        time.sleep(0.005)
 
 
 _CAP: list = []        # [(default group, capture group, retired)] of this process
@@ -81,7 +54,17 @@ def capture_group(device: torch.device):
     default = dist.distributed_c10d._get_default_group()
     if _CAP and _CAP[0][0] is default:
         return _CAP[0][1], _CAP[0][2]
-    g = dist.new_group(backend="nccl", device_id=device)
+    # its RCCL stream from torch's HIGH-priority stream pool: the default group draws from
+    # the low-priority one, so the two groups can never share a HIP stream (a captured
+    # collective would otherwise turn the default group's stream into a capturing one under
+    # an eager work the watchdog still polls: hipErrorCapturedEvent, utils/streams.py)
+    opts = None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+    except Exception:  # pragma: no cover - backend without options
+        opts = None
+    g = dist.new_group(backend="nccl", device_id=device, pg_options=opts)
     t = torch.ones(1, device=device)
     dist.all_reduce(t, group=g)
     if int(t.item()) != dist.get_world_size():
@@ -287,13 +270,20 @@ class GradSync:
             cands["twoshot"] = two
         return self._time_fns(cands)
 
+    def _tune_side(self):
+        """The tuner's warm-up stream (outside torch's stream pool: utils/streams.py)."""
+        if getattr(self, "_tside", None) is None:
+            from ..utils.streams import dedicated_stream
+            self._tside = dedicated_stream(self.ctx.device)
+        return self._tside
+
     def _time_fns(self, cands) -> Dict[str, float]:
         """µs per call of each candidate callable (max over ranks): an eager warm-up (RCCL
         communicator paths), then a HIP graph of 10 calls replayed 3 times."""
         dev = self.ctx.device
         out = []
         for fn in cands.values():
-            side = torch.cuda.Stream(dev)
+            side = self._tune_side()
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 fn()                          # eager warm-up (RCCL communicator paths)

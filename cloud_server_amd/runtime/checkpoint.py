@@ -103,6 +103,8 @@ def full_params(eng) -> Optional[torch.Tensor]:
 def engine_state(eng) -> Dict[str, Any]:
     """Everything needed to resume an engine exactly where it stopped.  Collective under
     the "ps" / "async_ps" strategies: call on every rank, write on the chief."""
+    if hasattr(eng, "flush_params"):
+        eng.flush_params()                  # a deferred dense update lands first
     st = eng.model.export_state()
     full = full_params(eng)
     if full is not None:
@@ -193,6 +195,7 @@ class AsyncCheckpointer:
         if not chief:
             return                                  # replicated params: the chief saves
         self.wait()
+        eng.flush_params()                          # (stream-ordered) deferred update first
         main = torch.cuda.current_stream(eng.device)
         for d, s in zip(self._dev, self._sources()):
             d.copy_(s)                              # stream-ordered device snapshot

@@ -407,8 +407,18 @@ class TrainEngine:
     def comm_ms_per_step(self) -> float:
         return getattr(self, "_comm_ms", 0.0)
 
+    def flush_params(self) -> None:
+        """Land a deferred parameter update now, ordered on the current stream (no host
+        sync): the data-parallel all-reduce programs apply the dense layers' update in the
+        next step's first launch (HipProgram._plan_carry).  Every read of the parameters
+        between steps goes through here or through ``sync_device``."""
+        prog = getattr(self, "program", None)
+        if prog is not None and getattr(prog, "carry", None) is not None:
+            prog.flush()
+
     def sync_device(self) -> None:
         if self.device.type == "cuda":
+            self.flush_params()
             torch.cuda.synchronize(self.device)
 
     def metrics_since(self, start_step: int) -> Dict[str, float]:

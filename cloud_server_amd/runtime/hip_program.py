@@ -44,6 +44,7 @@ from ..models.dsl import ActSpec, ConvSpec, DenseSpec, LayerPlan, NormSpec, Pool
 from ..ops import fused as K
 from ..ops import fused as _FK      # (K is shadowed by feature counts inside _alloc)
 from ..ops import optim_ref
+from ..utils.streams import dedicated_stream
 
 
 class Unsupported(Exception):
@@ -192,8 +193,74 @@ class HipProgram:
         self._zero_now()
         self._plan_stage()
         self._plan_grad_buckets()
+        self._plan_carry()
         self.opt_segments = self._opt_segments()
         self._plan_tail()
+
+    # ------------------------------------------------------------------ DP deferred update
+    def _plan_carry(self) -> None:
+        """Data-parallel all-reduce programs: the dense layers' parameter update, which must
+        follow the gradient exchange, runs as extra workgroups of the NEXT step's pair
+        forward (conv_pair.hip ``CPOptCarry``) instead of in the flat optimizer launch after
+        the exchange — those parameters are read again only by that step's dense forwards.
+        The flat optimizer launch keeps the rest (conv, BatchNorm, head parameters and the
+        side jobs) and raises a device flag; ``flush`` applies a pending update before any
+        host read of the parameters (TrainEngine.flush_params).  Only gradients stored whole
+        every step (keep ranges) are carried: the carry does not zero accumulators."""
+        self.carry = None
+        e = self.e
+        if (not e.ctx.enabled or e.sync.strategy != "allreduce" or e.aps is not None or self.pair is None
+                or os.environ.get("CSA_DP_CARRY", "1") != "1"
+                or not self.lib.csa_conv_pair_valu_ok(K.ints(self.pair))):
+            return
+        offs = self.model.state.offsets
+        keep = set(self.keep_ranges)
+        n = self.e.flat.numel()
+        spans = sorted(offs.values())
+        ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
+        carried, segs = set(), []
+        for u in self.units:
+            if u.kind != "dense" or (u.fused and self.fused) or u.lr_update:
+                continue
+            names = [f"{u.layer.name}.weight", f"{u.layer.name}.bias"]
+            if not all((offs[nm], offs[nm] + (self.gviews[nm].numel() // 4) * 4) in keep for nm in names):
+                continue
+            for nm in names:
+                carried.add(offs[nm])
+        if not carried:
+            return
+        for o in spans:
+            if o not in carried:
+                continue
+            lo, hi = o - o % 4, -(-ends[o] // 4) * 4
+            if segs and segs[-1][1] >= lo:
+                segs[-1][1] = max(segs[-1][1], hi)
+            else:
+                segs.append([lo, hi])
+        if len(segs) > 4:
+            return
+        m4 = sum(hi - lo for lo, hi in segs) // 4
+        self.carry = segs
+        self.carry_offsets = carried
+        self.carry_blocks = max(1, min(1024, -(-m4 // 256)))
+        self.carry_pending = torch.zeros(1, dtype=torch.int32, device=e.device)
+
+    def _carry_args(self):
+        e = self.e
+        s0 = e.slots[0] if e.slots.shape[0] > 0 else None
+        s1 = e.slots[1] if e.slots.shape[0] > 1 else None
+        lo = (C.c_long * 4)(*[x[0] for x in self.carry])
+        hi = (C.c_long * 4)(*[x[1] for x in self.carry])
+        return (e.opt_id, float(e.lr), K.ptr(e.dstep), K.ptr(e.flat), K.ptr(e.flat_grad), K.ptr(s0), K.ptr(s1),
+                K.ptr(self.carry_pending), len(self.carry), lo, hi, self.carry_blocks)
+
+    def flush(self, st=None) -> None:
+        """Apply a pending deferred dense update now (stream-ordered; a no-op on the device
+        when none is pending) and clear its flag."""
+        if getattr(self, "carry", None) is None:
+            return
+        self._rc(self.lib.csa_opt_carry_flush(*self._carry_args(), st if st is not None else K.stream()),
+                 "opt_carry_flush")
 
     # ------------------------------------------------------------------ DP overlap
     def _plan_grad_buckets(self) -> None:
@@ -226,7 +293,7 @@ class HipProgram:
         self.bucket_at: Dict[object, tuple] = {}
         if not self.overlap:
             return
-        self.side = torch.cuda.Stream(e.device)
+        self.side = dedicated_stream(e.device)      # (captured: outside torch's stream pool)
         offs = e.model.state.offsets
         end = e.flat.numel()
 
@@ -305,7 +372,7 @@ class HipProgram:
                 self.lr_ranges.append((a, b))
                 open_range = True
         if self.lr_units:
-            self.lr_side = torch.cuda.Stream(dev)
+            self.lr_side = dedicated_stream(dev)
             self.lr_first = min(self.units.index(u) for u in self.lr_units)
 
     def _lowrank_gather_inputs(self) -> None:
@@ -1081,6 +1148,8 @@ class HipProgram:
 
     def reset_after_warmup(self) -> None:
         self._zero_now()
+        if getattr(self, "carry", None) is not None:
+            self.carry_pending.zero_()      # the restored parameters have no pending update
         self.prime()
 
     # ------------------------------------------------------------------ helpers
@@ -1360,6 +1429,8 @@ class HipProgram:
             # (the tail program: the dense split-K outputs of this step, zeroed by the pair
             # forward's threads — not when predicting, which zeroes them itself)
             fz = [] if getattr(self, "_predicting", False) else getattr(self, "fwd_zero", [])
+            if getattr(self, "carry", None) is not None and not getattr(self, "_predicting", False):
+                self._rc(lib.csa_conv_pair_fwd_carry(*self._carry_args()), "conv_pair_fwd_carry")
             self._rc(lib.csa_conv_pair_fwd(
                 K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
                 K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,
@@ -1523,6 +1594,7 @@ class HipProgram:
         running statistics unless the model normalises with batch statistics in eval
         (``bn_mode == "batch"``), exactly as ``DigitNet.forward`` in eval mode."""
         st = K.stream()
+        self.flush(st)                      # a deferred dense update lands before the forward
         self._eval_bn = self.model.bn_mode != "batch"
         self._predicting = True
         # split-K forward outputs (and, with batch statistics, the forward BN slabs) are
@@ -1761,7 +1833,7 @@ class HipProgram:
         offs = self.model.state.offsets
         spans = sorted(offs.values())
         ends = {o: (spans[i + 1] if i + 1 < len(spans) else n) for i, o in enumerate(spans)}
-        skip = set()
+        skip = set(getattr(self, "carry_offsets", set()) if getattr(self, "carry", None) else set())
         for u in self.units:
             if u.kind == "dense" and ((u.fused and self.fused) or u.lr_update):
                 skip |= {offs[f"{u.layer.name}.weight"], offs[f"{u.layer.name}.bias"]}
@@ -1853,6 +1925,8 @@ class HipProgram:
         else:
             stage = (None, None, None, None, 0, 0, None, None)
             cursor_args = (K.ptr(e.stream.cursor), e.stream.wrap)
+        if getattr(self, "carry", None) is not None:
+            lib.csa_optimizer_set_pending(K.ptr(self.carry_pending))
         self._rc(lib.csa_optimizer2s(
             e.opt_id, K.ptr(w), K.ptr(g), K.ptr(s0), K.ptr(s1), w.numel(), slo, shi, len(segs),
             0 if self.ps_mode else 1, float(e.lr), K.ptr(e.dstep),

@@ -116,7 +116,10 @@ class PackedJobs:
             if not e.warmed:
                 e._warm_up()
         main = torch.cuda.current_stream(self.device)
-        streams = [torch.cuda.Stream(self.device) for _ in self.engines]
+        from ..utils.streams import dedicated_stream
+        if len(getattr(self, "_own_streams", [])) < len(self.engines):
+            self._own_streams = [dedicated_stream(self.device) for _ in self.engines]
+        streams = self._own_streams[:len(self.engines)]
         g = torch.cuda.CUDAGraph()
         with capture(g):
             cap = torch.cuda.current_stream(self.device)

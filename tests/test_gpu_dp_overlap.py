@@ -55,7 +55,7 @@ def test_overlap_buckets_match_single_gpu(pg, monkeypatch):
     b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
     for _ in range(20):
         a.step(); b.step()
-    torch.cuda.synchronize()
+    a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
 
 
@@ -67,6 +67,7 @@ def test_lowrank_strategy_matches_single_gpu(pg, monkeypatch):
     ds = synthetic_mnist(2000, seed=0)
     ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
     monkeypatch.setenv("CSA_XGMI", "1")
+    monkeypatch.setenv("CSA_GRAPH_STEPS", "8")
     a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy="lowrank")
     assert a.sync.xgmi is not None, a.sync.xgmi_reason
     assert a.backend == "hip", a.fallback_reason
@@ -88,7 +89,7 @@ def test_lowrank_strategy_matches_single_gpu(pg, monkeypatch):
     assert a.group_steps() == 8
     a.run_steps(16); b.run_steps(16)
     assert a.graph_k is not None and a.host_step == b.host_step == 20
-    torch.cuda.synchronize()
+    a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     assert a.sync._choice["lr_x"] is not None and a.sync._choice["lr_dy"] is not None, a.sync._choice
     a.sync.check()
     for n in a.model.state.shapes:          # the two flat layouts differ: compare by name
@@ -118,7 +119,7 @@ def test_ps_and_rccl_programs_match_single_gpu(pg, monkeypatch, strategy, xgmi):
     for _ in range(4):
         a.step(); b.step()
     a.run_steps(16); b.run_steps(16)
-    torch.cuda.synchronize()
+    a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     assert a.host_step == b.host_step == 20 and int(a.dstep.item()) == 20
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
     ma, mb = a.metrics_since(0), b.metrics_since(0)
@@ -140,7 +141,7 @@ def test_collective_autotune_records_both_paths(pg, monkeypatch):
     b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
     for _ in range(20):
         a.step(); b.step()
-    torch.cuda.synchronize()
+    a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     a.sync.check()
     assert set(a.sync.xgmi_tuning) >= {"lr_x", "lr_dy"}, a.sync.xgmi_tuning
     for v in a.sync.xgmi_tuning.values():
@@ -208,7 +209,7 @@ def test_capture_right_after_eager_collectives(pg, monkeypatch, strategy):
     a.prepare_group_graph()                      # every multi-step capture, right away
     b.prepare_group_graph()
     a.run_steps(15); b.run_steps(15)
-    torch.cuda.synchronize()
+    a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     assert a.host_step == b.host_step == 16
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
 
@@ -233,7 +234,7 @@ def test_hf_programs_match_single_gpu(pg, monkeypatch, strategy):
     for _ in range(4):
         a.step(); b.step()
     a.run_steps(16); b.run_steps(16)
-    torch.cuda.synchronize()
+    a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     assert a.host_step == b.host_step == 20 and int(a.dstep.item()) == 20
     assert p.tail_error() == 0
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)

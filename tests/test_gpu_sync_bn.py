@@ -53,7 +53,7 @@ def _worker(rank, world, port, q):
                 assert eng.model.sync_bn
                 w0 = eng.flat.clone()
                 eng.step()
-                torch.cuda.synchronize()
+                eng.sync_device()               # (lands a deferred dense update)
                 out[backend] = (eng, w0, eng.flat.clone())
             eh, w0h, w1h = out["hip"]
             et, w0t, w1t = out["torch"]

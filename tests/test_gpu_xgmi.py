@@ -208,7 +208,7 @@ def _worker_ps(rank: int, world: int, port: int, q, phases=(("ps1", "ps"), ("ps2
                     torch.cuda.synchronize()
                     if any(c.error() for c in eng.sync.xgmi.channels.values()):
                         raise failure(f"step {i}")
-            torch.cuda.synchronize()
+            eng.sync_device()                   # (lands a deferred dense update)
             if any(c.error() for c in eng.sync.xgmi.channels.values()):
                 raise failure("after 12 steps")
             # numpy copies: a tensor would travel through shared memory that dies with this
