@@ -115,11 +115,11 @@ def capture(graph: "torch.cuda.CUDAGraph", stream: Optional["torch.cuda.Stream"]
         wait_retired()
     _enter()
     try:
-        if stream is None:
+        if stream is None and torch.cuda.is_available():
             # outside torch's stream pool: never the stream of an RCCL group (utils/streams.py)
             from .streams import capture_stream
             stream = capture_stream()
-        kw = {"stream": stream}
+        kw = {} if stream is None else {"stream": stream}
         if pool is not None:
             kw["pool"] = pool
         with torch.cuda.graph(graph, capture_error_mode="thread_local", **kw):
