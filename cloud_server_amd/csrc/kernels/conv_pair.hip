@@ -626,6 +626,22 @@ __host__ __device__ inline int cp_bwd_tab_ints(const CPBwdLayout& L) { return L.
 // x tile and BN slab rows per thread.  The host picks ONE when every band fits.
 constexpr int CPB_UP = 8, CPB_UX = 2, CPB_US = 8, CPB_UT = 4;
 
+// The route's extent for workgroup (image b, band of L): unit rows [ua, ub) of the pair's
+// output (pooled or not) whose gradients land in the band's zero-padded dc2 tile.
+constexpr int CP_RU = 4;                   // route operands per thread and chunk
+struct CPRoute { int n2a, n2b, ua, n; long base; };
+__device__ __forceinline__ CPRoute cp_route(const CPGeom& g, const CPBwdLayout& L, int b) {
+  CPRoute r;
+  r.n2a = max(0, L.d2y0);
+  r.n2b = min(g.H2, L.d2y0 + L.D2H - 1);
+  const int ow = g.pool ? g.PW : g.W2;
+  r.ua = g.pool ? r.n2a / 2 : r.n2a;
+  const int ub = g.pool ? min(g.PH, (r.n2b + 1) / 2) : r.n2b;
+  r.n = max(0, ub - r.ua) * ow * g.C2;
+  r.base = ((long)b * (g.pool ? g.PH : g.H2) + r.ua) * ow * g.C2;
+  return r;
+}
+
 template <bool ONE>
 __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, float* smem) {
   __shared__ float s_bn[4 * CP_MAXC2];
@@ -667,6 +683,9 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   const int scol = (int)threadIdx.x % C2x2, srow = (int)threadIdx.x / C2x2;
   const bool sact = srow < sper;
   float pv[CPB_UP], vf[CPB_US], vb[CPB_US], sc = 0.f, of = 0.f;
+  const CPRoute rt = cp_route(g, L, b);
+  float rgz[CP_RU], ryv[CP_RU];
+  int ram[CP_RU];
   bool pok[CPB_UP], xok[CPB_UX];
   uint8_t xv[CPB_UX];
   // precomputed index tables: issued first (the host checks that a band's region fits
@@ -716,6 +735,18 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
       const int y = y0 + r, x = x0 + xx;
       xok[u] = e < nX && y >= 0 && y < g.H && x >= 0 && x < g.W;
       xv[u] = src[xok[u] ? ((long)y * g.W + x) * g.C0 + c : 0];
+    }
+    // the route's first chunk (dz, y, argmax of the band's unit rows: written by earlier
+    // launches) — in flight under the tables and the BatchNorm fold instead of a round
+    // trip of its own after them
+    if (rt.n > 0) {
+#pragma unroll
+      for (int u = 0; u < CP_RU; ++u) {
+        const int i = min(u * CP_THREADS + (int)threadIdx.x, rt.n - 1);
+        rgz[u] = a.dz[rt.base + i];
+        ryv[u] = a.y[rt.base + i];
+        ram[u] = g.pool ? (int)a.argmax[rt.base + i] : 0;
+      }
     }
   } else {
     const uint8_t* src = cp_image(a.img, a.idx, a.cursor, b, g.B, (long)g.H * g.W * g.C0);
@@ -810,23 +841,28 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   CP_STAMP(9);
   // ---- route: dc2 (zero-padded tile) for conv-B-output rows [d2y0, d2y0 + D2H - 1)
   {
-    const int n2a = max(0, L.d2y0), n2b = min(g.H2, L.d2y0 + L.D2H - 1);
+    const int n2a = rt.n2a, n2b = rt.n2b;
     const int ow = g.pool ? g.PW : g.W2;
-    const int ua = g.pool ? n2a / 2 : n2a, ub = g.pool ? min(g.PH, (n2b + 1) / 2) : n2b;   // unit rows
-    const int n = max(0, ub - ua) * ow * g.C2;
+    const int ua = rt.ua;
+    const int n = rt.n;
     const float inv_n = a.bn_on ? 1.0f / a.bn.count : 0.f;
-    const long base = ((long)b * (g.pool ? g.PH : g.H2) + ua) * ow * g.C2;
+    const long base = rt.base;
     const FastDiv dC(g.C2), dow(ow);
-    constexpr int U = 4;
+    constexpr int U = CP_RU;
     for (int i0 = 0; i0 < n; i0 += CP_THREADS * U) {
       float gz[U], yv[U];
       int am[U];
+      if (ONE && i0 == 0) {                        // prefetched with the prologue
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = min(i0 + u * CP_THREADS + (int)threadIdx.x, n - 1);
-        gz[u] = a.dz[base + i];
-        yv[u] = a.y[base + i];
-        am[u] = g.pool ? (int)a.argmax[base + i] : 0;
+        for (int u = 0; u < U; ++u) { pin(rgz[u]); pin(ryv[u]); gz[u] = rgz[u]; yv[u] = ryv[u]; am[u] = ram[u]; }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = min(i0 + u * CP_THREADS + (int)threadIdx.x, n - 1);
+          gz[u] = a.dz[base + i];
+          yv[u] = a.y[base + i];
+          am[u] = g.pool ? (int)a.argmax[base + i] : 0;
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {

@@ -37,6 +37,7 @@
 // and written once (32 MB) — instead of the split-K backward pair (dW written) plus the
 // flat optimizer pass (dW, W, acc re-read).
 #include "dense_update.h"
+#include <cstdlib>
 
 namespace csa {
 
@@ -89,7 +90,9 @@ static int du_cs(int K, int N) {
   // ranks sharing ONE GPU (g_csa_shared): a 16-wave workgroup of one process was seen
   // not to be placed for as long as another process's kernel spun in a peer wait (the
   // round-5 world-2 stall: profiles/r5_notes.md); 256-thread blocks always were
-  const int minb = (g_csa_packed || g_csa_shared) ? (1 << 30) : 128;
+  // CSA_DU_WIDE=0: 128-column blocks everywhere (an A/B knob for the one-GPU programs)
+  static const bool narrow_env = [] { const char* e = getenv("CSA_DU_WIDE"); return e && e[0] == '0'; }();
+  const int minb = (g_csa_packed || g_csa_shared || narrow_env) ? (1 << 30) : 128;
   if (N <= 512 && groups >= minb) return 1;
   return (N + 127) / 128;
 }

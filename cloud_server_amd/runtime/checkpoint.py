@@ -126,6 +126,8 @@ def engine_state(eng) -> Dict[str, Any]:
 
 
 def restore_engine(eng, obj: Dict[str, Any]) -> None:
+    if hasattr(eng, "flush_params"):
+        eng.flush_params()                  # no deferred update may land on restored params
     eng.model.import_state(obj["model"])
     slots = obj["slots"]
     layout = obj.get("layout")
