@@ -191,6 +191,9 @@ def main() -> int:
     # horizontal fusion: the deferred dense updates are host-side records that the pair
     # backward consumes, so every replay of that launch re-records them first
     defers = [(fn, args) for name, fn, args in rec.calls if name == "csa_dense_update_defer"]
+    if os.environ.get("MB_HF_ONLY"):        # e.g. MB_HF_ONLY=0: carry only the first deferred segment
+        keep = {int(x) for x in os.environ["MB_HF_ONLY"].split(",")}
+        defers = [d for i, d in enumerate(defers) if i in keep]
     host_only = ("csa_dense_update_defer", "csa_dense_update_clear", "csa_dense_update_pending")
 
     def call(name, fn, args):
