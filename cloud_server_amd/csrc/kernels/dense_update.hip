@@ -353,3 +353,19 @@ CSA_API int csa_dense_update_flush(hipStream_t st) {
 }
 
 CSA_API void csa_dense_update_clear() { g_du_def.n = 0; g_du_def.head = -1; }
+
+// Launch only the LAST deferred segment now, on ``st`` (its own stream: a graph branch that
+// overlaps the carrying launch and the next step's first launch), and drop it from the list.
+CSA_API int csa_dense_update_flush_last(hipStream_t st) {
+  const int n = g_du_def.n;
+  if (n < 1) return 0;
+  DUSegs u{};
+  u.nseg = 1;
+  u.head = g_du_def.head == n - 1 ? 0 : -1;
+  u.seg[0] = g_du_def.seg[n - 1];
+  u.start[0] = 0;
+  for (int s2 = 1; s2 <= DU_MAXDEF; ++s2) u.start[s2] = g_du_def.blocks[n - 1];
+  g_du_def.n = n - 1;
+  if (g_du_def.head == n - 1) g_du_def.head = -1;
+  return du_flush_segs(u, st);
+}

@@ -82,6 +82,7 @@ _SIGS = {
     "csa_conv_pair_fwd_carry": (I, [I, F, P, P, P, P, P, P, I, P, P, I]),
     "csa_opt_carry_flush": (I, [I, F, P, P, P, P, P, P, I, P, P, I, P]),
     "csa_optimizer_set_pending": (None, [P]),
+    "csa_dense_update_flush_last": (I, [P]),
     "csa_conv_pair_tail_table_bytes": (L, [P, I]),
     "csa_conv_pair_tail_plan": (I, [P, I, I, P, P, P, P, P, P, P, P, I]),
     "csa_dense_update_grad_mode": (I, [P, P]),

@@ -222,6 +222,7 @@ class TrainEngine:
         with torch.cuda.stream(s):
             for _ in range(2):      # warm up allocator / autotuning / RCCL comms off-graph
                 self.program.run()
+            self._join_branch()
         torch.cuda.current_stream(self.device).wait_stream(s)
         if device_sync:
             torch.cuda.synchronize(self.device)
@@ -231,13 +232,23 @@ class TrainEngine:
         self._restore(snap)
         self.warmed = True
 
+    def _join_branch(self) -> None:
+        """Join the program's pending side-stream branch (HipProgram.join_branch) into the
+        current stream: before a capture starts (a capture may not wait on work issued
+        outside it) and at the end of every captured sequence (every fork joined)."""
+        prog = getattr(self, "program", None)
+        if prog is not None and hasattr(prog, "join_branch"):
+            prog.join_branch()
+
     def _capture(self) -> None:
         self._warm_up()
         g = torch.cuda.CUDAGraph()
+        self._join_branch()
         # thread_local: the RCCL watchdog thread queries events of earlier collectives while
         # this thread captures; in "global" mode that query aborts the process
         with capture(g):
             self.program.run()
+            self._join_branch()
         self.graph = g
         # capture does not execute: the cursor/step still point at this step
 
@@ -300,11 +311,13 @@ class TrainEngine:
         if self.graph is None or self.graph_k is not None:
             return
         graphs = {}
+        self._join_branch()
         for k in self.group_sizes():
             g = torch.cuda.CUDAGraph()
             with capture(g):
                 for _ in range(k):
                     self.program.run()
+                self._join_branch()
             graphs[k] = g
         if not graphs:
             return

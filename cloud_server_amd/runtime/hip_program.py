@@ -570,6 +570,26 @@ class HipProgram:
             self.head_row and last.kind == "dense" and last.fused and len(self.units) > 2
             and not last.in_tf.has_bn
             and self.lib.csa_head_dgrad_ok(self.B, last.layer.spec.hidden, last.layer.in_shape.numel))
+        # CSA_DENSE_BRANCH=1: the FIRST dense layer's deferred update (fc1: 980 of the
+        # carrying launch's ~1 700 workgroups) runs as its own launch on a side stream — a
+        # graph branch from after its input-gradient launch to before the next step's
+        # BatchNorm apply that rewrites its operand — instead of inside the pair backward
+        self.br_unit = None
+        self._br_pending = False
+        # (its weight-gradient operand must be the materialised BatchNorm output, which only
+        # the next step's bn_act_apply rewrites: _alloc's xt)
+        d0 = dense[0]
+        if (not self.dp_hf and os.environ.get("CSA_DENSE_BRANCH", "0") == "1" and d0.in_tf.has_bn
+                and d0.layer.in_shape.numel % 4 == 0 and d0 is not self.units[-1]):
+            self.br_unit = d0
+            self.br_side = dedicated_stream(self.e.device)
+
+    def join_branch(self) -> None:
+        """Join a pending dense-update branch into the current stream (a capture ends with
+        every forked stream joined; the next step's BatchNorm apply needs it done)."""
+        if getattr(self, "_br_pending", False):
+            torch.cuda.current_stream(self.e.device).wait_stream(self.br_side)
+            self._br_pending = False
 
     # ------------------------------------------------------------------ pair-backward tail
     def _plan_tail(self) -> None:
@@ -1472,6 +1492,8 @@ class HipProgram:
                     e.sync.allreduce_tensors([oslab], tag=f"bnf{k}")
             else:
                 fin, fout = lp.in_shape.numel, lp.spec.hidden
+                if u is getattr(self, "br_unit", None):
+                    self.join_branch()          # the previous step's update read u.xt and W
                 if u.xt is not None:
                     self._rc(lib.csa_bn_act_apply(
                         K.ptr(u.x), K.ptr(u.xt), B * fin, tf.slab.shape[2], *bn, in_act, in_alpha,
@@ -1798,6 +1820,12 @@ class HipProgram:
                     K.ptr(u.x.view(B, -1)), _act_id(tf.act), _alpha(tf.act), *self._bn_args_c(tf),
                     K.ptr(tf.bwd_slab) if tf.has_bn else None, K.ptr(getattr(tf, "bn_tab", None)),
                     K.ptr(u.du_part), K.ptr(u.du_cnt), st), "dense_bwd_dgrad")
+            if u is getattr(self, "br_unit", None):
+                # the update reads W before nothing else does: fork after the input gradient
+                cur = torch.cuda.current_stream(e.device)
+                self.br_side.wait_stream(cur)
+                self._rc(lib.csa_dense_update_flush_last(self.br_side.cuda_stream), "dense_update_branch")
+                self._br_pending = True
             return
         if self.fused_grad:
             # data parallel: the same launch stores dW / db whole into the flat gradient

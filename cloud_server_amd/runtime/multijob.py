@@ -63,6 +63,7 @@ class PackedJobs:
                 with torch.cuda.stream(s):
                     for _ in range(k):
                         e.program.run()
+                    e._join_branch()
             for s in streams:
                 cap.wait_stream(s)
         self.graph_k = g
@@ -127,6 +128,7 @@ class PackedJobs:
                 s.wait_stream(cap)            # fork: each job a branch of the graph
                 with torch.cuda.stream(s):
                     e.program.run()
+                    e._join_branch()
             for s in streams:
                 cap.wait_stream(s)            # join
         self.graph = g
