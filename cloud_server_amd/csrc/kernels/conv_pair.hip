@@ -36,10 +36,11 @@ constexpr int CP_MAXC2 = 64;
 constexpr int CP_MAXC1 = 32;
 constexpr size_t CP_LDS_MAX = 150 * 1024;
 
-__constant__ long long* g_cp_dbg = nullptr;   // diagnostics: s_memtime stamps of block 0
+__constant__ long long* g_cp_dbg = nullptr;   // diagnostics: s_memtime stamps of one block
+__constant__ int g_cp_dbg_blk = 0;            //   (block 0 unless csa_cp_debug_block chose another)
 #define CP_STAMP(i)                                                                           \
   do {                                                                                        \
-    if (g_cp_dbg && threadIdx.x == 0 && blockIdx.x == 0) g_cp_dbg[i] = (long long)__builtin_amdgcn_s_memtime(); \
+    if (g_cp_dbg && threadIdx.x == 0 && (int)blockIdx.x == g_cp_dbg_blk) g_cp_dbg[i] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
 struct CPGeom {
@@ -525,6 +526,7 @@ struct CPBwdArgs {
   float* dwA; float* dbA; float* dwB; float* dbB; int stripes;
   const int* tabs; int tab_stride;  // per-band index tables (csa_conv_pair_bwd_tables) or null
   unsigned* img_tk;                 // tail: +1 per workgroup once its image tile is in LDS (or null)
+  const float* bn_tab;              // [mean | rstd | a | b][C2] the step's bn_act_apply wrote, or null
 };
 
 // LDS carve of the backward (float offsets), shared by the kernel and the host size check.
@@ -712,7 +714,17 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
       const float* p = !ok ? a.wA : (inA ? a.wA + k * g.C1 + n : a.wB + f);
       pv[u] = *p;
     }
-    if (a.bn_on) {
+    if (a.bn_on && a.bn_tab) {
+      // the forward tables come folded (one value per thread); of the backward slab only
+      // the row batches that exist are loaded (a uniform branch per batch)
+      sc = a.bn_tab[min((int)threadIdx.x, 4 * g.C2 - 1)];
+#pragma unroll
+      for (int u = 0; u < CPB_US; ++u) {
+        const int r = srow + u * sper;
+        vb[u] = 0.f;
+        if (u * sper < a.bwd_nslab) vb[u] = a.bwd_slab[(size_t)(sact && r < a.bwd_nslab ? r : 0) * C2x2 + scol];
+      }
+    } else if (a.bn_on) {
       const int cc = (int)threadIdx.x < g.C2 ? (int)threadIdx.x : g.C2 - 1;
 #pragma unroll
       for (int u = 0; u < CPB_US; ++u) {
@@ -788,7 +800,22 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   // small slabs; block 0 writes the BN parameter gradients and running statistics)
   CP_STAMP(19);
   if (a.bn_on) {
-    if (ONE) {
+    if (ONE && a.bn_tab) {
+      pin(sc);
+      float ab = 0.f;
+#pragma unroll
+      for (int u = 0; u < CPB_US; ++u) {
+        pin(vb[u]);
+        ab += srow + u * sper < a.bwd_nslab ? vb[u] : 0.f;
+      }
+      if ((int)threadIdx.x < 4 * g.C2) {
+        const int k = (int)threadIdx.x / g.C2;
+        s_bn[k * CP_MAXC2 + (int)threadIdx.x - k * g.C2] = sc;
+      }
+      __syncthreads();                             // the zeroing of s_ss
+      if (sact) atomicAdd(&s_ss[scol], ab);
+      __syncthreads();
+    } else if (ONE) {
 #pragma unroll
       for (int u = 0; u < CPB_US; ++u) { pin(vf[u]); pin(vb[u]); }
       float af = 0.f, ab = 0.f;
@@ -1874,6 +1901,10 @@ CSA_API int csa_cp_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cp_dbg), &p, sizeof(p));
 }
 
+CSA_API int csa_cp_debug_block(int b) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cp_dbg_blk), &b, sizeof(b));
+}
+
 // geom = {B, H, W, C0, KAh, KAw, PTA, PLA, C1, H1, W1, KBh, KBw, PTB, PLB, C2, H2, W2, pool, PH, PW}
 // Returns 1 when the pair is inside the fused family (the launchers below accept it).
 CSA_API int csa_conv_pair_ok(const int* geom) {
@@ -2116,6 +2147,11 @@ CSA_API int csa_conv_pair_bwd_tables(const int* geom, int* out, hipStream_t st) 
   return (int)hipGetLastError();
 }
 
+// The forward BatchNorm tables of the NEXT csa_conv_pair_bwd call (bn_act_apply's [4][C2]
+// output for this step), so its workgroups load them instead of folding the statistic slab.
+static thread_local const float* g_cp_bn_tab = nullptr;
+CSA_API void csa_conv_pair_bn_tab(const float* tab) { g_cp_bn_tab = tab; }
+
 CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t* idx, const int64_t* cursor,
                               const float* wA, const float* bA, int actA, float alphaA, const float* wB, int hasBiasB,
                               int actB, float alphaB, const float* dz, const float* y, const uint8_t* argmax,
@@ -2132,6 +2168,8 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
   a.wB = wB; a.actB = actB; a.alphaB = alphaB; a.hasBiasB = hasBiasB; a.dz = dz; a.y = y; a.argmax = argmax;
   a.bn = BNRef{bn_slab, bn_nslab, a.g.C2, bn_count, bn_eps, bn_scale, bn_offset};
   a.bn_on = bn_slab != nullptr; a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab;
+  a.bn_tab = a.bn_on ? g_cp_bn_tab : nullptr;
+  g_cp_bn_tab = nullptr;
   a.dscale = dscale; a.doffset = doffset; a.run_mean = run_mean; a.run_var = run_var; a.momentum = momentum;
   a.dwA = dwA; a.dbA = dbA; a.dwB = dwB; a.dbB = dbB; a.stripes = stripes < 1 ? 1 : stripes;
   static bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_kernel<true>,

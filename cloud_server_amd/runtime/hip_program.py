@@ -1670,6 +1670,11 @@ class HipProgram:
         simg, srows, scur = self._batch_src()
         if getattr(self, "tail", False):
             self._tail_set()
+        # this step's forward BatchNorm tables (bn_act_apply wrote them for the dense
+        # consumer): the pair's workgroups load them instead of each folding the slab
+        tab = getattr(nt, "bn_tab", None) if nt.has_bn else None
+        if tab is not None and os.environ.get("CSA_PAIR_BN_TAB", "1") == "1":
+            lib.csa_conv_pair_bn_tab(K.ptr(tab))
         self._rc(lib.csa_conv_pair_bwd(
             K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
             K.ptr(V[f"{ua.layer.name}.weight"]), K.ptr(V.get(f"{ua.layer.name}.bias")) if ua.layer.spec.bias else None,

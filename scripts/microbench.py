@@ -207,6 +207,14 @@ def main() -> int:
         # launches), and the pair backward carrying them
         lib = eng.program.lib
         pb = [(fn, args) for name, fn, args in rec.calls if name == "csa_conv_pair_bwd"][0]
+        tabs = [(fn, args) for name, fn, args in rec.calls if name == "csa_conv_pair_bn_tab"]
+        if tabs:                              # the BN-table pointer is consumed by each launch
+            pb0 = pb
+
+            def _pb(*args):
+                tabs[-1][0](*tabs[-1][1])
+                pb0[0](*args)
+            pb = (_pb, pb0[1])
 
         def timed(f):
             for _ in range(5):
@@ -236,17 +244,21 @@ def main() -> int:
         print(f"HF: pair alone {timed(pair_alone):.2f} us | updates alone {timed(upd_alone):.2f} us | "
               f"pair + updates in one launch {timed(fused):.2f} us")
         cdbg = torch.zeros(24, dtype=torch.int64, device="cuda")
-        for label, f in (("pair alone", pair_alone), ("pair + updates", fused)):
-            for _ in range(3):
-                cdbg.zero_()
-                lib.csa_cp_debug(cdbg.data_ptr())
-                f()
-                torch.cuda.synchronize()
-                lib.csa_cp_debug(None)
-            t = cdbg.tolist()
-            print(f"  {label} block 0: loads {t[16]-t[8]} tables {t[17]-t[16]} stores {t[18]-t[17]} "
-                  f"bn {t[9]-t[19]} route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} dc1 {t[13]-t[12]} "
-                  f"dwA {t[14]-t[13]} atomics {t[15]-t[14]} | total {t[15]-t[8]} (s_memtime ticks)")
+        # MB_CP_BLOCKS=0,350,699: whose stamps (pair workgroups come first in both launches)
+        for blk in [int(x) for x in os.environ.get("MB_CP_BLOCKS", "0").split(",")]:
+            lib.csa_cp_debug_block(blk)
+            for label, f in (("pair alone", pair_alone), ("pair + updates", fused)):
+                for _ in range(3):
+                    cdbg.zero_()
+                    lib.csa_cp_debug(cdbg.data_ptr())
+                    f()
+                    torch.cuda.synchronize()
+                    lib.csa_cp_debug(None)
+                t = cdbg.tolist()
+                print(f"  {label} block {blk}: loads {t[16]-t[8]} tables {t[17]-t[16]} stores {t[18]-t[17]} "
+                      f"bn {t[9]-t[19]} route {t[10]-t[9]} convA {t[11]-t[10]} dwB {t[12]-t[11]} dc1 {t[13]-t[12]} "
+                      f"dwA {t[14]-t[13]} atomics {t[15]-t[14]} | total {t[15]-t[8]} (s_memtime ticks)")
+        lib.csa_cp_debug_block(0)
         # per-block stamps of the update-only launches (100 MHz realtime: start, dY staged,
         # W landed, MFMA + update done, stores issued)
         dbg = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
