@@ -697,9 +697,10 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   if (a.tabs) {
     const int* tsrc = a.tabs + (long)band * a.tab_stride;
 #pragma unroll
-    for (int u = 0; u < CPB_UT; ++u) {
+    for (int u = 0; u < CPB_UT; ++u) {              // (batches past the table: not issued)
       const int e = u * CP_THREADS + (int)threadIdx.x;
-      tv[u] = tsrc[e < ntab ? e : 0];
+      tv[u] = 0;
+      if (u * CP_THREADS < ntab) tv[u] = tsrc[e < ntab ? e : 0];
     }
   }
   if (ONE) {
@@ -711,8 +712,9 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
       const int k = e >> 4, n = e & 15, f = e - nA;
       const bool ok = inA ? (k < L.KA && n < g.C1) : (e < nP && f < nWB);
       pok[u] = ok;
+      pv[u] = 0.f;
       const float* p = !ok ? a.wA : (inA ? a.wA + k * g.C1 + n : a.wB + f);
-      pv[u] = *p;
+      if (u * CP_THREADS < nP) pv[u] = *p;         // (whole batches past the panels: none)
     }
     if (a.bn_on && a.bn_tab) {
       // the forward tables come folded (one value per thread); of the backward slab only
@@ -746,7 +748,8 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
       dc.divmod(rem, xx, c);
       const int y = y0 + r, x = x0 + xx;
       xok[u] = e < nX && y >= 0 && y < g.H && x >= 0 && x < g.W;
-      xv[u] = src[xok[u] ? ((long)y * g.W + x) * g.C0 + c : 0];
+      xv[u] = 0;
+      if (u * CP_THREADS < nX) xv[u] = src[xok[u] ? ((long)y * g.W + x) * g.C0 + c : 0];
     }
     // the route's first chunk (dz, y, argmax of the band's unit rows: written by earlier
     // launches) — in flight under the tables and the BatchNorm fold instead of a round
@@ -755,9 +758,13 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
 #pragma unroll
       for (int u = 0; u < CP_RU; ++u) {
         const int i = min(u * CP_THREADS + (int)threadIdx.x, rt.n - 1);
-        rgz[u] = a.dz[rt.base + i];
-        ryv[u] = a.y[rt.base + i];
-        ram[u] = g.pool ? (int)a.argmax[rt.base + i] : 0;
+        rgz[u] = ryv[u] = 0.f;
+        ram[u] = 0;
+        if (u * CP_THREADS < rt.n) {               // (batches past the band's rows: none)
+          rgz[u] = a.dz[rt.base + i];
+          ryv[u] = a.y[rt.base + i];
+          ram[u] = g.pool ? (int)a.argmax[rt.base + i] : 0;
+        }
       }
     }
   } else {
