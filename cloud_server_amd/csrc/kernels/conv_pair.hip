@@ -1206,10 +1206,19 @@ __device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs
   cp_tail_body(t, npair, bid - npair - nupd);
 }
 
+// diagnostics: [block][2] start / end (s_memrealtime, 100 MHz, one clock for every XCD) of
+// each workgroup of the carrying launch (scripts/microbench.py MB_HF)
+__constant__ long long* g_cp_life = nullptr;
+
 template <bool ONE, int NSLOT>
 __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u, CPTail t) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (g_cp_life && threadIdx.x == 0) g_cp_life[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   cp_bwd_upd_body<ONE, NSLOT>(a, u, t, smem);
+  if (g_cp_life) {
+    __syncthreads();
+    if (threadIdx.x == 0) g_cp_life[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1906,6 +1915,16 @@ using namespace csa;
 
 CSA_API int csa_cp_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cp_dbg), &p, sizeof(p));
+}
+
+// this code object's copy of the dense-update stamps (dense_update.h, [block][8]) for the
+// update workgroups carried by the pair backward (segment-local block numbers)
+CSA_API int csa_cp_du_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_du_dbg), &p, sizeof(p));
+}
+
+CSA_API int csa_cp_life_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cp_life), &p, sizeof(p));
 }
 
 CSA_API int csa_cp_debug_block(int b) {

@@ -359,6 +359,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     if (j == 0 && a.bn_on && dgrad && !tabs)              // no precomputed tables: reduce here
       bn_reduce_to_lds(a.bn, s_bn, s_bn + MAXC_DU, s_bn + 2 * MAXC_DU, s_bn + 3 * MAXC_DU, s_st);
     __syncthreads();
+    if (UPO && j == 1) DU_STAMP(4);                        // (update-only: stamps 4 / 5 are free)
     if (j == 0) {
       DU_STAMP(1);
 #pragma unroll
@@ -366,6 +367,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     }
     pin(wv[j]); pin(s0v[j]); pin(s1v[j]);
     if (j == 0) DU_STAMP(2);
+    if (UPO && j == 1) DU_STAMP(5);
     if (!sok[j]) continue;                                 // wave-uniform
     const int n0 = 16 * (wave + WAVES * j);                // block-local
     // input-gradient partial (OLD weights): 4 batch tiles x 4 k-steps
@@ -406,6 +408,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     wv[j] = make_float4(w[0], w[1], w[2], w[3]);
     s0v[j] = make_float4(s0[0], s0[1], s0[2], s0[3]);
     s1v[j] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    if (UPO && j == 0) DU_STAMP(7);
   }
   pin(bw); pin(bs0); pin(bs1); pin(xf);
   // bias: column sums of dY over the batch, one column per wave (prefetched operands)

@@ -78,6 +78,8 @@ _SIGS = {
     "csa_conv_pair_ok": (I, [P]),
     "csa_cp_debug": (I, [P]),
     "csa_cp_debug_block": (I, [I]),
+    "csa_cp_life_debug": (I, [P]),
+    "csa_cp_du_debug": (I, [P]),
     "csa_conv_pair_bn_tab": (None, [P]),
     "csa_head_debug": (I, [P]),
     "csa_conv_pair_fwd": (I, [P, P, P, P, P, P, I, F, P, P, I, F, P, P, P, I, P, P, I, P]),

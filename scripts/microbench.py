@@ -244,6 +244,52 @@ def main() -> int:
         print(f"HF: pair alone {timed(pair_alone):.2f} us | updates alone {timed(upd_alone):.2f} us | "
               f"pair + updates in one launch {timed(fused):.2f} us")
         cdbg = torch.zeros(24, dtype=torch.int64, device="cuda")
+        # every workgroup's start / end in the carrying launch: who is on the critical path
+        life = torch.zeros(2 * 4096, dtype=torch.int64, device="cuda")
+        for _ in range(3):
+            life.zero_()
+            lib.csa_cp_life_debug(life.data_ptr())
+            fused()
+            torch.cuda.synchronize()
+            lib.csa_cp_life_debug(None)
+        lv = life.view(-1, 2).cpu()
+        nblk = int((lv[:, 0] > 0).sum())
+        lv = lv[:nblk].double()
+        t0 = lv[:, 0].min()
+        st, en = (lv[:, 0] - t0) / 100.0, (lv[:, 1] - t0) / 100.0      # us
+        npair = int(os.environ.get("MB_NPAIR", "700"))
+        segs = [("pair", 0, npair)]
+        # deferred segments follow in record order, then the tail
+        print(f"  life: {nblk} workgroups, launch span {float(en.max()):.2f} us")
+        edges = [int(x) for x in os.environ.get("MB_EDGES", "").split(",") if x] or []
+        bounds = [0, npair] + edges + [nblk]
+        for k in range(len(bounds) - 1):
+            lo, hi = bounds[k], bounds[k + 1]
+            if hi <= lo:
+                continue
+            s_, e_ = st[lo:hi], en[lo:hi]
+            print(f"    blocks [{lo},{hi}): start {float(s_.min()):.2f}..{float(s_.max()):.2f} "
+                  f"end {float(e_.min()):.2f}..{float(e_.max()):.2f} life mean {float((e_ - s_).mean()):.2f} "
+                  f"max {float((e_ - s_).max()):.2f} us")
+        q = torch.quantile(en, torch.tensor([0.5, 0.9, 0.99], dtype=torch.float64))
+        print(f"    block ends p50/p90/p99 {q[0]:.2f}/{q[1]:.2f}/{q[2]:.2f} us")
+        # the carried update workgroups' own stamps (segment-local numbering: carry ONE
+        # segment, MB_HF_ONLY, so that they do not collide)
+        if len(defers) == 1:
+            cdu = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
+            for _ in range(3):
+                cdu.zero_()
+                lib.csa_cp_du_debug(cdu.data_ptr())
+                fused()
+                torch.cuda.synchronize()
+                lib.csa_cp_du_debug(None)
+            t = cdu.view(-1, 8)
+            t = t[t[:, 0] > 0].double()
+            d = lambda k1, k0: ((t[:, k1] - t[:, k0]) / 100)
+            print(f"  carried segment: blocks {len(t)} | stage {d(1, 0).mean():.2f} | W {d(2, 1).mean():.2f} | "
+                  f"half 0 MFMA+update {d(7, 2).mean():.2f} | half 1 dY staged {d(4, 7).mean():.2f} | half 1 W {d(5, 4).mean():.2f} | "
+                  f"half 1 MFMA+update + bias {d(3, 5).mean():.2f} | store issue {d(6, 3).mean():.2f} | "
+                  f"life {d(6, 0).mean():.2f} (mean us)")
         # MB_CP_BLOCKS=0,350,699: whose stamps (pair workgroups come first in both launches)
         for blk in [int(x) for x in os.environ.get("MB_CP_BLOCKS", "0").split(",")]:
             lib.csa_cp_debug_block(blk)
@@ -277,6 +323,9 @@ def main() -> int:
                   f"start spread {(t[:, 0].max() - t0) / 100:.2f} | stage {d(1, 0).mean():.2f}/{d(1, 0).max():.2f} | "
                   f"W {d(2, 1).mean():.2f}/{d(2, 1).max():.2f} | mfma+upd {d(3, 2).mean():.2f}/{d(3, 2).max():.2f} | "
                   f"store issue {d(6, 3).mean():.2f}/{d(6, 3).max():.2f} | block life {d(6, 0).mean():.2f}/{d(6, 0).max():.2f} (mean/max us)")
+            if bool((t[:, 5] > 0).all()):         # update-only bodies: the second column half
+                print(f"    half 0 MFMA+update {d(4, 2).mean():.2f} | half 1 W {d(5, 4).mean():.2f} | "
+                      f"half 1 MFMA+update + bias {d(3, 5).mean():.2f} (mean us)")
     for i, (name, fn, args) in enumerate(rec.calls):
         if name in host_only:
             continue
