@@ -384,15 +384,18 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     }
     if (DGO) continue;
     // weight gradient: A = dY[4s + q][n0 + i] (LDS), two accumulators
+    // every k-step's A operand is read before the first MFMA (one LDS round trip instead of
+    // one per step: an early exit at M would keep the reads behind it).  Steps past the
+    // batch read a clamped row and meet Xw = 0 (the slice is zero-filled), adding nothing.
     du_f32x4 g0 = du_f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
     const float* col = sdy + n0 + i;
+    float av[DU_KS];
+#pragma unroll
+    for (int s = 0; s < DU_KS; ++s) av[s] = col[min(4 * s + q, M - 1) * SN];
 #pragma unroll
     for (int s = 0; s < DU_KS; s += 2) {
-      if (4 * s >= M) break;                               // uniform
-      const float a0 = col[min(4 * s + q, M - 1) * SN];
-      const float a1 = col[min(4 * s + 4 + q, M - 1) * SN];
-      g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, xb[s], g0, 0, 0, 0);
-      g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, xb[s + 1], g1, 0, 0, 0);
+      g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], xb[s], g0, 0, 0, 0);
+      g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s + 1], xb[s + 1], g1, 0, 0, 0);
     }
     // optimizer update of the lane's 4 weights (D lane (i, q) = dW[f0 + i][n0 + 4q + r]);
     // written back late: a store in flight would hold the next barrier (the compiler drains
