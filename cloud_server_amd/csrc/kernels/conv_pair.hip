@@ -1279,10 +1279,11 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
   // LDS weights: [wA | pad to 4 | wB] (wB read as float2 / float4 rows)
   float wv[CPV_UW];
 #pragma unroll
-  for (int u = 0; u < CPV_UW; ++u) {
-    const int e = u * CPV_T + tid;
+  for (int u = 0; u < CPV_UW; ++u) {                     // (batches wholly past the weights:
+    const int e = u * CPV_T + tid;                          //  not issued)
     const float* p = e < nwA ? a.wA + e : (e >= nwA4 && e < nw ? a.wB + (e - nwA4) : a.wA);
-    wv[u] = *p;
+    wv[u] = 0.f;
+    if (u * CPV_T < nw) wv[u] = *p;
   }
   float bv = 0.f;
   if (tid < nb) bv = tid < g.C1 ? (a.bA ? a.bA[tid] : 0.f) : (a.bB ? a.bB[tid - g.C1] : 0.f);
@@ -1296,7 +1297,8 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
     const int c = e % g.C0, rem = e / g.C0, xx = rem % t.TXW, r = rem / t.TXW;
     const int yy = y0 + r, xg = x0 + xx;
     xok[u] = e < nX && yy >= 0 && yy < g.H && xg >= 0 && xg < g.W;
-    xv[u] = src[xok[u] ? ((long)yy * g.W + xg) * g.C0 + c : 0];
+    xv[u] = 0;
+    if (u * CPV_T < nX) xv[u] = src[xok[u] ? ((long)yy * g.W + xg) * g.C0 + c : 0];
   }
 #pragma unroll
   for (int u = 0; u < CPV_UW; ++u) pin(wv[u]);

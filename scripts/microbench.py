@@ -143,7 +143,20 @@ def main() -> int:
     if os.environ.get("MB_CP"):
         dbg = torch.zeros(24, dtype=torch.int64, device="cuda")
         for i, (name, fn, args) in enumerate(rec.calls):
-            if name.startswith("csa_conv_pair_"):
+            if name.startswith("csa_conv_pair_fwd"):
+                for blk in [int(x) for x in os.environ.get("MB_CP_BLOCKS", "0").split(",")]:
+                    eng.program.lib.csa_cp_debug_block(blk)
+                    for _ in range(3):
+                        dbg.zero_()
+                        eng.program.lib.csa_cp_debug(dbg.data_ptr())
+                        fn(*args)
+                        torch.cuda.synchronize()
+                        eng.program.lib.csa_cp_debug(None)
+                    t = dbg.tolist()
+                    print(f"{i:2d} {name} block {blk}: stage {t[1]-t[0]} convA {t[2]-t[1]} convB+pool {t[3]-t[2]} "
+                          f"stats {t[4]-t[3]} (s_memtime ticks)")
+                eng.program.lib.csa_cp_debug_block(0)
+            elif name.startswith("csa_conv_pair_"):
                 for _ in range(3):
                     dbg.zero_()
                     eng.program.lib.csa_cp_debug(dbg.data_ptr())
@@ -152,8 +165,7 @@ def main() -> int:
                     eng.program.lib.csa_cp_debug(None)
                 t = dbg.tolist()
                 if "fwd" in name:
-                    print(f"{i:2d} {name}: stage {t[1]-t[0]} convA {t[2]-t[1]} convB+pool {t[3]-t[2]} "
-                          f"stats {t[4]-t[3]} (s_memtime ticks)")
+                    pass
                 elif t[14] == 0:      # VALU backward (cpv_bwd_kernel)
                     print(f"{i:2d} {name}: loads {t[9]-t[8]} bn+c1 {t[10]-t[9]} route {t[11]-t[10]} "
                           f"dwB+dc1 {t[12]-t[11]} dwA {t[13]-t[12]} (s_memtime ticks)")
