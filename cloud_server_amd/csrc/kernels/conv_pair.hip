@@ -1115,18 +1115,30 @@ __device__ __forceinline__ bool cp_tail_wait(const CPTail& t, int k, unsigned wa
   return s_ok != 0;
 }
 
-// Tail workgroup k < param_blocks: its table entry's 256 elements; each thread's stripe /
-// parameter / slot loads are issued together (one memory round trip).
-__device__ __forceinline__ void cp_tail_params(const CPTail& t, int k) {
-  const CPTailSeg d = t.segs[k];                       // uniform address: scalar loads
+// Tail workgroup k < param_blocks: its table entry's 256 elements.  The entry and the
+// parameter / slot values (which no pair workgroup writes) are loaded BEFORE the wait, so
+// after the last pair workgroup only the stripe loads — one round trip — remain.
+struct CPTailPre { CPTailSeg d; float wv, z0, z1; };
+__device__ __forceinline__ CPTailPre cp_tail_prefetch(const CPTail& t, int k) {
+  CPTailPre p;
+  p.d = t.segs[k];                                     // uniform address: scalar loads
+  const int i = max(min(p.d.base + (int)threadIdx.x, p.d.n - 1), 0);
+  const int nslot = opt_nslots(t.opt);
+  p.wv = p.d.w[i];
+  p.z0 = nslot >= 1 ? p.d.s0[i] : 0.f;
+  p.z1 = nslot >= 2 ? p.d.s1[i] : 0.f;
+  return p;
+}
+
+__device__ __forceinline__ void cp_tail_params(const CPTail& t, int k, CPTailPre& p) {
+  const CPTailSeg& d = p.d;
   const int i = d.base + (int)threadIdx.x;
   if (i < d.n) {
     const int nslot = opt_nslots(t.opt);
     float v[16];
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) v[s2] = d.src[(s2 < d.S ? s2 : 0) * d.ld + i];   // all in flight
-    float wv = d.w[i];
-    float z0 = nslot >= 1 ? d.s0[i] : 0.f, z1 = nslot >= 2 ? d.s1[i] : 0.f;
+    float wv = p.wv, z0 = p.z0, z1 = p.z1;
     float gsum = 0.f;
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) gsum += s2 < d.S ? v[s2] : 0.f;
@@ -1163,7 +1175,8 @@ __device__ __forceinline__ void cp_tail_stage(const CPTail& t, int blk) {
 
 __device__ __forceinline__ void cp_tail_body(const CPTail& t, int npair, int k) {
   if (k < t.param_blocks) {
-    if (cp_tail_wait(t, 0, (unsigned)npair)) cp_tail_params(t, k);
+    CPTailPre p = cp_tail_prefetch(t, k);
+    if (cp_tail_wait(t, 0, (unsigned)npair)) cp_tail_params(t, k, p);
   } else {
     if (cp_tail_wait(t, 1, (unsigned)npair)) cp_tail_stage(t, k - t.param_blocks);
   }
