@@ -220,11 +220,15 @@ def main() -> int:
         lib = eng.program.lib
         pb = [(fn, args) for name, fn, args in rec.calls if name == "csa_conv_pair_bwd"][0]
         tabs = [(fn, args) for name, fn, args in rec.calls if name == "csa_conv_pair_bn_tab"]
-        if tabs:                              # the BN-table pointer is consumed by each launch
+        # MB_TAIL=1: the pair-backward tail too (its plan is consumed by each launch)
+        tails = [(fn, args) for name, fn, args in rec.calls if name == "csa_conv_pair_tail_set"]
+        tails = tails if os.environ.get("MB_TAIL") == "1" else []
+        if tabs or tails:                     # the BN-table pointer is consumed by each launch
             pb0 = pb
 
             def _pb(*args):
-                tabs[-1][0](*tabs[-1][1])
+                for tfn, targs in tails[-1:] + tabs[-1:]:
+                    tfn(*targs)
                 pb0[0](*args)
             pb = (_pb, pb0[1])
 
