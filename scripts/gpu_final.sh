@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 5 closing run: the whole-repo GPU check, then a kernel trace of the step.
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+bash scripts/gpu_check.sh || exit $?
+rm -rf gpurun_out/final_tr
+(cd /tmp && timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/final_tr -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1100 --warmup 100 > /dev/null 2>&1) || exit 6
+python3 scripts/step_timeline.py $(find gpurun_out/final_tr -name "*kernel_trace.csv" | head -1) --skip 1000 --steps 3 > gpurun_out/final_timeline.txt
+cat gpurun_out/final_timeline.txt
