@@ -1088,7 +1088,7 @@ struct CPTail {
   int B, words; uint32_t* out_img; int64_t* out_lbl;
 };
 
-__device__ __forceinline__ bool cp_tail_wait(const CPTail& t, int k, unsigned want) {
+__device__ __forceinline__ bool cp_tail_wait(const CPTail& t, int k, unsigned want, bool acquire = true) {
   __shared__ int s_ok;
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
@@ -1108,7 +1108,7 @@ __device__ __forceinline__ bool cp_tail_wait(const CPTail& t, int k, unsigned wa
       }
       __builtin_amdgcn_s_sleep(8);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     s_ok = ok;
   }
   __syncthreads();
@@ -1178,13 +1178,20 @@ __device__ __forceinline__ void cp_tail_body(const CPTail& t, int npair, int k) 
     CPTailPre p = cp_tail_prefetch(t, k);
     if (cp_tail_wait(t, 0, (unsigned)npair)) cp_tail_params(t, k, p);
   } else {
-    if (cp_tail_wait(t, 1, (unsigned)npair)) cp_tail_stage(t, k - t.param_blocks);
+    // (the staging copy reads nothing the pairs write — it only must not overwrite an
+    // image before every pair has it in LDS — so no acquire: that would invalidate this
+    // XCD's L2 under the update workgroups)
+    if (cp_tail_wait(t, 1, (unsigned)npair, false)) cp_tail_stage(t, k - t.param_blocks);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned ntail = (unsigned)(t.param_blocks + t.stage_blocks);
     unsigned* fin = t.tk + 2 * CPT_SPREAD * CPT_LINE;
-    const unsigned prev = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed: this workgroup's ticket polls have returned (its exit depended on them)
+    // before the add issues, and the reset stores depend on its result.  An acq_rel add
+    // would write back this XCD's L2 (the update workgroups' dirty W / slot lines) on the
+    // launch's critical path; the launch's end publishes the parameters anyway.
+    const unsigned prev = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == ntail - 1) {                      // every tail read the tickets: reset them
       for (int j = 0; j < 2 * CPT_SPREAD; ++j)
         __hip_atomic_store(t.tk + j * CPT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
