@@ -87,12 +87,13 @@ namespace csa {
 
 
 // diagnostics: s_memrealtime stamps (100 MHz, one clock for all XCDs) of EVERY block,
-// [block][8] = start, dY staged, W landed, MFMA + update done, fold done, dX stored, end
+// [block][16] = start, dY staged, W landed, MFMA + update done, fold done, dX stored, end
+// (update-only bodies: 4 / 5 / 7 / 8 stamp the column halves)
 // (scripts/microbench.py MB_DU)
 static __constant__ long long* g_du_dbg = nullptr;   // (per code object)
 #define DU_STAMP(i)                                                                          \
   do {                                                                                       \
-    if (g_du_dbg && threadIdx.x == 0) g_du_dbg[bid * 8 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    if (g_du_dbg && threadIdx.x == 0) g_du_dbg[bid * 16 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 __host__ __device__ constexpr int du_nb(int waves) { return 32 * waves; }      // columns per block
@@ -412,6 +413,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     s0v[j] = make_float4(s0[0], s0[1], s0[2], s0[3]);
     s1v[j] = make_float4(s1[0], s1[1], s1[2], s1[3]);
     if (UPO && j == 0) DU_STAMP(7);
+    if (UPO && j == 1) DU_STAMP(8);
   }
   pin(bw); pin(bs0); pin(bs1); pin(xf);
   // bias: column sums of dY over the batch, one column per wave (prefetched operands)

@@ -93,14 +93,14 @@ def main() -> int:
         for i, (name, fn, args) in enumerate(rec.calls):
             if name.startswith("csa_dense_bwd_update"):
                 grid = 4096
-                dbg = torch.zeros(grid * 8, dtype=torch.int64, device="cuda")
+                dbg = torch.zeros(grid * 16, dtype=torch.int64, device="cuda")
                 for _ in range(3):
                     dbg.zero_()
                     eng.program.lib.csa_du_debug(dbg.data_ptr())
                     fn(*args)
                     torch.cuda.synchronize()
                     eng.program.lib.csa_du_debug(None)
-                t = dbg.view(-1, 8)
+                t = dbg.view(-1, 16)
                 t = t[t[:, 0] > 0].double()
                 t0 = t[:, 0].min()
                 names = ["stage", "W landed", "mfma+update", "fold", "epilogue", "slab atomics"]
@@ -292,19 +292,19 @@ def main() -> int:
         # the carried update workgroups' own stamps (segment-local numbering: carry ONE
         # segment, MB_HF_ONLY, so that they do not collide)
         if len(defers) == 1:
-            cdu = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
+            cdu = torch.zeros(4096 * 16, dtype=torch.int64, device="cuda")
             for _ in range(3):
                 cdu.zero_()
                 lib.csa_cp_du_debug(cdu.data_ptr())
                 fused()
                 torch.cuda.synchronize()
                 lib.csa_cp_du_debug(None)
-            t = cdu.view(-1, 8)
+            t = cdu.view(-1, 16)
             t = t[t[:, 0] > 0].double()
             d = lambda k1, k0: ((t[:, k1] - t[:, k0]) / 100)
             print(f"  carried segment: blocks {len(t)} | stage {d(1, 0).mean():.2f} | W {d(2, 1).mean():.2f} | "
                   f"half 0 MFMA+update {d(7, 2).mean():.2f} | half 1 dY staged {d(4, 7).mean():.2f} | half 1 W {d(5, 4).mean():.2f} | "
-                  f"half 1 MFMA+update + bias {d(3, 5).mean():.2f} | store issue {d(6, 3).mean():.2f} | "
+                  f"half 1 MFMA+update {d(8, 5).mean():.2f} | bias {d(3, 8).mean():.2f} | store issue {d(6, 3).mean():.2f} | "
                   f"life {d(6, 0).mean():.2f} (mean us)")
         # MB_CP_BLOCKS=0,350,699: whose stamps (pair workgroups come first in both launches)
         for blk in [int(x) for x in os.environ.get("MB_CP_BLOCKS", "0").split(",")]:
@@ -323,7 +323,7 @@ def main() -> int:
         lib.csa_cp_debug_block(0)
         # per-block stamps of the update-only launches (100 MHz realtime: start, dY staged,
         # W landed, MFMA + update done, stores issued)
-        dbg = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
+        dbg = torch.zeros(4096 * 16, dtype=torch.int64, device="cuda")
         for dfn, dargs in defers:
             dbg.zero_()
             lib.csa_du_debug(dbg.data_ptr())
@@ -331,7 +331,7 @@ def main() -> int:
             lib.csa_dense_update_flush(None)
             torch.cuda.synchronize()
             lib.csa_du_debug(None)
-            t = dbg.view(-1, 8)
+            t = dbg.view(-1, 16)
             t = t[t[:, 0] > 0].double()
             t0 = t[:, 0].min()
             d = lambda k1, k0: ((t[:, k1] - t[:, k0]) / 100)
