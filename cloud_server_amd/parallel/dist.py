@@ -47,7 +47,16 @@ def rccl_env_defaults() -> None:
       so the first collective of the dedicated capture group
       (``GradSync._setup_capture_group``) may be one inside a capture;
     * ``TORCH_NCCL_TRACE_BUFFER_SIZE`` — the flight recorder, whose active list tells when
-      the watchdog has retired that group's one eager collective (``utils.graphs.wait_retired``)."""
+      the watchdog has retired that group's one eager collective (``utils.graphs.wait_retired``);
+    * ``TORCH_NCCL_BLOCKING_WAIT=1`` — no watchdog thread at all.  The separate capture
+      group, the streams outside torch's pool and the retirement wait made the watchdog's
+      hipErrorCapturedEvent abort rare, but it still hit one world-1 ``allreduce`` run in the
+      round-5 closing check (``profiles/r5_notes.md``).  Without the thread nothing queries an
+      event of a capturing stream.  Eager collectives (set-up, agreement flags, log points)
+      then block the host until they finish, and a hung one raises after the group timeout
+      instead of being aborted by the watchdog.  Measured: the DP GPU tests and 3 x 4 world-1
+      DP benches at unchanged ms/step (``scripts/gpu_r5bw.sh``)."""
+    os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
     os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")
