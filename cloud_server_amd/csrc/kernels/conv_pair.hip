@@ -2208,6 +2208,8 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
                               float* doffset, float* run_mean, float* run_var, float momentum, float* dwA, float* dbA,
                               float* dwB, float* dbB, int stripes, const int* tabs, hipStream_t st) {
   CPBwdArgs a{};
+  const float* bn_tab = g_cp_bn_tab;                 // consumed by this call, whatever it returns
+  g_cp_bn_tab = nullptr;
   if (!cp_geom(geom, a.g) || cp_lds(a.g, true) > CP_LDS_MAX) return -1;
   a.tabs = tabs;
   a.tab_stride = tabs ? cp_bwd_tab_stride(a.g) : 0;
@@ -2216,8 +2218,7 @@ CSA_API int csa_conv_pair_bwd(const int* geom, const uint8_t* img, const int64_t
   a.wB = wB; a.actB = actB; a.alphaB = alphaB; a.hasBiasB = hasBiasB; a.dz = dz; a.y = y; a.argmax = argmax;
   a.bn = BNRef{bn_slab, bn_nslab, a.g.C2, bn_count, bn_eps, bn_scale, bn_offset};
   a.bn_on = bn_slab != nullptr; a.bwd_slab = bwd_slab; a.bwd_nslab = bwd_nslab;
-  a.bn_tab = a.bn_on ? g_cp_bn_tab : nullptr;
-  g_cp_bn_tab = nullptr;
+  a.bn_tab = a.bn_on ? bn_tab : nullptr;
   a.dscale = dscale; a.doffset = doffset; a.run_mean = run_mean; a.run_var = run_var; a.momentum = momentum;
   a.dwA = dwA; a.dbA = dbA; a.dwB = dwB; a.dbB = dbB; a.stripes = stripes < 1 ? 1 : stripes;
   static bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_kernel<true>,
