@@ -12,7 +12,8 @@ MNIST-shaped dataset resident in HBM; gradients are all-reduced over RCCL/xGMI e
 step (synchronous DP), so ``value`` is the whole-job samples/s.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
-        (N>1: torchrun --nproc-per-node N ... bench.py --gpus N)
+        (N>1: bench.py starts ``torch.distributed.run --nproc-per-node N`` on itself as a
+        child process; under an outer torchrun WORLD_SIZE must equal N)
 
 Multi-tenant (one GPU, K independent sample-config jobs; value = aggregate samples/s):
         python bench.py --jobs K --pack graph   # one process, one graph with K branches
@@ -138,6 +139,48 @@ def bench_packed(args) -> int:
     return 0
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(args):
+    """``--gpus N`` means N ranks however bench.py is started.
+
+    * under ``torch.distributed.run`` (``WORLD_SIZE`` set): it must equal ``--gpus``, else
+      the run would be mislabelled — exit non-zero;
+    * plain ``python bench.py --gpus N`` with N > 1: start ``torch.distributed.run
+      --nproc-per-node N`` on this same script as a CHILD process (127.0.0.1 rendezvous on
+      a free port) and exit with its return code; the child's rank 0 prints the one JSON
+      line on the inherited stdout.  This process has made no GPU call at that point (torch
+      is not even imported), so nothing initialised here outlives the hand-off;
+    * ``--gpus 1`` without ``WORLD_SIZE``: ``None`` — the single-process path, unchanged.
+
+    Reference: the cluster is the host lists the launcher writes into the worker's flags
+    (construct_distribute.py:37-40, :344-346; cmd.py:54-70)."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={world_env} but --gpus {args.gpus}; launch "
+                  f"--nproc-per-node {args.gpus} or pass --gpus {world_env}", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if args.gpus == 1:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, cwd=os.path.dirname(os.path.abspath(__file__))).returncode
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +199,9 @@ def main() -> int:
     args = ap.parse_args()
     if args.jobs > 1:
         return bench_packed(args)
+    rc = _launch_ranks(args)
+    if rc is not None:
+        return rc
 
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

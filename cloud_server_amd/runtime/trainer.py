@@ -103,6 +103,25 @@ def _fault_step(rank: int, model_dir: str) -> int:
     return int(v)
 
 
+def _strip_final_tail(path: str) -> None:
+    """A resumed (extended) job appends its step lines after the previous run's; drop that
+    run's ``final_accuracy`` tail first, so the file stays one run of step lines and then
+    one final line — the reference monitor reads only up to the first non-step line
+    (apps/runtime/views.py:55)."""
+    if not os.path.exists(path):
+        return
+    with open(path) as f:
+        lines = f.readlines()
+    keep = 0
+    while keep < len(lines) and lines[keep].startswith("step"):
+        keep += 1
+    if keep < len(lines):
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.writelines(lines[:keep])
+        os.replace(tmp, path)
+
+
 class _MetricLog:
     """Training-log lines without stalling the device queue.
 
@@ -122,6 +141,8 @@ class _MetricLog:
         self.t_host = time.perf_counter()
         self.h_step = eng.host_step
         self.last_acc = float("nan")
+        if chief:
+            _strip_final_tail(result_path)
         self.fr = open(result_path, "a") if chief else None
         self.fm = open(metrics_path, "a") if chief else None
         self.lines = 0
@@ -402,28 +423,33 @@ def _agree(ctx: DistContext, action: str) -> str:
 
 
 def read_train_results(path: str, iters: int) -> Dict[str, Any]:
-    """Reference monitor parse (apps/runtime/views.py:44-72): ``every_result`` rows with
-    string values; ``final_accuracy`` from the final line, or — once more than iter/100
-    rows exist without one — the mean of the logged accuracies."""
+    """Reference monitor parse (apps/runtime/views.py:44-72).
+
+    * ``every_result``: the leading run of ``step...`` lines, string values; the parse stops
+      at the first line that is not a step line, as the reference's ``while`` does (:55);
+    * ``final_accuracy`` is attached only when more than ``iter/100`` step rows exist (:66),
+      and then it is the STRING after ``:`` on the line that ended the run (:70), or — if
+      the file ended there — the float mean of the logged batch accuracies (:67-68).
+    A stopper line without ``:`` (which would raise in the reference) falls back to the
+    mean."""
     out: Dict[str, Any] = {"every_result": []}
     if not os.path.exists(path):
         return out
-    final = None
+    accs = []
+    stopper = ""
     with open(path) as f:
         for line in f:
-            line = line.strip()
-            if not line:
-                continue
-            if line.startswith("final_accuracy:"):
-                final = float(line.split(":", 1)[1])
-                continue
+            if not line.startswith("step"):
+                stopper = line
+                break
             parts = dict(p.split(":", 1) for p in line.split(",") if ":" in p)
-            if {"step", "accuracy", "duration"} <= parts.keys():
-                out["every_result"].append({"step": parts["step"], "accuracy": parts["accuracy"],
-                                            "duration": parts["duration"]})
-    rows = out["every_result"]
-    if final is not None:
-        out["final_accuracy"] = final
-    elif rows and len(rows) > max(int(iters), 0) // 100:
-        out["final_accuracy"] = float(np.mean([float(r["accuracy"]) for r in rows]))
+            row = {"step": parts.get("step", ""), "accuracy": parts.get("accuracy", "").strip(),
+                   "duration": parts.get("duration", "").strip()}
+            out["every_result"].append(row)
+            accs.append(float(row["accuracy"]))
+    if len(accs) > int(iters) / 100:
+        if len(stopper) < 1 or ":" not in stopper:
+            out["final_accuracy"] = float(sum(accs)) / len(accs)
+        else:
+            out["final_accuracy"] = stopper.split(":")[1].strip()
     return out

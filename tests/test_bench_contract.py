@@ -100,3 +100,29 @@ def test_run_steps_warm_replay_and_remainder_graphs(monkeypatch):
     _FakeGraph.log = []
     eng.run_steps(6)
     assert _FakeGraph.log == [4, 2]
+
+
+def test_bench_gpus2_without_torchrun_launches_two_ranks():
+    """``python bench.py --gpus 2`` (no outer torchrun) runs two ranks —
+    bench.py starts torch.distributed.run as a child and relays rank 0's JSON line."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--strategy", "allreduce"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 100
+    assert d["config"]["parallelism"].startswith("dp2")
+
+
+def test_bench_world_size_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1",
+           "--warmup", "0"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0
+    assert "WORLD_SIZE=2" in out.stderr and not out.stdout.strip()

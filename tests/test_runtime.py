@@ -116,7 +116,8 @@ def test_run_job_result_contract_and_resume(tmp_path):
     assert [l.split(",")[0] for l in lines[:3]] == ["step:0", "step:10", "step:20"]
     assert lines[3].startswith("final_accuracy:") and lines[4] == ""
     res = read_train_results(os.path.join(mdir, RESULT), 30)
-    assert len(res["every_result"]) == 3 and res["final_accuracy"] == pytest.approx(out["final_accuracy"], abs=1e-6)
+    assert len(res["every_result"]) == 3 and isinstance(res["final_accuracy"], str)   # views.py:70
+    assert float(res["final_accuracy"]) == pytest.approx(out["final_accuracy"], abs=1e-6)
     last = ckpt.latest(mdir)
     assert last[0] == 30
     obj = torch.load(last[1], weights_only=True)                 # safe loader works
@@ -186,6 +187,22 @@ def test_monitor_mean_fallback(tmp_path):
     r = read_train_results(str(p), 1000)
     assert "final_accuracy" not in r
     assert read_train_results(str(tmp_path / "none.txt"), 10) == {"every_result": []}
+
+
+def test_monitor_final_line_gated_and_string(tmp_path):
+    """views.py:55-70: the final line's value is returned as a string, and only when more
+    than iter/100 rows were logged; the parse stops at the first non-step line."""
+    p = tmp_path / "result.txt"
+    body = "".join(f"step:{s},accuracy:{a},duration:0.1\n" for s, a in [(0, 0.1), (100, 0.3)])
+    p.write_text(body + "final_accuracy:0.912000\n\n")
+    r = read_train_results(str(p), 100)                    # 2 > 1: gated in
+    assert r["final_accuracy"] == "0.912000"
+    r = read_train_results(str(p), 200)                    # 2 > 2 is false: gated out
+    assert "final_accuracy" not in r and len(r["every_result"]) == 2
+    # a step line after a non-step line is not read (the reference's while loop stops)
+    p.write_text(body + "final_accuracy:0.5\nstep:300,accuracy:0.9,duration:0.1\n")
+    r = read_train_results(str(p), 0)
+    assert [x["step"] for x in r["every_result"]] == ["0", "100"] and r["final_accuracy"] == "0.5"
 
 
 # ---------------------------------------------------------------- job manager
