@@ -242,8 +242,9 @@ def main() -> int:
     eng.sync_device()
     dt = time.perf_counter() - t0
     dt = all_reduce_max(ctx, dt)
-    if eng.sync is not None:
-        eng.sync.check()   # a timed-out xGMI peer wait invalidates the run: fail loudly
+    # a timed-out xGMI peer wait or in-kernel tail wait (skipped updates) invalidates the
+    # run: fail loudly (agreed by every rank under data parallelism)
+    eng.check_health()
     m = eng.metrics_since(eng.host_step - min(args.steps, 100))
 
     total = args.batch * ctx.world * args.steps / dt

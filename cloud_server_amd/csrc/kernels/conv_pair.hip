@@ -1080,6 +1080,9 @@ struct CPTail {
   unsigned* tk;                     // [CPT_TK_WORDS]: pair workgroups done | image tiles
                                     // consumed (CPT_SPREAD words each) | tails done
   int* err;                         // [1]: a tail wait timed out (nothing of that tail ran)
+  int* force;                       // [1] or null: debug — while nonzero every tail's wait
+                                    // asks for one ticket more than exists (forced timeout);
+                                    // the closing tail clears it (one-shot, host-armed)
   int opt; float lr; const int64_t* step;
   const CPTailSeg* segs;            // [param_blocks]
   int nz; float* zp[CP_MAXZ]; int zn[CP_MAXZ];
@@ -1174,14 +1177,17 @@ __device__ __forceinline__ void cp_tail_stage(const CPTail& t, int blk) {
 }
 
 __device__ __forceinline__ void cp_tail_body(const CPTail& t, int npair, int k) {
+  // (debug) a host-armed forced timeout: the wait asks for a ticket no workgroup adds
+  const unsigned want = (unsigned)npair +
+      ((t.force && __hip_atomic_load(t.force, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 1u : 0u);
   if (k < t.param_blocks) {
     CPTailPre p = cp_tail_prefetch(t, k);
-    if (cp_tail_wait(t, 0, (unsigned)npair)) cp_tail_params(t, k, p);
+    if (cp_tail_wait(t, 0, want)) cp_tail_params(t, k, p);
   } else {
     // (the staging copy reads nothing the pairs write — it only must not overwrite an
     // image before every pair has it in LDS — so no acquire: that would invalidate this
     // XCD's L2 under the update workgroups)
-    if (cp_tail_wait(t, 1, (unsigned)npair, false)) cp_tail_stage(t, k - t.param_blocks);
+    if (cp_tail_wait(t, 1, want, false)) cp_tail_stage(t, k - t.param_blocks);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1196,6 +1202,7 @@ __device__ __forceinline__ void cp_tail_body(const CPTail& t, int npair, int k) 
       for (int j = 0; j < 2 * CPT_SPREAD; ++j)
         __hip_atomic_store(t.tk + j * CPT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t.force) __hip_atomic_store(t.force, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1210,6 +1217,27 @@ __device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs
       // the barrier drains every wave's stripe atomics (device-scope: visible once done);
       // block 0's plain stores (BN parameter gradients, running statistics) get ONE
       // release — not 700 L2 write-backs
+      //
+      // Why the ticket add below may be RELAXED (memory-ordering argument):
+      //  * what the tail reads from the pairs are the weight-gradient stripes, written
+      //    ONLY by device-scope atomic adds (agent scope: performed at the L2 that owns the
+      //    line, never cached dirty in this CU's L1 / another XCD's L2 — there is no copy
+      //    to publish);
+      //  * __syncthreads() compiles to s_waitcnt vmcnt(0) + s_barrier: every wave of this
+      //    workgroup has had its atomics RETURN (performed, globally visible at agent scope)
+      //    before thread 0 passes the barrier, so the ticket add is issued strictly after
+      //    them; a relaxed atomic cannot be hoisted above the barrier;
+      //  * the tail's poll sees the ticket count reach `want` only after every pair's add
+      //    issued, hence after all of that pair's stripe atomics were performed; its single
+      //    agent-scope ACQUIRE after the poll invalidates its own L1 / non-coherent lines
+      //    so its stripe loads read the L2 value;
+      //  * block 0's plain (non-atomic) stores — BN parameter gradients, running
+      //    statistics — are the only non-atomic data the tail reads, hence block 0's one
+      //    agent-scope RELEASE before its ticket add (write-back of its dirty lines).
+      // The staging tails read nothing any pair writes (they wait only so an image is not
+      // overwritten before every pair loaded it into LDS), so they skip the acquire.
+      // Pinned by tests/test_gpu_dp_overlap.py (tail error word stays 0 over many steps,
+      // results equal the deterministic program's) and test_hip_step's per-step gradients.
       __syncthreads();
       if (threadIdx.x == 0) {
         if (bid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -2120,13 +2148,17 @@ CSA_API int csa_conv_pair_tail_plan(void* table, int opt, int nseg, float* const
 // segments: the MFMA carrier): `param_blocks` workgroups over the planned table, nz <= 4
 // float regions zeroed, the next batch staged when out_img != null (imsz % 4 == 0).
 // tk: 3 zeroed uints, err: 1 int (device).
+// (debug) the forced-timeout word of the tail set NEXT by this thread (null: none)
+static thread_local int* g_cp_tail_force = nullptr;
+CSA_API void csa_conv_pair_tail_force(int* force) { g_cp_tail_force = force; }
+
 CSA_API int csa_conv_pair_tail_set(unsigned* tk, int* err, int opt, float lr, const int64_t* step,
                                    const void* table, int param_blocks, int nz, float* const* zp, const long* zn,
                                    const uint8_t* img, const int64_t* labels, const int64_t* rows,
                                    const int64_t* cursor, int B, long imsz, uint8_t* out_img, int64_t* out_lbl) {
   if (!tk || !err || !step || !table || param_blocks < 1 || nz < 0 || nz > CP_MAXZ) return -1;
   CPTail t{};
-  t.on = 1; t.tk = tk; t.err = err; t.opt = opt; t.lr = lr; t.step = step;
+  t.on = 1; t.tk = tk; t.err = err; t.force = g_cp_tail_force; t.opt = opt; t.lr = lr; t.step = step;
   t.segs = static_cast<const CPTailSeg*>(table); t.param_blocks = param_blocks;
   t.nz = nz;
   for (int k = 0; k < nz; ++k) { t.zp[k] = zp[k]; t.zn[k] = (int)zn[k]; }

@@ -91,6 +91,7 @@ _SIGS = {
     "csa_conv_pair_tail_plan": (I, [P, I, I, P, P, P, P, P, P, P, P, I]),
     "csa_dense_update_grad_mode": (I, [P, P]),
     "csa_conv_pair_tail_set": (I, [P, P, I, F, P, P, I, I, P, P, P, P, P, P, I, L, P, P]),
+    "csa_conv_pair_tail_force": (None, [P]),
     "csa_conv_pair_tail_pending": (I, []),
     "csa_conv_pair_tail_ticket_words": (I, []),
     "csa_dense_update_head_params": (I, [P, P, P, P, P, P]),

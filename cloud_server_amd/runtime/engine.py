@@ -154,6 +154,10 @@ class TrainEngine:
                 enable_deterministic_torch()
                 self.model.deterministic = True
             self.program = TorchProgram(self)
+        # an in-kernel bounded wait that timed out (the pair backward's tail) is part of the
+        # ranks' agreed health check under data parallelism, like a poisoned xGMI channel
+        if hasattr(self.program, "health_words"):
+            self.sync.extra_errors.append(lambda: any(int(w.item()) for w in self.program.health_words()))
         # the program re-stages its batch whenever the host moves the cursor (seek/resume)
         self.stream.on_reset = (lambda: self.program.prime()) if hasattr(self.program, "prime") else None
         if use_graph is None:
@@ -404,6 +408,25 @@ class TrainEngine:
             self.sync_device()
             # a timeout anywhere raises on EVERY rank together (never one rank alone)
             self.sync.check_agreed()
+
+    def health_words(self) -> List[torch.Tensor]:
+        """Device words that turn nonzero when an in-kernel bounded wait timed out (the
+        program's tail); copied without a host sync by the job loop's metric drain."""
+        f = getattr(self.program, "health_words", None)
+        return list(f()) if f is not None else []
+
+    def check_health(self) -> None:
+        """Raise if any in-kernel bounded wait or peer transport timed out: the state is then
+        not a valid training state (skipped updates / un-reduced gradients).  Under data
+        parallelism the verdict is agreed by every rank (``GradSync.check_agreed``, which
+        also reads the program's words); on one rank the words are read here.  A host sync."""
+        if self.ctx.enabled:
+            self.sync.check_agreed()
+            return
+        self.sync.check()
+        if any(int(w.item()) for w in self.health_words()):
+            raise RuntimeError("in-kernel wait timed out (pair-backward tail): conv / BatchNorm "
+                               "updates, statistic zeroing or batch staging were skipped")
 
     def close(self) -> None:
         """Release the peer-buffer transports (collective under data parallelism: every rank

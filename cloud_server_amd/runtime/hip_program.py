@@ -669,6 +669,7 @@ class HipProgram:
         self.tail_tk = torch.zeros(int(self.lib.csa_conv_pair_tail_ticket_words()), dtype=torch.int32,
                                    device=e.device)                           # spread tickets
         self.tail_err = torch.zeros(1, dtype=torch.int32, device=e.device)
+        self.tail_force = torch.zeros(1, dtype=torch.int32, device=e.device)   # debug: arm_tail_timeout
         # the parameter workgroups' table (one entry per 256 elements of a parameter)
         tp = self.tail_params
         n = len(tp)
@@ -704,6 +705,7 @@ class HipProgram:
         self.tail_tk = torch.zeros(int(self.lib.csa_conv_pair_tail_ticket_words()), dtype=torch.int32,
                                    device=e.device)
         self.tail_err = torch.zeros(1, dtype=torch.int32, device=e.device)
+        self.tail_force = torch.zeros(1, dtype=torch.int32, device=e.device)   # debug: arm_tail_timeout
         P = C.c_void_p
         n = len(jobs)
         ns = (C.c_int * 8)(*[j[0].numel() for j in jobs])
@@ -724,6 +726,7 @@ class HipProgram:
         deferred dense segments) and switch the head segment to in-place updates."""
         e, lib = self.e, self.lib
         P = C.c_void_p
+        lib.csa_conv_pair_tail_force(K.ptr(self.tail_force))
         if not self.tail_update:           # the ":hf" data-parallel fold: nothing else
             self._rc(lib.csa_conv_pair_tail_set(
                 K.ptr(self.tail_tk), K.ptr(self.tail_err), 0, 0.0, K.ptr(e.dstep), K.ptr(self.tail_table),
@@ -743,8 +746,28 @@ class HipProgram:
         self._rc(rc, "conv_pair_tail_set")
 
     def tail_error(self) -> int:
-        """Nonzero when a tail workgroup's bounded wait timed out (its work did not run)."""
+        """Nonzero when a tail workgroup's bounded wait timed out (its work did not run).
+
+        STICKY by design: a timed-out tail skipped parameter updates, the statistic-slab
+        zeroing and the next batch's staging, so the engine's state is no longer a valid
+        training state — nothing resets the word; the job fails (``TrainEngine.check_health``)
+        and restarts from its last checkpoint in a fresh engine."""
         return int(self.tail_err.item()) if getattr(self, "tail", False) else 0
+
+    def health_words(self):
+        """Device int32 words that are nonzero once an in-kernel bounded wait timed out
+        (read without a host sync by the job loop's metric drain)."""
+        return [self.tail_err] if getattr(self, "tail", False) else []
+
+    def arm_tail_timeout(self) -> bool:
+        """Debug / fault injection: the NEXT pair-backward launch's tail waits
+        for one ticket more than exists, times out after its 1 s bound and sets the error
+        word, as a starved or hung pair workgroup would.  Stream-ordered (a fill before the
+        launch); the launch's closing tail disarms it.  False when this program has no tail."""
+        if not getattr(self, "tail", False):
+            return False
+        self.tail_force.fill_(1)
+        return True
 
     # ------------------------------------------------------------------ deterministic mode
     def _check_det(self) -> None:

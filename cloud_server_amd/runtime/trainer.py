@@ -103,6 +103,21 @@ def _fault_step(rank: int, model_dir: str) -> int:
     return int(v)
 
 
+def _tail_timeout_step(model_dir: str) -> int:
+    """``CSA_TAIL_TIMEOUT_AT_STEP=s``: arm the HIP program's forced tail timeout
+    (``HipProgram.arm_tail_timeout``) before step ``s`` — the in-kernel failure a starved
+    pair workgroup would cause.  Fires once per model dir (a marker file), so the
+    automatic restart from the last checkpoint can be watched to succeed."""
+    v = os.environ.get("CSA_TAIL_TIMEOUT_AT_STEP", "").strip()
+    if not v:
+        return -1
+    marker = os.path.join(model_dir, ".tail_timeout_fired")
+    if os.path.exists(marker):
+        return -1
+    open(marker, "w").close()
+    return int(v)
+
+
 def _strip_final_tail(path: str) -> None:
     """A resumed (extended) job appends its step lines after the previous run's; drop that
     run's ``final_accuracy`` tail first, so the file stays one run of step lines and then
@@ -146,6 +161,10 @@ class _MetricLog:
         self.fr = open(result_path, "a") if chief else None
         self.fm = open(metrics_path, "a") if chief else None
         self.lines = 0
+        # one rank: the in-kernel timeout words ride with the metric copies (no host sync)
+        # and a nonzero one fails the job when its log line drains; under data parallelism
+        # the ranks' agreed check at control points reads them instead
+        self.health = eng.health_words() if world == 1 else []
 
     def mark(self, step: int, int_start: int) -> None:
         e = self.eng
@@ -154,25 +173,33 @@ class _MetricLog:
             pl = torch.empty(e.ring_loss.shape, dtype=e.ring_loss.dtype, pin_memory=True)
             pc.copy_(e.ring_correct, non_blocking=True)
             pl.copy_(e.ring_loss, non_blocking=True)
+            ph = None
+            if self.health:
+                ph = torch.empty(len(self.health), dtype=torch.int32, pin_memory=True)
+                for i, w in enumerate(self.health):
+                    ph[i:i + 1].copy_(w, non_blocking=True)
             ev = torch.cuda.Event(enable_timing=True)
             ev.record(torch.cuda.current_stream(e.device))
-            self.pending.append((step, int_start, e.host_step, ev, pc, pl, time.perf_counter()))
+            self.pending.append((step, int_start, e.host_step, ev, pc, pl, time.perf_counter(), ph))
             self.drain(block=False)
         else:
             self.pending.append((step, int_start, e.host_step, None, e.ring_correct, e.ring_loss,
-                                 time.perf_counter()))
+                                 time.perf_counter(), None))
             self.drain(block=True)
 
     def drain(self, block: bool) -> None:
         from .engine import RING
         B = self.eng.cfg.batch_size
         while self.pending:
-            step, s0, s1, ev, pc, pl, th = self.pending[0]
+            step, s0, s1, ev, pc, pl, th, ph = self.pending[0]
             if ev is not None and not block and not ev.query():
                 return
             self.pending.popleft()
             if ev is not None:
                 ev.synchronize()
+            if ph is not None and bool(ph.any()):
+                raise RuntimeError(f"in-kernel wait timed out by step {s1} (pair-backward tail): "
+                                   "parameter updates / statistic zeroing / batch staging skipped")
             n = max(s1 - self.h_step, 1)
             if ev is not None and self.prev_ev is not None:
                 step_time = self.prev_ev.elapsed_time(ev) / 1e3 / n
@@ -238,6 +265,7 @@ class JobRun:
             if last is not None:
                 ckpt.restore_engine(eng, ckpt.load(last[1]))
             self.fault_at = _fault_step(ctx.rank, model_dir)                       # raise (crash) at this step
+            self.tail_timeout_at = _tail_timeout_step(model_dir)                   # forced in-kernel timeout
             self.hang_at = int(os.environ.get("CSA_HANG_AT_STEP", "-1"))   # stop making progress (watchdog tests)
             self.log_every = max(1, cfg.log_every)
             # control / time-checkpoint decisions: every log point on one rank (a file stat); under
@@ -267,6 +295,10 @@ class JobRun:
         if step == self.hang_at:
             while True:
                 time.sleep(1.0)
+        if step == self.tail_timeout_at:
+            arm = getattr(self.eng.program, "arm_tail_timeout", None)
+            if arm is None or not arm():
+                raise RuntimeError("CSA_TAIL_TIMEOUT_AT_STEP: this program has no pair-backward tail")
 
     def step(self) -> None:
         eng, ctx = self.eng, self.ctx
@@ -296,7 +328,8 @@ class JobRun:
                 return False
         return (step + k <= self.cfg.iter
                 and all((s % self.log_every) != 0 for s in range(step, step + k - 1))
-                and not (step <= self.fault_at < step + k) and not (step <= self.hang_at < step + k))
+                and not (step <= self.fault_at < step + k) and not (step <= self.hang_at < step + k)
+                and not (step <= self.tail_timeout_at < step + k))
 
     def after_step(self) -> str:
         """Bookkeeping after step ``host_step - 1`` ran; returns "" to continue, or the
@@ -316,6 +349,7 @@ class JobRun:
             self.t_status = now
         self.nlog += 1
         if self.cfg.ckpt_every > 0 and step > 0 and step % self.cfg.ckpt_every == 0:
+            eng.check_health()          # never checkpoint a state an in-kernel timeout corrupted
             self.ckpter.save(self.chief)
             self.t_ckpt = now
         if self.nlog % self.ctl_every:
@@ -327,9 +361,12 @@ class JobRun:
                 action = "ckpt"         # Supervisor(save_model_secs=60), construct_distribute.py:391
         action = _agree(self.ctx, action)
         if self.ctx.enabled:
-            # a peer-buffer transport that timed out (xGMI channel, async_ps state) stops
-            # every rank together, at the next control point, not only at the end
+            # a peer-buffer transport or in-kernel wait that timed out (xGMI channel,
+            # async_ps state, the pair-backward tail) stops every rank together, at the
+            # next control point, not only at the end
             eng.sync.check_agreed()
+        elif action in ("ckpt", "pause"):
+            eng.check_health()
         if action == "ckpt":
             with trace_range("csa.ckpt"):
                 self.ckpter.save(self.chief)
@@ -351,8 +388,9 @@ class JobRun:
         eng.finish_async()            # async_ps: drain outstanding pushes, pull final shards
         eng.sync_device()
         # a peer wait that timed out after the last log step left this rank's gradient
-        # un-reduced: fail before evaluating / checkpointing diverged parameters
-        eng.sync.check_agreed()
+        # un-reduced, an in-kernel tail wait skipped updates: fail before evaluating /
+        # checkpointing diverged parameters (every rank together under data parallelism)
+        eng.check_health()
         self.mlog.close()
         final_acc = None
         if state == "done":
