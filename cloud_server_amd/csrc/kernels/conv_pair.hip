@@ -89,7 +89,8 @@ struct CPOptCarry {
   int blocks;                          // extra workgroups (0: no carry)
   int opt; float lr; const int64_t* step;
   float* w; const float* g; float* s0; float* s1;
-  const unsigned* pending;             // 1: the exchanged gradient awaits its update
+  unsigned* pending;                   // [0] 1: the exchanged gradient awaits its update;
+                                       // [1] retire ticket (the last workgroup clears [0])
   int count; long lo4[CP_MAXCS]; long start4[CP_MAXCS + 1];   // flat spans, float4 units
 };
 
@@ -97,11 +98,27 @@ struct CPOptCarry {
 // thread and iteration (the carrying forward keeps its occupancy; ~1 000 workgroups keep
 // 12 MB in flight).  Segment lookup by unrolled selects (no per-lane index into the
 // argument struct).
+__device__ __forceinline__ void cp_opt_carry_apply(const CPOptCarry& c, int k, int nblk);
+
+// The flag is retired by the carry itself: every workgroup takes a ticket after it read the
+// flag, and the last one clears it — so a host flush after the carrying forward (or a carry
+// after a flush) never applies the update twice, at any point of the step.
 __device__ __forceinline__ void cp_opt_carry(const CPOptCarry& c, int k, int nblk) {
   __shared__ unsigned s_pend;
   if (threadIdx.x == 0) s_pend = __hip_atomic_load(c.pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (!s_pend) return;
+  if (s_pend) cp_opt_carry_apply(c, k, nblk);
+  if (threadIdx.x == 0) {
+    // (relaxed: the flag carries no data; thread 0 read it before the barrier above)
+    unsigned* tk = c.pending + 1;
+    if (__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1) {
+      __hip_atomic_store(c.pending, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ void cp_opt_carry_apply(const CPOptCarry& c, int k, int nblk) {
   const int nslot = opt_nslots(c.opt);
   const float lr = opt_step_lr(c.opt, c.lr, c.step);
   const long m4 = c.start4[c.count];
@@ -536,6 +553,8 @@ struct CPBwdLayout {
   int KA, kpadA, KB, kpadB, KD, kpadD, c16, n16a, n16b;
   int npix2, kp2, npix1, kp1;       // owned pixels (conv B out / c1), padded to 4
   int wA, pA, pB, x, c1, dc2, dc1, red, offs, end;
+  int rA;                           // dwA's per-wave partials: inside the dc2 tile when it is
+                                    // large enough (dead by then), else after the bias sums
 };
 
 __host__ __device__ inline CPBwdLayout cp_bwd_layout(const CPGeom& g, int band, int TXH, int TXW, int T1H, int T1W) {
@@ -562,7 +581,17 @@ __host__ __device__ inline CPBwdLayout cp_bwd_layout(const CPGeom& g, int band, 
   L.c1 = o; o += (T1H * T1W * g.C1 + 3) & ~3;
   L.dc2 = o; o += (L.D2H * L.D2W * g.C2 + 3) & ~3;
   L.dc1 = o; o += ((L.npix1 + 1) * g.C1 + 3) & ~3;    // + one zero pixel row
-  L.red = o; o += (L.n16b * L.c16 + L.n16a * 16 + 4 * 16 * 16 + g.C2 + g.C1 + 3) & ~3;
+  // reduction region (round 6: 5 workgroups per CU in the carrying launch need <= ~31 KB):
+  //   [n16b x c16] dwB tile | [C2 + C1] bias sums | ([4][16][16] dwA partials, only when the
+  //   dc2 tile cannot hold them)
+  // and, earlier in the workgroup's life, the BatchNorm scratch: [2 MAXC2] slab sums |
+  // [4 MAXC2] tables | [2 MAXC2] backward sums (dead before the dwB tile is written)
+  const int dc2n = L.D2H * L.D2W * g.C2;
+  const int rmain = L.n16b * L.c16 + g.C2 + g.C1;
+  const bool rA_in_dc2 = dc2n >= 4 * 16 * 16;
+  const int rsz = rmain + (rA_in_dc2 ? 0 : 4 * 16 * 16);
+  L.red = o; o += ((rsz > 8 * CP_MAXC2 ? rsz : 8 * CP_MAXC2) + 3) & ~3;
+  L.rA = rA_in_dc2 ? L.dc2 : L.red + rmain;
   L.offs = o; o += 2 * L.kpadA + L.kp2 * 2 + L.kpadD * 2 + L.kp1 * 2 + L.n16b + 16;
   L.end = o;
   (void)L.wA;
@@ -646,8 +675,6 @@ __device__ __forceinline__ CPRoute cp_route(const CPGeom& g, const CPBwdLayout& 
 
 template <bool ONE>
 __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, float* smem) {
-  __shared__ float s_bn[4 * CP_MAXC2];
-  __shared__ float s_ss[2 * CP_MAXC2];
   const CPGeom& g = a.g;
   const int b = bid / g.nbands, band = bid % g.nbands;
   const int pr0 = band * g.PR;
@@ -665,6 +692,10 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   float* s_dc2 = smem + L.dc2;
   float* s_dc1 = smem + L.dc1;
   float* s_red = smem + L.red;
+  // BatchNorm tables / backward sums: dynamic LDS inside the reduction region (its dwB tile
+  // is written only after the route, their last reader) — no static LDS in this launch
+  float* s_bn = s_red + 2 * CP_MAXC2;                        // [4][MAXC2] mean | rstd | a | b
+  float* s_ss = s_bn + 4 * CP_MAXC2;                         // [2][C2] backward sums
   int* s_offA = reinterpret_cast<int*>(smem + L.offs);      // conv A (recompute): x offsets
   int* s_offPA = s_offA + L.kpadA;                           //                    panel rows
   int* s_pix2 = s_offPA + L.kpadA;                           // dwB: pixel -> c1 tile offset
@@ -925,8 +956,9 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
   CP_STAMP(11);
   // ---- weight gradient B: [taps (i, j, c1)] x [C2], K = owned conv-B-output pixels
   float* s_rB = s_red;                                        // [n16b][c16]
-  float* s_rA = s_red + L.n16b * L.c16;                       // [4 waves][16][16] partials
-  float* s_bias = s_rA + 4 * 16 * 16;                         // [C2] + [C1]
+  float* s_bias = s_red + L.n16b * L.c16;                     // [C2] + [C1]
+  float* s_rA = smem + L.rA;                                  // [4 waves][16][16] partials
+  const bool rA_alias = L.rA == L.dc2;                        // (uniform)
   cp_gemm(smem, L.n16b >> 4, L.c16 >> 4, L.kp2 >> 2, s_pix2, s_pixd,
           [&](int m) { return L.c1 + s_tapB[m]; },
           [&](int n) { return L.dc2 + n; },
@@ -997,6 +1029,8 @@ __device__ __forceinline__ void cp_bwd_body(const CPBwdArgs& a, const int bid, f
       const int p = 4 * ks + q;
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s_pix1x[p]], pb[s_pix1d[p]], acc, 0, 0, 0);
     }
+    // the partials overwrite the dc2 tile: every wave's bias sums (its last reader) first
+    if (rA_alias) __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) s_rA[wave * 256 + (4 * q + r) * 16 + i16] = acc[r];
   }
@@ -1259,7 +1293,7 @@ __device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs
 __constant__ long long* g_cp_life = nullptr;
 
 template <bool ONE, int NSLOT>
-__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u, CPTail t) {
+__device__ __forceinline__ void cp_bwd_upd_entry(const CPBwdArgs& a, const DUSegs& u, const CPTail& t) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (g_cp_life && threadIdx.x == 0) g_cp_life[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   cp_bwd_upd_body<ONE, NSLOT>(a, u, t, smem);
@@ -1267,6 +1301,21 @@ __global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd_kernel(CPBwdArgs
     __syncthreads();
     if (threadIdx.x == 0) g_cp_life[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   }
+}
+
+// Residency (round 6): 5 workgroups per CU.  The registers: the update-only body stages dY
+// through LDS-DMA (no staging VGPRs), 95-96 VGPRs at 5 waves per SIMD without spills for
+// 0 / 1 optimizer slots; the LDS: <= 31.2 KB per workgroup (the pair's BatchNorm scratch and
+// dwA partials alias dead regions, the head epilogue reuses the Xw slice, no static LDS).
+// Two slots (Adam) would spill at 5 waves: that form keeps the compiler's choice (4).
+template <bool ONE, int NSLOT>
+__global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(5)))
+void conv_pair_bwd_upd_kernel(CPBwdArgs a, DUSegs u, CPTail t) {
+  cp_bwd_upd_entry<ONE, NSLOT>(a, u, t);
+}
+template <bool ONE>
+__global__ __launch_bounds__(CP_THREADS) void conv_pair_bwd_upd2_kernel(CPBwdArgs a, DUSegs u, CPTail t) {
+  cp_bwd_upd_entry<ONE, 2>(a, u, t);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1322,6 +1371,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
   const int nX = t.TXH * t.TXW * g.C0;
   const int tid = threadIdx.x;
   CP_STAMP(0);
+  if (g_cp_life && tid == 0) g_cp_life[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   // ---- one batch of loads: weights + biases first, then the image rows (the staged
   // image is at a fixed address; otherwise its row index chain runs under the weights).
   // LDS weights: [wA | pad to 4 | wB] (wB read as float2 / float4 rows)
@@ -1489,6 +1539,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
   }
   cp_zero_early(z, npair);            // (at the end: stores in front would delay the loads)
   CP_STAMP(4);
+  if (g_cp_life && tid == 0) g_cp_life[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 // Small-pair VALU backward (round 3).  One workgroup per (image, band) as the MFMA
@@ -2008,7 +2059,7 @@ CSA_API int csa_conv_pair_valu_ok(const int* geom) {
 static thread_local CPOptCarry g_cp_carry{};
 
 static int cp_carry_make(CPOptCarry& c, int opt, float lr, const int64_t* step, float* w, const float* g, float* s0,
-                         float* s1, const unsigned* pending, int nseg, const long* seg_lo, const long* seg_hi,
+                         float* s1, unsigned* pending, int nseg, const long* seg_lo, const long* seg_hi,
                          int blocks) {
   c = CPOptCarry{};
   if (nseg < 1 || nseg > CP_MAXCS || !w || !g || !pending || blocks < 1) return -1;
@@ -2027,7 +2078,7 @@ static int cp_carry_make(CPOptCarry& c, int opt, float lr, const int64_t* step, 
 }
 
 CSA_API int csa_conv_pair_fwd_carry(int opt, float lr, const int64_t* step, float* w, const float* g, float* s0,
-                                    float* s1, const unsigned* pending, int nseg, const long* seg_lo,
+                                    float* s1, unsigned* pending, int nseg, const long* seg_lo,
                                     const long* seg_hi, int blocks) {
   return cp_carry_make(g_cp_carry, opt, lr, step, w, g, s0, s1, pending, nseg, seg_lo, seg_hi, blocks);
 }
@@ -2092,11 +2143,15 @@ static thread_local CPTail g_cp_tail{};
 
 template <bool ONE, int NSLOT>
 static int cp_launch_bwd_upd_t(const CPBwdArgs& a, const DUSegs& u, const CPTail& t, size_t lds, hipStream_t st) {
-  static const bool attr = hipFuncSetAttribute((const void*)conv_pair_bwd_upd_kernel<ONE, NSLOT>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
+  const void* fn = NSLOT == 2 ? (const void*)conv_pair_bwd_upd2_kernel<ONE>
+                              : (const void*)conv_pair_bwd_upd_kernel<ONE, NSLOT < 2 ? NSLOT : 0>;
+  static const bool attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CP_LDS_MAX) == hipSuccess;
   if (!attr) return -3;
   const unsigned blocks = (unsigned)(a.g.B * a.g.nbands + u.start[u.nseg] + (t.on ? t.param_blocks + t.stage_blocks : 0));
-  hipLaunchKernelGGL((conv_pair_bwd_upd_kernel<ONE, NSLOT>), dim3(blocks), dim3(CP_THREADS), lds, st, a, u, t);
+  if constexpr (NSLOT == 2)
+    hipLaunchKernelGGL((conv_pair_bwd_upd2_kernel<ONE>), dim3(blocks), dim3(CP_THREADS), lds, st, a, u, t);
+  else
+    hipLaunchKernelGGL((conv_pair_bwd_upd_kernel<ONE, NSLOT>), dim3(blocks), dim3(CP_THREADS), lds, st, a, u, t);
   return (int)hipGetLastError();
 }
 
@@ -2107,9 +2162,9 @@ static int cp_launch_bwd_upd(CPBwdArgs a, const DUSegs& u, hipStream_t st) {
   g_cp_tail = CPTail{};
   if (t.on) a.img_tk = cpt_word(t.tk, 1, 0);
   size_t lds = cp_lds(a.g, true);
-  const size_t dl = du_lds_floats(u.seg[0].M, 4) * sizeof(float);
+  const size_t dl = du_upo_lds_floats(u.seg[0].M) * sizeof(float);     // the update-only body
   for (int s = 1; s < u.nseg; ++s)
-    if (du_lds_floats(u.seg[s].M, 4) * sizeof(float) > dl) return -5;
+    if (du_upo_lds_floats(u.seg[s].M) * sizeof(float) > dl) return -5;
   if (dl > lds) lds = dl;
   const int ns = opt_nslots(u.seg[0].opt);
   const bool one = cp_bwd_one_batch(a);

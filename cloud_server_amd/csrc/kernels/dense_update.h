@@ -97,6 +97,18 @@ static __constant__ long long* g_du_dbg = nullptr;   // (per code object)
   } while (0)
 
 __host__ __device__ constexpr int du_nb(int waves) { return 32 * waves; }      // columns per block
+// Update-only (carried) body, 4 waves: the two 64-column dY halves land in LDS straight from
+// global memory (global_load_lds_dwordx4: no staging registers), each as [M4][64] with the
+// column quads of row r rotated by r (the bank spread the +4 row padding gave the register
+// path: a wave's LDS-DMA writes 1 KB contiguous, 4 rows); then the Xw slice [64][16], whose
+// space the head epilogue reuses ([64][DU_HMAXR] | [64][10]).  M = 50: 31.2 KB, so the
+// carrying launch fits 5 workgroups per CU (round 6).
+__host__ __device__ constexpr int du_upo_hw_floats() { return 64 * (8 + 10); }
+__host__ __device__ inline size_t du_upo_lds_floats(int M) {
+  const size_t m4 = (size_t)((M + 3) & ~3);
+  const size_t tail = 1024 > du_upo_hw_floats() ? 1024 : du_upo_hw_floats();
+  return 2 * m4 * 64 + tail;
+}
 __host__ __device__ inline size_t du_lds_floats(int M, int waves) {
   const size_t a = (size_t)M * (du_nb(waves) + 4), b = (size_t)waves * 4 * 16 * DU_FT;   // dY | the fold
   return (a > b ? a : b) + DU_MAXM * DU_FT + 6 * MAXC_DU + 4;
@@ -232,9 +244,12 @@ template <int NSLOT, int WAVES, bool HEAD, bool DGO = false, bool UPO = false>
 __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const int nblk, float* smem) {
   constexpr int THREADS = 64 * WAVES, NB = du_nb(WAVES), SN = NB + 4, HW = 16 * WAVES;
   const int M = a.M, K = a.K, N = a.N, cs = a.cs;
+  static_assert(!UPO || WAVES == 4, "the update-only body is the 4-wave carried form");
   float* sdy = smem;                                       // [M][SN] dY columns of the block, later the fold
   float* s_bn = smem + du_lds_floats(M, WAVES) - 6 * MAXC_DU - 4;   // [mean | rstd | a | b] x MAXC_DU
-  float* sxw = s_bn - DU_MAXM * DU_FT;                     // [64 m][16 f] Xw slice, later BN partials
+  const int M4 = (M + 3) & ~3;                             // UPO: rows of one DMA'd dY half
+  // [64 m][16 f] Xw slice, later BN partials (UPO: after the two dY halves, later s_hw)
+  float* sxw = UPO ? smem + 2 * M4 * 64 : s_bn - DU_MAXM * DU_FT;
   float* s_st = s_bn + 4 * MAXC_DU;                        // [2][MAXC_DU] slab-reduction scratch
   int* s_flag = reinterpret_cast<int*>(s_st + 2 * MAXC_DU);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -250,7 +265,13 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
   const int C = a.bn.C > 0 ? a.bn.C : 1;
   constexpr int nslot = NSLOT;
   DU_STAMP(0);
-  __shared__ float s_hw[HEAD ? 64 * (DU_HMAXR + DU_HNC) : 1];
+  float* s_hw;
+  if constexpr (UPO) {
+    s_hw = sxw;                                            // dead after the j = 1 barrier
+  } else {
+    __shared__ float s_hw_st[HEAD ? 64 * (DU_HMAXR + DU_HNC) : 1];
+    s_hw = s_hw_st;
+  }
   DUHead hd;
 
   // ---- every load, issued in the order it is consumed (vmcnt retires in order).  Two
@@ -266,7 +287,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
   // (0b) BN tables -> LDS (4C <= 512 values)
   const float* tsrc = tabs ? a.bn_tab : a.Xw;               // address select: unconditional loads
   float tv[512 / THREADS > 0 ? 512 / THREADS : 1];
-  constexpr int NTV = 512 / THREADS > 0 ? 512 / THREADS : 1;
+  constexpr int NTV = UPO ? 0 : (512 / THREADS > 0 ? 512 / THREADS : 1);   // (UPO: no BN)
 #pragma unroll
   for (int u = 0; u < NTV; ++u) {
     const int e = u * THREADS + tid;
@@ -284,6 +305,20 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
   bool sok[DU_SUB];
 #pragma unroll
   for (int j = 0; j < DU_SUB; ++j) {
+    if constexpr (UPO) {
+      // (1') dY half j straight into LDS: chunk c = 4 rows x 16 quads (one wave instruction);
+      // lane l writes LDS quad p = l & 15 of row r = 4c + l / 16, which holds column quad
+      // (p - r) & 15.  Chunks wave + 4u; a wave past the last chunk re-loads the last one
+      // (identical bytes to identical addresses).  Rows >= M: clamped, never read as data.
+      const int nch = M4 >> 2;
+#pragma unroll
+      for (int u = 0; u < DU_MAXM / 16; ++u) {
+        const int c = min(wave + 4 * u, nch - 1);
+        const int r = 4 * c + (lane >> 4), cq = ((lane & 15) - r) & 15;
+        const float* src = a.dY + (long)min(r, M - 1) * N + cb + HW * j + 4 * cq;
+        __builtin_amdgcn_global_load_lds(src, sdy + (j * M4 + 4 * c) * 64, 16, 0, 0);
+      }
+    } else {
     // (1) dY half j: float4 e = u * THREADS + tid -> row e / h4, block column HW j + 4 (e % h4)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -292,6 +327,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
       if (h4[j] == HW / 4) { row = e / (HW / 4); c4 = e % (HW / 4); }
       else if (h4[j] > 0) { row = e / h4[j]; c4 = e - row * h4[j]; }
       dyv[j][u] = reinterpret_cast<const float4*>(a.dY)[min(row, M - 1) * n4 + (h4[j] > 0 ? (cb + HW * j) / 4 + c4 : 0)];
+    }
     }
     // (2) W and slot float4s of sub-tile j
     const int lc = 16 * (wave + WAVES * j);                 // block-local first column
@@ -345,7 +381,9 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     }
     // stage dY half j (rows < M only: dgrad rows >= M are clamped reads whose outputs are
     // dropped, wgrad rows >= M meet Xw = 0); its columns are disjoint from half 0's, which
-    // other waves may still be reading
+    // other waves may still be reading.  (UPO: already in LDS; the compiler waits for the
+    // LDS-DMA before the barrier below.)
+    if constexpr (!UPO) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) pin(dyv[j][u]);
 #pragma unroll
@@ -356,6 +394,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
         const int c4 = e - row * h4[j];
         *reinterpret_cast<float4*>(sdy + row * SN + HW * j + 4 * c4) = dyv[j][u];
       }
+    }
     }
     if (j == 0 && a.bn_on && dgrad && !tabs)              // no precomputed tables: reduce here
       bn_reduce_to_lds(a.bn, s_bn, s_bn + MAXC_DU, s_bn + 2 * MAXC_DU, s_bn + 3 * MAXC_DU, s_st);
@@ -391,8 +430,19 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     du_f32x4 g0 = du_f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
     const float* col = sdy + n0 + i;
     float av[DU_KS];
+    if constexpr (UPO) {
+      // rotated half: column lc = 16 wave + i of half j, row r at quad ((lc >> 2) + r) & 15
+      const float* hb = sdy + j * M4 * 64;
+      const int lc = 16 * wave + i;
 #pragma unroll
-    for (int s = 0; s < DU_KS; ++s) av[s] = col[min(4 * s + q, M - 1) * SN];
+      for (int s = 0; s < DU_KS; ++s) {
+        const int r = min(4 * s + q, M - 1);
+        av[s] = hb[r * 64 + ((((lc >> 2) + r) & 15) << 2) + (lc & 3)];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < DU_KS; ++s) av[s] = col[min(4 * s + q, M - 1) * SN];
+    }
 #pragma unroll
     for (int s = 0; s < DU_KS; s += 2) {
       g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], xb[s], g0, 0, 0, 0);
@@ -422,7 +472,13 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
       const int lcol = grp * bper + u;
       if (lcol >= nb) break;
       const int n = cb + lcol;
-      float v = lane < M ? sdy[lane * SN + lcol] : 0.f;
+      float v;
+      if constexpr (UPO) {
+        const int lh = lcol & 63;
+        v = lane < M ? sdy[((lcol >> 6) * M4 + lane) * 64 + ((((lh >> 2) + lane) & 15) << 2) + (lh & 3)] : 0.f;
+      } else {
+        v = lane < M ? sdy[lane * SN + lcol] : 0.f;
+      }
       v = wave_sum(v);
       if (lane == 0) {
         if (u == wave) {                                   // the prefetched first column,

@@ -697,6 +697,14 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // KPT = head-input values per thread (Kh <= 256 KPT), KQ = W float4s per thread (Kh = 64 KQ)
+// diagnostics (csa_head_debug, scripts/microbench.py MB_HD): per workgroup b, four
+// s_memrealtime stamps (100 MHz, one clock for every XCD) at [8 + 4 b]: start | logits done
+// (loads landed) | softmax + dh done | dX stored
+#define HD_STAMP(k)                                                                           \
+  do {                                                                                        \
+    if (g_head_dbg && threadIdx.x == 0) g_head_dbg[8 + 4 * (long)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 template <int KPT, int KQ>
 __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
   __shared__ float s_part[HD_T / 64][HD_R][NCLS];
@@ -717,6 +725,7 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
   }
   const int m0 = rt * HD_R, f0 = fs * HD_FS;
   const int nr = min(HD_R, M - m0);
+  HD_STAMP(0);
   if (bid == 0 && tid == 0) {
     *a.step += 1;
     if (a.adv_cursor) {
@@ -772,6 +781,7 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
     }
   }
   __syncthreads();
+  HD_STAMP(1);
   if (wave < nr) {
     // wave r: row m0 + r; lane j < 10: logit j (waves folded in fixed order)
     const int r = wave, m = m0 + r;
@@ -826,6 +836,7 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
     }
   }
   __syncthreads();
+  HD_STAMP(2);
   // ---- dX[m0 + r][f0 + f] = sum_k dh[r][k] W[f][k]: 16 lanes per feature, DPP row sums
   float p[HD_R];
 #pragma unroll
@@ -850,6 +861,7 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
     if (a.act) g = act_bwd(g, xe, act_fwd(xe, a.act, a.alpha), a.act, a.alpha);
     a.dX[(long)(m0 + c) * K1 + f0 + f] = g;
   }
+  HD_STAMP(3);
 }
 
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.

@@ -52,7 +52,9 @@ def rccl_env_defaults() -> None:
       group, the streams outside torch's pool and the retirement wait made the watchdog's
       hipErrorCapturedEvent abort rare, but it still hit one world-1 ``allreduce`` run in the
       round-5 closing check (``profiles/r5_notes.md``).  Without the thread nothing queries an
-      event of a capturing stream.  Eager collectives (set-up, agreement flags, log points)
+      event of a capturing stream.  Measured on this torch (2.10.0+rocm7.0, RCCL 2.26.6): with
+      blocking wait the process has no ``pt_nccl_watchdg`` / ``pt_nccl_heartbt`` thread, without
+      it both run (``tests/test_gpu_rccl_threads.py``, ``profiles/r6_notes.md``).  Eager collectives (set-up, agreement flags, log points)
       then block the host until they finish, and a hung one raises after the group timeout
       instead of being aborted by the watchdog.  Measured: the DP GPU tests and 3 x 4 world-1
       DP benches at unchanged ms/step (``scripts/gpu_r5bw.sh``)."""

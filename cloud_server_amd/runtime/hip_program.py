@@ -243,7 +243,8 @@ class HipProgram:
         self.carry = segs
         self.carry_offsets = carried
         self.carry_blocks = max(1, min(1024, -(-m4 // 256)))
-        self.carry_pending = torch.zeros(1, dtype=torch.int32, device=e.device)
+        # [flag, retire ticket]: the carrying workgroups clear the flag themselves
+        self.carry_pending = torch.zeros(2, dtype=torch.int32, device=e.device)
 
     def _carry_args(self):
         e = self.e
@@ -371,6 +372,12 @@ class HipProgram:
             else:
                 self.lr_ranges.append((a, b))
                 open_range = True
+        # each range's end rounded up to 16 bytes through the alignment padding behind it
+        # (never-written zeros): the xGMI kernels take 16-byte multiples only, and a range
+        # left on RCCL would be the one collective of this program inside the graph that the
+        # peer-buffer path does not carry
+        starts = sorted(a for a, _ in spans) + [e.flat.numel()]
+        self.lr_ranges = [(a, min(-(-b // 4) * 4, min(x for x in starts if x >= b))) for a, b in self.lr_ranges]
         if self.lr_units:
             self.lr_side = dedicated_stream(dev)
             self.lr_first = min(self.units.index(u) for u in self.lr_units)

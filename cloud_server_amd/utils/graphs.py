@@ -71,7 +71,8 @@ def wait_retired(group=None, timeout_s: float = 10.0) -> Optional[bool]:
     if int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) <= 0:
         return None
     if os.environ.get("TORCH_NCCL_BLOCKING_WAIT", "0") == "1":
-        return None      # no watchdog thread exists, so nothing queries a captured event
+        return None      # no watchdog thread exists (tests/test_gpu_rccl_threads.py), so
+                         # nothing queries a captured event
     if group is None:
         if dist.get_backend() != "nccl":
             return None

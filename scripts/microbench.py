@@ -200,6 +200,47 @@ def main() -> int:
                 t = dbg.tolist()
                 print(f"{i:2d} {name}: stage {t[1]-t[0]} labels+sync {t[2]-t[1]} logits {t[3]-t[2]} "
                       f"loss {t[4]-t[3]} dW/dh {t[5]-t[4]} | total {t[5]-t[0]}")
+    if os.environ.get("MB_FWD_LIFE"):
+        # VALU pair forward: per-workgroup start / end (s_memrealtime, 100 MHz)
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name != "csa_conv_pair_fwd":
+                continue
+            life = torch.zeros(2 * 8192, dtype=torch.int64, device="cuda")
+            for _ in range(3):
+                life.zero_()
+                eng.program.lib.csa_cp_life_debug(life.data_ptr())
+                fn(*args)
+                torch.cuda.synchronize()
+                eng.program.lib.csa_cp_life_debug(None)
+            t = life.view(-1, 2).double().cpu()
+            t = t[t[:, 0] > 0]
+            t0 = float(t[:, 0].min())
+            st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0
+            print(f"{i:2d} {name}: {t.shape[0]} blocks, starts 0..{float(st.max()):.2f} us, ends "
+                  f"{float(en.min()):.2f}..{float(en.max()):.2f} us | life mean {float((en - st).mean()):.2f} "
+                  f"max {float((en - st).max()):.2f}")
+    if os.environ.get("MB_HD"):
+        # head_dgrad: per-workgroup stamps (start | logits | softmax + dh | dX), 100 MHz
+        for i, (name, fn, args) in enumerate(rec.calls):
+            if name != "csa_head_dgrad":
+                continue
+            nblk = 4096
+            dbg = torch.zeros(8 + 4 * nblk, dtype=torch.int64, device="cuda")
+            for _ in range(3):
+                dbg.zero_()
+                eng.program.lib.csa_head_debug(dbg.data_ptr())
+                fn(*args)
+                torch.cuda.synchronize()
+                eng.program.lib.csa_head_debug(None)
+            t = dbg[8:].view(nblk, 4).double().cpu()
+            t = t[t[:, 0] > 0]
+            t0 = float(t[:, 0].min())
+            st, en = (t[:, 0] - t0) / 100.0, (t[:, 3] - t0) / 100.0
+            ph = (t[:, 1:] - t[:, :-1]) / 100.0
+            print(f"{i:2d} {name}: {t.shape[0]} blocks, starts 0..{float(st.max()):.2f} us, ends "
+                  f"{float(en.min()):.2f}..{float(en.max()):.2f} us | life mean {float((en - st).mean()):.2f} "
+                  f"max {float((en - st).max()):.2f} | phases mean loads+logits {float(ph[:, 0].mean()):.2f} "
+                  f"softmax+dh {float(ph[:, 1].mean()):.2f} dX {float(ph[:, 2].mean()):.2f} us")
     # horizontal fusion: the deferred dense updates are host-side records that the pair
     # backward consumes, so every replay of that launch re-records them first
     defers = [(fn, args) for name, fn, args in rec.calls if name == "csa_dense_update_defer"]
