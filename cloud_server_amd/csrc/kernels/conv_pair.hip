@@ -1291,6 +1291,8 @@ __device__ __forceinline__ void cp_bwd_upd_body(const CPBwdArgs& a, const DUSegs
 // diagnostics: [block][2] start / end (s_memrealtime, 100 MHz, one clock for every XCD) of
 // each workgroup of the carrying launch (scripts/microbench.py MB_HF)
 __constant__ long long* g_cp_life = nullptr;
+// the same for the VALU pair forward (csa_cpv_life_debug)
+__constant__ long long* g_cpv_life = nullptr;
 
 template <bool ONE, int NSLOT>
 __device__ __forceinline__ void cp_bwd_upd_entry(const CPBwdArgs& a, const DUSegs& u, const CPTail& t) {
@@ -1371,7 +1373,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
   const int nX = t.TXH * t.TXW * g.C0;
   const int tid = threadIdx.x;
   CP_STAMP(0);
-  if (g_cp_life && tid == 0) g_cp_life[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (g_cpv_life && tid == 0) g_cpv_life[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   // ---- one batch of loads: weights + biases first, then the image rows (the staged
   // image is at a fixed address; otherwise its row index chain runs under the weights).
   // LDS weights: [wA | pad to 4 | wB] (wB read as float2 / float4 rows)
@@ -1539,7 +1541,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
   }
   cp_zero_early(z, npair);            // (at the end: stores in front would delay the loads)
   CP_STAMP(4);
-  if (g_cp_life && tid == 0) g_cp_life[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (g_cpv_life && tid == 0) g_cpv_life[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 // Small-pair VALU backward (round 3).  One workgroup per (image, band) as the MFMA
@@ -2022,6 +2024,10 @@ CSA_API int csa_cp_debug(long long* p) {
 // update workgroups carried by the pair backward (segment-local block numbers)
 CSA_API int csa_cp_du_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_du_dbg), &p, sizeof(p));
+}
+
+CSA_API int csa_cpv_life_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cpv_life), &p, sizeof(p));
 }
 
 CSA_API int csa_cp_life_debug(long long* p) {

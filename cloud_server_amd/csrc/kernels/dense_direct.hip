@@ -112,12 +112,33 @@ struct DDFwd {
 // table the conv pair's last workgroup folded — was measured slower than the separate
 // bn_act_apply launch both times: profiles/r2_dense_direct.md, profiles/r3_notes.md.)
 template <bool V4>
+__device__ __forceinline__ void dd_fwd_body(const DDFwd& a, const int nt, const int mb, const int ks, float* s_red);
+
+template <bool V4>
 __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
   __shared__ float s_red[DD_WAVES * 32 * 64];
   DD_STAMP(0);
   DD_SPAN_BEGIN();
+  dd_fwd_body<V4>(a, blockIdx.x, blockIdx.y, blockIdx.z, s_red);
+  DD_STAMP(3);
+  DD_SPAN_END();
+}
+
+// Grouped forward (round 6 prototype): G same-shape forwards of G packed
+// jobs in ONE launch — blockIdx.z = job * ksplit + k-split, a per-job argument table.
+constexpr int DD_GMAX = 16;
+struct DDFwdGroup { DDFwd a[DD_GMAX]; int g, ks; };
+
+template <bool V4>
+__global__ __launch_bounds__(DD_THREADS) void dd_fwd_group_kernel(DDFwdGroup grp) {
+  __shared__ float s_red[DD_WAVES * 32 * 64];
+  const int j = (int)blockIdx.z / grp.ks, ks = (int)blockIdx.z - j * grp.ks;
+  dd_fwd_body<V4>(grp.a[j], blockIdx.x, blockIdx.y, ks, s_red);
+}
+
+template <bool V4>
+__device__ __forceinline__ void dd_fwd_body(const DDFwd& a, const int nt, const int mb, const int ks, float* s_red) {
   const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-  const int nt = blockIdx.x, mb = blockIdx.y, ks = blockIdx.z;
   const int n0 = nt * 32, m0 = mb * 64;
   const int kg0 = ks * a.kper, kg1 = min(a.K, kg0 + a.kper);
   int ka, kb;
@@ -212,8 +233,6 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
     float* p = a.y + (long)m * a.N + nn;
     if (a.ksplit > 1) atomicAdd(p, v); else *p = v;
   }
-  DD_STAMP(3);
-  DD_SPAN_END();
 }
 
 // ------------------------------------------------------------------ dgrad
@@ -485,6 +504,28 @@ CSA_API int csa_dd_fwd_splits(int M, int N, int K) {
   return dd_splits(((N + 31) / 32) * ((M + 63) / 64), K);
 }
 
+// Grouping (prototype): between csa_dd_group_begin and csa_dd_group_end the forwards this
+// thread issues are recorded instead of launched, then run as ONE launch (same shapes).
+static thread_local DDFwdGroup g_dd_group{};
+static thread_local bool g_dd_grouping = false;
+CSA_API void csa_dd_group_begin() { g_dd_grouping = true; g_dd_group.g = 0; }
+CSA_API int csa_dd_group_end(hipStream_t st) {
+  g_dd_grouping = false;
+  const int G = g_dd_group.g;
+  if (G == 0) return 0;
+  const DDFwd& a0 = g_dd_group.a[0];
+  for (int j = 1; j < G; ++j) {
+    const DDFwd& a = g_dd_group.a[j];
+    if (a.M != a0.M || a.N != a0.N || a.K != a0.K || a.ksplit != a0.ksplit || a.kper != a0.kper) return -2;
+  }
+  g_dd_group.ks = a0.ksplit;
+  const dim3 grid((a0.N + 31) / 32, (a0.M + 63) / 64, a0.ksplit * G);
+  if (a0.K % 4 == 0) hipLaunchKernelGGL(dd_fwd_group_kernel<true>, grid, dim3(DD_THREADS), 0, st, g_dd_group);
+  else hipLaunchKernelGGL(dd_fwd_group_kernel<false>, grid, dim3(DD_THREADS), 0, st, g_dd_group);
+  g_dd_group.g = 0;
+  return (int)hipGetLastError();
+}
+
 // Y[M][N] (+)= act(X)[M][K] . W[K][N] + bias.  Y must be zeroed when splits > 1.
 CSA_API int csa_dd_fwd(const float* X, const float* W, const float* bias, float* Y, int M, int N, int K,
                        int act, float alpha, hipStream_t st) {
@@ -494,6 +535,11 @@ CSA_API int csa_dd_fwd(const float* X, const float* W, const float* bias, float*
   const int kper = dd_kper(K, ks);
   ks = (K + kper - 1) / kper;
   DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper};
+  if (g_dd_grouping) {
+    if (g_dd_group.g >= DD_GMAX) return -3;
+    g_dd_group.a[g_dd_group.g++] = a;
+    return 0;
+  }
   if (K % 4 == 0) hipLaunchKernelGGL(dd_fwd_kernel<true>, dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
   else hipLaunchKernelGGL(dd_fwd_kernel<false>, dim3(nt, mb, ks), dim3(DD_THREADS), 0, st, a);
   return (int)hipGetLastError();

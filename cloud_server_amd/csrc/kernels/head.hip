@@ -688,6 +688,14 @@ struct HeadDgradArgs {
   float* dX;                                                  // [M][K1]
 };
 
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xf, 0xf, false)));
+  return v;
+}
+
 __device__ __forceinline__ float row16_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
@@ -697,12 +705,12 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // KPT = head-input values per thread (Kh <= 256 KPT), KQ = W float4s per thread (Kh = 64 KQ)
-// diagnostics (csa_head_debug, scripts/microbench.py MB_HD): per workgroup b, four
-// s_memrealtime stamps (100 MHz, one clock for every XCD) at [8 + 4 b]: start | logits done
-// (loads landed) | softmax + dh done | dX stored
+// diagnostics (csa_head_debug, scripts/microbench.py MB_HD): per workgroup b, six
+// s_memrealtime stamps (100 MHz, one clock for every XCD) at [8 + 8 b]: start | head input
+// landed (act applied) | logits done | softmax + dh done | dX dot done | dX stored
 #define HD_STAMP(k)                                                                           \
   do {                                                                                        \
-    if (g_head_dbg && threadIdx.x == 0) g_head_dbg[8 + 4 * (long)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    if (g_head_dbg && threadIdx.x == 0) g_head_dbg[8 + 8 * (long)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 template <int KPT, int KQ>
@@ -769,31 +777,74 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
 #pragma unroll
     for (int r = 0; r < HD_R; ++r) hx[r][u] = ok ? act_fwd(hv[r][u], a.in_act, a.in_alpha) : 0.f;
   }
+  if (g_head_dbg) {                                        // (diagnostics: after hx exists)
+    float z = 0.f;
 #pragma unroll
-  for (int r = 0; r < HD_R; ++r) {
+    for (int r = 0; r < HD_R; ++r) z += hx[r][0];
+    if (threadIdx.x == 0) g_head_dbg[8 + 8 * (long)blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime() + (z == 12345.f);
+  }
+  // the R x 10 logit partials of this thread's k values, then their sums over the 256
+  // threads.  Round 6: a transposed reduction instead of 40 wave reductions (each 4 DPP +
+  // 2 cross-row shuffles, serialised: 4.7 us of the launch's 9 us workgroup life,
+  // scripts/mb/graph_life.py): two DPP exchange rounds inside each quad halve the values
+  // per lane twice (40 -> 20 -> 10, a lane keeps one half and adds its partner's copy of
+  // it), the quads' 40 sums go to LDS output-major, 160 threads sum 16 quads each, in fixed
+  // order (bitwise-repeatable).
+  {
+    float v[HD_R * NCLS];
 #pragma unroll
-    for (int j = 0; j < NCLS; ++j) {
-      float acc = 0.f;
+    for (int r = 0; r < HD_R; ++r)
 #pragma unroll
-      for (int u = 0; u < KPT; ++u) acc = fmaf(hx[r][u], wv[u][j], acc);
-      acc = wave_sum_dpp(acc);
-      if (lane == 0) s_part[wave][r][j] = acc;
+      for (int j = 0; j < NCLS; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) acc = fmaf(hx[r][u], wv[u][j], acc);
+        v[r * NCLS + j] = acc;
+      }
+    constexpr int NO = HD_R * NCLS, H1 = NO / 2, H2 = NO / 4;
+    const bool b0 = lane & 1, b1 = lane & 2;
+    float w1[H1];
+#pragma unroll
+    for (int m = 0; m < H1; ++m) {                         // partner lane ^ 1
+      const float send = b0 ? v[m] : v[m + H1], keep = b0 ? v[m + H1] : v[m];
+      w1[m] = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0xb1, 0xf, 0xf, false));
+    }
+    // [NO][68]: 64 quads of the workgroup per output, +4 so the 4 lanes of a quad (4
+    // different outputs) hit different banks
+    __shared__ __attribute__((aligned(16))) float s_red[HD_R * NCLS * 68];
+    const int gq = wave * 16 + (lane >> 2), base = (b0 ? H1 : 0) + (b1 ? H2 : 0);
+#pragma unroll
+    for (int m = 0; m < H2; ++m) {                         // partner lane ^ 2
+      const float send = b1 ? w1[m] : w1[m + H2], keep = b1 ? w1[m + H2] : w1[m];
+      const float w2 = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x4e, 0xf, 0xf, false));
+      s_red[(base + m) * 68 + gq] = w2;
+    }
+    __syncthreads();
+    if (tid < NO * 4) {                                    // output o, wave w: its 16 quads
+      const int o = tid >> 2, w = tid & 3;
+      const float4* p4 = reinterpret_cast<const float4*>(s_red + o * 68 + w * 16);
+      const float4 x0 = p4[0], x1 = p4[1], x2 = p4[2], x3 = p4[3];
+      float acc = ((x0.x + x0.y) + (x0.z + x0.w)) + ((x1.x + x1.y) + (x1.z + x1.w));
+      acc += ((x2.x + x2.y) + (x2.z + x2.w)) + ((x3.x + x3.y) + (x3.z + x3.w));
+      s_part[w][o / NCLS][o % NCLS] = acc;
     }
   }
   __syncthreads();
-  HD_STAMP(1);
+  HD_STAMP(2);
   if (wave < nr) {
     // wave r: row m0 + r; lane j < 10: logit j (waves folded in fixed order)
     const int r = wave, m = m0 + r;
     float z = -INFINITY;
     if (lane < NCLS) z = s_part[0][r][lane] + s_part[1][r][lane] + s_part[2][r][lane] + s_part[3][r][lane] + bias;
-    const float mx = wave_max(z);
+    // the 10 classes live in lanes 0..9 (row 0 of the wave): 16-lane DPP reductions, no
+    // cross-row shuffles (lanes >= 16 reduce their own rows, unused)
+    const float mx = row16_max(z);
     const unsigned long long hit = __ballot(lane < NCLS && z == mx);
     const int am = __builtin_ctzll(hit);       // lowest index attaining the max (tf.argmax)
     float d = 0.f, lterm = 0.f;
     if (a.loss == 0) {
       const float e = lane < NCLS ? __expf(z - mx) : 0.f;
-      const float se = wave_sum(e);
+      const float se = row16_sum(e);
       const float lse = mx + __logf(se);
       if (lane < NCLS) {
         d = (__expf(z - lse) - (lane == label ? 1.f : 0.f)) * (a.grad_scale / (float)M);
@@ -804,7 +855,7 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
       lterm = t * t;
       d = t * (2.f * a.grad_scale / (float)(M * NCLS));
     }
-    const float ls = wave_sum(lterm);
+    const float ls = row16_sum(lterm);
     if (lane < NCLS) s_dl[r][lane] = d;
     if (fs == 0) {
       if (lane < NCLS) a.dl[(long)m * NCLS + lane] = d;
@@ -836,7 +887,7 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
     }
   }
   __syncthreads();
-  HD_STAMP(2);
+  HD_STAMP(3);
   // ---- dX[m0 + r][f0 + f] = sum_k dh[r][k] W[f][k]: 16 lanes per feature, DPP row sums
   float p[HD_R];
 #pragma unroll
@@ -856,12 +907,13 @@ __global__ __launch_bounds__(HD_T) void head_dgrad_kernel(HeadDgradArgs a) {
     const float t = row16_sum(p[r]);
     mine = c == r ? t : mine;
   }
+  if (g_head_dbg && threadIdx.x == 0) g_head_dbg[8 + 8 * (long)blockIdx.x + 4] = (long long)__builtin_amdgcn_s_memrealtime() + (mine == 12345.f);
   if (c < nr && f0 + f < K1) {
     float g = mine;
     if (a.act) g = act_bwd(g, xe, act_fwd(xe, a.act, a.alpha), a.act, a.alpha);
     a.dX[(long)(m0 + c) * K1 + f0 + f] = g;
   }
-  HD_STAMP(3);
+  HD_STAMP(5);
 }
 
 // General fallback (M > 64 or too large for LDS): VALU, operands through L2.

@@ -79,6 +79,9 @@ _SIGS = {
     "csa_cp_debug": (I, [P]),
     "csa_cp_debug_block": (I, [I]),
     "csa_cp_life_debug": (I, [P]),
+    "csa_cpv_life_debug": (I, [P]),
+    "csa_dd_group_begin": (None, []),
+    "csa_dd_group_end": (I, [P]),
     "csa_cp_du_debug": (I, [P]),
     "csa_conv_pair_bn_tab": (None, [P]),
     "csa_head_debug": (I, [P]),
@@ -184,8 +187,16 @@ def load(required: bool = True) -> Optional[C.CDLL]:
                 raise RuntimeError(f"HIP kernel library missing: {path} (run python -m cloud_server_amd.ops.build)")
             return None
     lib = C.CDLL(path)
+    variant = bool(os.environ.get("CSA_KERNEL_LIB"))
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            # an A/B baseline built from an older revision (CSA_KERNEL_LIB) may lack entry
+            # points added since; the in-tree library must have every one
+            if variant:
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _LIB = lib

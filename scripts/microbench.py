@@ -208,10 +208,10 @@ def main() -> int:
             life = torch.zeros(2 * 8192, dtype=torch.int64, device="cuda")
             for _ in range(3):
                 life.zero_()
-                eng.program.lib.csa_cp_life_debug(life.data_ptr())
+                eng.program.lib.csa_cpv_life_debug(life.data_ptr())
                 fn(*args)
                 torch.cuda.synchronize()
-                eng.program.lib.csa_cp_life_debug(None)
+                eng.program.lib.csa_cpv_life_debug(None)
             t = life.view(-1, 2).double().cpu()
             t = t[t[:, 0] > 0]
             t0 = float(t[:, 0].min())

@@ -143,9 +143,11 @@ def test_collective_autotune_records_both_paths(pg, monkeypatch):
         a.step(); b.step()
     a.sync_device(); b.sync_device()   # (lands a deferred dense update)
     a.sync.check()
-    assert set(a.sync.xgmi_tuning) >= {"lr_x", "lr_dy"}, a.sync.xgmi_tuning
-    for v in a.sync.xgmi_tuning.values():
-        assert v["xgmi_us"] > 0 and v["rccl_us"] > 0
+    # gather sites (lr_x, lr_dy) time the xGMI gather; the remainder all-reduce (lr_rem,
+    # 16-byte aligned since round 6) times the one-shot protocol — each against RCCL
+    assert set(a.sync.xgmi_tuning) >= {"lr_x", "lr_dy", "lr_rem"}, a.sync.xgmi_tuning
+    for tag, v in a.sync.xgmi_tuning.items():
+        assert v["rccl_us"] > 0 and v["xgmi_us" if tag in ("lr_x", "lr_dy") else "oneshot_us"] > 0, (tag, v)
     print("collective tuning (world 1):", a.sync.xgmi_tuning)
     for n in a.model.state.shapes:          # lowrank uses the dense-last layout: compare by name
         torch.testing.assert_close(a.model.state.view(n, a.flat), b.model.state.view(n, b.flat),

@@ -482,7 +482,11 @@ def _worker_prod(rank: int, world: int, port: int, q, sync_bn: bool, det: bool) 
         cfg = _prod_cfg(50, sync_bn)
         ds = synthetic_mnist(2000, seed=0)
         res = {}
+        os.makedirs("gpurun_out", exist_ok=True)
+        prog = open(f"gpurun_out/prod_progress_{world}_{rank}.txt", "a")   # (a live sign per phase)
         for strategy in (("allreduce",) if det else PROD_STRATEGIES):
+            prog.write(f"{time.time():.1f} world {world} rank {rank} det {det} sync_bn {sync_bn}: {strategy}\n")
+            prog.flush()
             ctx = DistContext(rank=rank, world=world, local_rank=0, backend="nccl", device=dev)
             eng = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
             assert eng.backend == "hip", (strategy, eng.fallback_reason)
