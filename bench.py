@@ -242,6 +242,19 @@ def main() -> int:
     eng.sync_device()
     dt = time.perf_counter() - t0
     dt = all_reduce_max(ctx, dt)
+    dt_train = None
+    if eng.extra_group_sizes:
+        # the same K steps again through the graph sizes training's run_steps uses (32, 16,
+        # .., 2: no K-step graph) — reported beside the headline
+        eng.extra_group_sizes = []
+        barrier(ctx)
+        eng.sync_device()
+        t1 = time.perf_counter()
+        eng.run_steps(args.steps)
+        eng.sync_device()
+        barrier(ctx)
+        eng.sync_device()
+        dt_train = all_reduce_max(ctx, time.perf_counter() - t1)
     # a timed-out xGMI peer wait or in-kernel tail wait (skipped updates) invalidates the
     # run: fail loudly (agreed by every rank under data parallelism)
     eng.check_health()
@@ -261,6 +274,8 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt * 1e3 / args.steps, 5),
+            # the same K steps replayed as training's graph sizes (null: K > 64, already so)
+            "ms_per_step_training_graphs": None if dt_train is None else round(dt_train * 1e3 / args.steps, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(total / BASELINE_SAMPLES_PER_S, 2),

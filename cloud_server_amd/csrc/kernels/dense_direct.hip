@@ -25,6 +25,7 @@
 // workgroup's K range; their partials meet in LDS in fixed wave order.
 #include "common.h"
 #include "optim_common.h"
+#include "head_dgrad.h"
 #include <cstdlib>
 
 namespace csa {
@@ -106,7 +107,14 @@ __device__ __forceinline__ void dd_wave_range(int k0, int k1, int& a, int& b) {
 struct DDFwd {
   const float* x; const float* w; const float* bias; float* y;
   int M, N, K, act; float alpha; int ksplit, kper;   // kper: K per workgroup (multiple of 8)
+  int life_base;                                     // (diagnostics: first stamp slot)
 };
+
+// diagnostics: per-workgroup start / end of the forward (s_memrealtime, 100 MHz) at
+// [base + 2 b], b the linear block index; base advances by 2 x grid per launch, so one
+// buffer holds a step's two forwards (csa_dd_life_debug; scripts/mb/graph_life.py)
+__constant__ long long* g_dd_life = nullptr;
+
 
 // (Applying a producer's BatchNorm while loading A — from its statistic slab, or from a
 // table the conv pair's last workgroup folded — was measured slower than the separate
@@ -114,12 +122,16 @@ struct DDFwd {
 template <bool V4>
 __device__ __forceinline__ void dd_fwd_body(const DDFwd& a, const int nt, const int mb, const int ks, float* s_red);
 
+
 template <bool V4>
 __global__ __launch_bounds__(DD_THREADS) void dd_fwd_kernel(DDFwd a) {
   __shared__ float s_red[DD_WAVES * 32 * 64];
   DD_STAMP(0);
   DD_SPAN_BEGIN();
+  const long lb = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+  if (g_dd_life && threadIdx.x == 0) g_dd_life[2 * lb + 2 * a.life_base] = (long long)__builtin_amdgcn_s_memrealtime();
   dd_fwd_body<V4>(a, blockIdx.x, blockIdx.y, blockIdx.z, s_red);
+  if (g_dd_life && threadIdx.x == 0) g_dd_life[2 * lb + 2 * a.life_base + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   DD_STAMP(3);
   DD_SPAN_END();
 }
@@ -134,6 +146,106 @@ __global__ __launch_bounds__(DD_THREADS) void dd_fwd_group_kernel(DDFwdGroup grp
   __shared__ float s_red[DD_WAVES * 32 * 64];
   const int j = (int)blockIdx.z / grp.ks, ks = (int)blockIdx.z - j * grp.ks;
   dd_fwd_body<V4>(grp.a[j], blockIdx.x, blockIdx.y, ks, s_red);
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused forward chain (round 6): fc1 forward -> fc2 forward -> head_dgrad as ONE launch.
+// In the one-GPU step each of these was its own launch, and every boundary cost ~2-3 us
+// between the last workgroup of one and the first of the next (scripts/mb/graph_life.py:
+// the end-of-kernel write-back + the next dispatch).  Here the stages are blockIdx ranges
+// [fc1 | fc2 | head]; dispatch is in order, so a stage's workgroups are all dispatched
+// before any of the next, and a later stage's workgroup waits (bounded) on the earlier
+// stage's ticket.  Both forwards are split-K with device-scope atomic outputs, so a
+// workgroup's results are performed once its waves' atomics have returned (the barrier's
+// s_waitcnt) — a relaxed ticket add after that barrier publishes them; the consumer's one
+// agent-scope acquire after its poll invalidates its stale lines (the carrier's tail uses
+// the same argument, conv_pair.hip).  A forward with one k-split (plain stores) releases
+// before its ticket.  A timed-out wait (1 s) sets the error word and skips that
+// workgroup's work (never a hung launch); the job's health check reads it.
+// ---------------------------------------------------------------------------------------
+
+constexpr int CH_LINE = 16;                          // words on their own 64-byte lines
+constexpr int CH_GO = 16;                            // go-flag lines per stage (spread polling)
+constexpr int CH_WORDS = (3 + 2 * CH_GO) * CH_LINE;  // counts [3] | go of fc2 [16] | go of head [16]
+struct ChainArgs {
+  DDFwd f[2];
+  int n1, n2, n3;                                    // workgroups of fc1, fc2, head
+  HeadDgradArgs h;
+  unsigned* tk;                                      // [CH_WORDS] zero between launches
+  int* err;
+};
+
+__device__ __forceinline__ unsigned* chain_go(unsigned* tk, int stage, int j) {
+  return tk + (3 + stage * CH_GO + j) * CH_LINE;
+}
+
+// A waiting workgroup polls ITS go line (one of CH_GO per stage: hundreds of pollers on
+// one word made every poll and the producers' atomics queue at that word's channel —
+// measured: the stages started 15-20 us late), which the producing stage's last workgroup
+// sets.
+__device__ __forceinline__ bool chain_wait(unsigned* tk, int stage, int bid, int* err) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    const unsigned* go = chain_go(tk, stage, bid % CH_GO);
+    const unsigned long long t0 = wall_clock64();
+    int ok = 1;
+    while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      if (wall_clock64() - t0 > 100000000ull) {       // 1 s
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// this workgroup's results are out (its waves' stores / atomics drained): count it
+__device__ __forceinline__ unsigned chain_ticket(unsigned* tk, bool release) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ unsigned s_prev;
+  if (threadIdx.x == 0) {
+    if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_prev;
+}
+
+template <bool V4>
+__device__ __forceinline__ void dd_fwd_body(const DDFwd& a, const int nt, const int mb, const int ks, float* s_red);
+
+template <int KPT, int KQ>
+__global__ __launch_bounds__(DD_THREADS) void fwd_chain_kernel(ChainArgs c) {
+  __shared__ float s_red[DD_WAVES * 32 * 64];
+  const int bid = (int)blockIdx.x;
+  if (bid < c.n1 + c.n2) {
+    const int st = bid < c.n1 ? 0 : 1;
+    const DDFwd& a = c.f[st];
+    const int lb = st ? bid - c.n1 : bid;
+    bool go = true;
+    if (st == 1) go = chain_wait(c.tk, 0, lb, c.err);
+    if (g_dd_life && threadIdx.x == 0) g_dd_life[2 * (lb + a.life_base)] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (go) {
+      const int ntile = (a.N + 31) / 32, mbn = (a.M + 63) / 64;
+      dd_fwd_body<true>(a, lb % ntile, (lb / ntile) % mbn, lb / (ntile * mbn), s_red);
+    }
+    if (g_dd_life && threadIdx.x == 0) g_dd_life[2 * (lb + a.life_base) + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+    const unsigned prev = chain_ticket(c.tk + st * CH_LINE, a.ksplit == 1);
+    if (threadIdx.x < CH_GO && prev == (unsigned)(st ? c.n2 : c.n1) - 1)   // the stage is done
+      __hip_atomic_store(chain_go(c.tk, st, threadIdx.x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int hb = bid - c.n1 - c.n2;
+  if (chain_wait(c.tk, 1, hb, c.err)) head_dgrad_body<KPT, KQ>(c.h, hb);
+  const unsigned prev = chain_ticket(c.tk + 2 * CH_LINE, false);
+  if (threadIdx.x < 3 + 2 * CH_GO && prev == (unsigned)c.n3 - 1)   // every wait is over: reset
+    __hip_atomic_store(c.tk + threadIdx.x * CH_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool V4>
@@ -496,12 +608,54 @@ static int dd_kper(int K, int ks) { return (((K + ks - 1) / ks) + 7) & ~7; }
 
 using namespace csa;
 
+CSA_API int csa_dd_life_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dd_life), &p, sizeof(p));
+}
+
 CSA_API int csa_dd_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dd_dbg), &p, sizeof(p));
 }
 
 CSA_API int csa_dd_fwd_splits(int M, int N, int K) {
   return dd_splits(((N + 31) / 32) * ((M + 63) / 64), K);
+}
+
+// Forward chain recording: between csa_chain_begin and csa_chain_end, the two forwards and
+// the head_dgrad this thread issues are recorded, then launched as fwd_chain_kernel.
+namespace csa { thread_local HDRecord g_hd_rec{}; }
+static thread_local int g_chain_on = 0, g_chain_n = 0;
+static thread_local DDFwd g_chain_f[2];
+CSA_API void csa_chain_begin() { g_chain_on = 1; g_chain_n = 0; g_hd_rec.on = 1; g_hd_rec.has = 0; }
+CSA_API void csa_chain_reset() { g_chain_on = 0; g_chain_n = 0; g_hd_rec.on = 0; g_hd_rec.has = 0; }
+CSA_API int csa_chain_ok(int kh) { return kh == 256 || kh == 512 || kh == 1024 ? 1 : 0; }
+// tk: csa_chain_words() zeroed uint32 (device), err: 1 int (device)
+CSA_API int csa_chain_words() { return CH_WORDS; }
+CSA_API int csa_chain_end(unsigned* tk, int* err, hipStream_t st) {
+  const int n = g_chain_n, has = g_hd_rec.has, kq = g_hd_rec.kq;
+  const HeadDgradArgs h = g_hd_rec.a;
+  csa_chain_reset();
+  if (n != 2 || !has || !tk || !err) return -1;
+  ChainArgs c{};
+  for (int j = 0; j < 2; ++j) {
+    const DDFwd& a = g_chain_f[j];
+    if (a.K % 4) return -2;
+    c.f[j] = a;
+  }
+  c.n1 = ((c.f[0].N + 31) / 32) * ((c.f[0].M + 63) / 64) * c.f[0].ksplit;
+  c.n2 = ((c.f[1].N + 31) / 32) * ((c.f[1].M + 63) / 64) * c.f[1].ksplit;
+  c.n3 = ((h.M + HD_R - 1) / HD_R) * ((h.K1 + HD_FS - 1) / HD_FS);
+  c.h = h; c.tk = tk; c.err = err;
+  const dim3 grid((unsigned)(c.n1 + c.n2 + c.n3)), blk(DD_THREADS);
+  static_assert(DD_THREADS == HD_T, "one block shape for every stage");
+  if (kq == 4) hipLaunchKernelGGL((fwd_chain_kernel<1, 4>), grid, blk, 0, st, c);
+  else if (kq == 8) hipLaunchKernelGGL((fwd_chain_kernel<2, 8>), grid, blk, 0, st, c);
+  else if (kq == 16) hipLaunchKernelGGL((fwd_chain_kernel<4, 16>), grid, blk, 0, st, c);
+  else return -3;
+  return (int)hipGetLastError();
+}
+
+CSA_API int csa_chain_head_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hd_dbg), &p, sizeof(p));
 }
 
 // Grouping (prototype): between csa_dd_group_begin and csa_dd_group_end the forwards this
@@ -534,7 +688,13 @@ CSA_API int csa_dd_fwd(const float* X, const float* W, const float* bias, float*
   int ks = dd_splits(nt * mb, K);
   const int kper = dd_kper(K, ks);
   ks = (K + kper - 1) / kper;
-  DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper};
+  DDFwd a{X, W, bias, Y, M, N, K, act, alpha, ks, kper, 0};
+  a.life_base = K > 1024 ? 0 : 4096;                 // (diagnostics: wide layers first)
+  if (g_chain_on) {
+    if (g_chain_n >= 2) return -4;
+    g_chain_f[g_chain_n++] = a;
+    return 0;
+  }
   if (g_dd_grouping) {
     if (g_dd_group.g >= DD_GMAX) return -3;
     g_dd_group.a[g_dd_group.g++] = a;

@@ -15,8 +15,13 @@ struct ApplyArgs {
   float* tab;   // optional [4][C] mean | rstd | a | b for later consumers (block 0 writes)
 };
 
+// diagnostics: per-workgroup start / end (s_memrealtime, 100 MHz) at [2 b], [2 b + 1]
+// (csa_ew_life_debug; scripts/mb/graph_life.py)
+__constant__ long long* g_ew_life = nullptr;
+
 __global__ __launch_bounds__(256) void bn_act_apply_kernel(ApplyArgs a) {
   __shared__ float s_bn[4 * 128 + 2 * 128];
+  if (g_ew_life && threadIdx.x == 0) g_ew_life[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   // the element loads go out before the slab reduction (overlapping round trips)
   const long i4 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long n4 = a.n >> 2;
@@ -26,6 +31,7 @@ __global__ __launch_bounds__(256) void bn_act_apply_kernel(ApplyArgs a) {
   __syncthreads();
   if (a.tab && blockIdx.x == 0)
     for (int c = threadIdx.x; c < 4 * a.C; c += blockDim.x) a.tab[c] = s_bn[(c / a.C) * 128 + c % a.C];
+  if (g_ew_life && threadIdx.x == 0) g_ew_life[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   if (i4 >= n4) return;
   const FastDiv dc(a.C);
   int q, c0;
@@ -43,6 +49,10 @@ __global__ __launch_bounds__(256) void bn_act_apply_kernel(ApplyArgs a) {
 }  // namespace csa
 
 using namespace csa;
+
+CSA_API int csa_ew_life_debug(long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ew_life), &p, sizeof(p));
+}
 
 // n % 4 == 0; channel of element e is e % C (NHWC flattened).
 CSA_API int csa_bn_act_apply(const float* x, float* y, long n, int C, const float* bn_slab,

@@ -81,6 +81,14 @@ _SIGS = {
     "csa_cp_life_debug": (I, [P]),
     "csa_cpv_life_debug": (I, [P]),
     "csa_dd_group_begin": (None, []),
+    "csa_chain_begin": (None, []),
+    "csa_chain_reset": (None, []),
+    "csa_chain_ok": (I, [I]),
+    "csa_chain_words": (I, []),
+    "csa_chain_end": (I, [P, P, P]),
+    "csa_chain_head_debug": (I, [P]),
+    "csa_dd_life_debug": (I, [P]),
+    "csa_ew_life_debug": (I, [P]),
     "csa_dd_group_end": (I, [P]),
     "csa_cp_du_debug": (I, [P]),
     "csa_conv_pair_bn_tab": (None, [P]),

@@ -26,9 +26,19 @@ from .dist import DistContext, all_reduce_max, barrier
 
 def time_strategy(cfg, ds, ctx: DistContext, strategy: str, steps: int = 30, warmup: int = 5,
                   backend: str = "auto") -> float:
-    """Seconds per step of ``strategy`` (max over ranks)."""
+    """Seconds per step of ``strategy`` (max over ranks); ``inf`` for a ":hf" trial whose
+    engine did not come out as the :hf program (no HIP program, or its hfuse / tail-fold
+    preconditions failed) — it would only time a duplicate of the plain strategy."""
     from ..runtime.engine import TrainEngine
     eng = TrainEngine(cfg, ds, device=ctx.device, ctx=ctx, backend=backend, strategy=strategy)
+    if strategy.endswith(":hf"):
+        built = bool(getattr(getattr(eng, "program", None), "dp_hf", False))
+        if all_reduce_max(ctx, 0.0 if built else 1.0) > 0.0:   # the same answer on every rank
+            if eng.sync is not None and eng.sync.xgmi is not None:
+                barrier(ctx)
+                eng.sync.xgmi.close()
+            del eng
+            return float("inf")
     for _ in range(warmup):
         eng.step()
     eng.sync_device()
@@ -101,4 +111,5 @@ def pick_strategy(cfg, ds, ctx: DistContext, candidates: Optional[Sequence[str]]
         return candidates[0], {}
     times = {s: time_strategy(cfg, ds, ctx, s, steps=steps, backend=backend) * 1e3 for s in candidates}
     best = min(candidates, key=lambda s: (times[s], candidates.index(s)))
-    return best, {k: round(v, 4) for k, v in times.items()}
+    # (a skipped ":hf" trial is reported as null)
+    return best, {k: (round(v, 4) if v != float("inf") else None) for k, v in times.items()}

@@ -196,6 +196,34 @@ class HipProgram:
         self._plan_carry()
         self.opt_segments = self._opt_segments()
         self._plan_tail()
+        self._plan_chain()
+
+    def _plan_chain(self) -> None:
+        """One-GPU program: fc1's forward, fc2's forward and the head launch run as ONE
+        launch (``csa_chain_begin`` / ``csa_chain_end``: dense_direct.hip fwd_chain_kernel,
+        stages handed over by tickets) instead of three — each launch boundary cost ~2-3 us
+        between one launch's last workgroup and the next one's first (scripts/mb/
+        graph_life.py, profiles/r6_notes.md).  MEASURED SLOWER, so opt-in (``CSA_FWD_CHAIN=1``):
+        a stage hand-off inside the launch — the producer's atomics drained, its ticket RMW,
+        the go flag, the consumer's poll and acquire — took 4.5-5.8 us, against ~2.4 us for
+        the kernel boundary it replaces (0.0889 vs 0.0753 ms/step, profiles/r6_notes.md)."""
+        e = self.e
+        self.chain = False
+        try:
+            chain_ok = self.lib.csa_chain_ok
+        except AttributeError:              # an A/B baseline library (CSA_KERNEL_LIB) without it
+            return
+        dense = [u for u in self.units if u.kind == "dense"]
+        if (e.ctx.enabled or self.det or self.packed or self.forward_only
+                or not getattr(self, "head_dgrad", False) or os.environ.get("CSA_FWD_CHAIN", "0") != "1"
+                or len(dense) != 2 or self.units[-2:] != dense or not all(u.direct for u in dense)
+                or getattr(self, "br_unit", None) is not None
+                or not chain_ok(self.units[-1].layer.spec.hidden)):
+            return
+        # counts and spread go flags, each on its own line
+        self.chain_tk = torch.zeros(int(self.lib.csa_chain_words()), dtype=torch.int32, device=e.device)
+        self.chain_err = torch.zeros(1, dtype=torch.int32, device=e.device)
+        self.chain = True
 
     # ------------------------------------------------------------------ DP deferred update
     def _plan_carry(self) -> None:
@@ -763,8 +791,12 @@ class HipProgram:
 
     def health_words(self):
         """Device int32 words that are nonzero once an in-kernel bounded wait timed out
-        (read without a host sync by the job loop's metric drain)."""
-        return [self.tail_err] if getattr(self, "tail", False) else []
+        (read without a host sync by the job loop's metric drain): the pair-backward tail's
+        and the forward chain's."""
+        words = [self.tail_err] if getattr(self, "tail", False) else []
+        if getattr(self, "chain", False):
+            words.append(self.chain_err)
+        return words
 
     def arm_tail_timeout(self) -> bool:
         """Debug / fault injection: the NEXT pair-backward launch's tail waits
@@ -1259,7 +1291,15 @@ class HipProgram:
             r.zero_()
         if getattr(self, "hfuse", False):
             lib.csa_dense_update_clear()        # no stale segment from an aborted step
-        self._forward(st)
+        chain = getattr(self, "chain", False)
+        if chain:
+            lib.csa_chain_begin()               # the two dense forwards + the head: recorded
+        try:
+            self._forward(st)
+        except BaseException:
+            if chain:
+                lib.csa_chain_reset()
+            raise
 
         self._lowrank_gather_inputs()
 
@@ -1269,7 +1309,7 @@ class HipProgram:
         if getattr(self, "head_dgrad", False):
             staged = getattr(self, "staged", False)
             ltf = last.in_tf
-            self._rc(lib.csa_head_dgrad(
+            rc_hd = (lib.csa_head_dgrad(
                 K.ptr(hin), B, hin.shape[1], _act_id(self.head_tf.act), _alpha(self.head_tf.act),
                 K.ptr(V["head.weight"]), K.ptr(V["head.bias"]),
                 K.ptr(self.stage_lbl if staged else e.data.labels), None if staged else K.ptr(rows),
@@ -1277,7 +1317,13 @@ class HipProgram:
                 K.ptr(last.dy), K.ptr(self.hdl), K.ptr(self.hrl), K.ptr(self.hrc), K.ptr(e.dstep),
                 K.ptr(cur) if staged else None, e.stream.wrap if staged else 0,
                 K.ptr(V[f"{last.layer.name}.weight"]), last.layer.in_shape.numel, K.ptr(last.x.view(B, -1)),
-                _act_id(ltf.act), _alpha(ltf.act), K.ptr(self.units[-2].dy), st), "head_dgrad")
+                _act_id(ltf.act), _alpha(ltf.act), K.ptr(self.units[-2].dy), st))
+            if chain:                           # fc1 forward | fc2 forward | head: one launch
+                rc = lib.csa_chain_end(K.ptr(self.chain_tk), K.ptr(self.chain_err), st) if rc_hd >= 0 else 0
+                if rc_hd < 0:
+                    lib.csa_chain_reset()
+                self._rc(rc, "fwd_chain")
+            self._rc(rc_hd, "head_dgrad")
         elif self.head_row:
             staged = getattr(self, "staged", False)
             self._rc(lib.csa_head_row(

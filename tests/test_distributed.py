@@ -511,3 +511,23 @@ def test_async_ps_checkpoint_saves_owner_shards_and_resumes(tmp_path):
         assert step == 9
         torch.testing.assert_close(rflat, flat, rtol=0, atol=0)
         torch.testing.assert_close(rslots, obj["slots"][:, lo:hi], rtol=0, atol=0)
+
+
+def _pick_hf(rank, world, port, out):
+    from cloud_server_amd.parallel.dist import shutdown
+    from cloud_server_amd.parallel.strategy import pick_strategy
+    ctx = _init(rank, world, port)
+    cfg = parse_train_config(CFG)
+    best, times = pick_strategy(cfg, synthetic_mnist(256, seed=1), ctx, candidates=("allreduce", "allreduce:hf"),
+                                steps=2, backend="torch")
+    out[rank] = (best, times)
+    shutdown(ctx)
+
+
+def test_tuner_skips_hf_trial_without_hf_program():
+    """a ':hf' candidate whose engine did not build the :hf program (here the
+    eager program) is not timed — it would be a duplicate of the plain strategy."""
+    out = _spawn(_pick_hf, 2)
+    for r in range(2):
+        best, times = out[r]
+        assert best == "allreduce" and times["allreduce:hf"] is None and times["allreduce"] > 0

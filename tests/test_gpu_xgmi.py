@@ -560,8 +560,9 @@ def _prod_results(world: int):
     if world not in _PROD_CACHE:
         from cloud_server_amd.data.datasets import synthetic_mnist
         from cloud_server_amd.runtime.engine import TrainEngine
-        out = {"prod": _spawn_prod(world, False, False), "det": _spawn_prod(world, False, True),
-               "prod_sbn": _spawn_prod(world, True, False)}
+        out = {"prod_sbn": _spawn_prod(world, True, False)}
+        if world == 2:      # (per-rank BN vs the deterministic program: world 2 only — runtime)
+            out.update(prod=_spawn_prod(world, False, False), det=_spawn_prod(world, False, True))
         # one process, batch world x 50: the same global sample set every step (rank r of
         # the DP job takes positions r, r+W, .. of the same permutation: data/stream.py)
         eng = TrainEngine(_prod_cfg(50 * world, False), synthetic_mnist(2000, seed=0), device="cuda:0",
@@ -575,20 +576,28 @@ def _prod_results(world: int):
     return _PROD_CACHE[world]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+# world 4 on the box's ONE GPU: the production programs (buckets overlapped with the
+# backward on side streams, spinning peer waits) of 4 processes sharing one device ran
+# 1-2 min per engine phase (GPU time-slicing between the processes' queues;
+# profiles/r6_notes.md) — opt in with CSA_TEST_WORLD4=1.  On a node every rank has its GPU.
+_WORLDS = [2, 4] if os.environ.get("CSA_TEST_WORLD4") == "1" else [2]
+
+
+@pytest.mark.parametrize("world", _WORLDS)
 @pytest.mark.parametrize("strategy", PROD_STRATEGIES)
 def test_production_dp_programs_multi_rank(world, strategy):
     """the production (non-deterministic) data-parallel programs at world 2
-    and 4 on the device, each checked two ways after 12 steps:
-    * sample config (per-rank BatchNorm, the bench's): replicas equal across ranks to fp32
-      reassociation and within rtol=2e-3 / atol=2e-5 of the deterministic allreduce
-      program at the same world (itself bitwise-pinned: test_xgmi_ps_step_bitwise...);
-    * with SyncBN (statistics over the global batch): within the same tolerance of ONE
-      process training at batch world x 50 on the same global batches.
+    and 4 on the device, checked after 12 steps:
+    * with SyncBN (statistics over the global batch): replicas agree and every program is
+      within rtol=2e-3 / atol=2e-5 of ONE process training at batch world x 50 on the same
+      global batches (world 2 and 4);
+    * sample config (per-rank BatchNorm, the bench's; world 2): replicas agree and every
+      program is within the same tolerance of the deterministic allreduce program (itself
+      bitwise-pinned: test_xgmi_ps_step_bitwise...).
     The program features under test must actually be on (carry, :hf, lowrank, overlap)."""
     import numpy as np
     R = _prod_results(world)
-    for kind in ("prod", "prod_sbn"):
+    for kind in [k for k in ("prod", "prod_sbn") if k in R]:
         f = R[kind][0][strategy]["flags"]
         assert f["shared_gpu"], f                                   # (one-GPU box: shared profile)
         if strategy == "allreduce":
@@ -599,15 +608,17 @@ def test_production_dp_programs_multi_rank(world, strategy):
             assert f["lowrank"], f
         for r in range(world):
             assert R[kind][r][strategy]["tail_err"] == 0 and R[kind][r][strategy]["host_step"] == 12
-    got = R["prod"][0][strategy]["state"]
-    for r in range(1, world):
+    for kind in [k for k in ("prod", "prod_sbn") if k in R]:          # replicas agree
+        got = R[kind][0][strategy]["state"]
+        for r in range(1, world):
+            for k, v in got.items():
+                torch.testing.assert_close(torch.from_numpy(R[kind][r][strategy]["state"][k]), torch.from_numpy(v),
+                                           rtol=1e-4, atol=1e-6, msg=lambda m: f"{kind} rank {r} {k}: {m}")
+    if "det" in R:
+        got, ref = R["prod"][0][strategy]["state"], R["det"][0]["allreduce"]["state"]
         for k, v in got.items():
-            torch.testing.assert_close(torch.from_numpy(R["prod"][r][strategy]["state"][k]), torch.from_numpy(v),
-                                       rtol=1e-4, atol=1e-6, msg=lambda m: f"rank {r} {k}: {m}")
-    ref = R["det"][0]["allreduce"]["state"]
-    for k, v in got.items():
-        torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref[k]), rtol=2e-3, atol=2e-5,
-                                   msg=lambda m: f"{strategy} vs det allreduce, {k}: {m}")
+            torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref[k]), rtol=2e-3, atol=2e-5,
+                                       msg=lambda m: f"{strategy} vs det allreduce, {k}: {m}")
     sb = R["prod_sbn"][0][strategy]["state"]
     for k, v in sb.items():
         assert np.isfinite(v).all()
