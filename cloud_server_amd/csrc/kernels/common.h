@@ -13,6 +13,25 @@
 
 #define CSA_API extern "C" __attribute__((visibility("default")))
 
+// Non-temporal stores for the activations one launch writes for the next (A/B knob,
+// CSA_NT_OUT): each code object has its own flag and setter (CSA_NT_SETTER).
+typedef float csa_f2v __attribute__((ext_vector_type(2)));
+typedef float csa_f4v __attribute__((ext_vector_type(4)));
+static __constant__ int g_nt_out = 0;
+#define CSA_NT_SETTER(name)                                                                   \
+  CSA_API int name(int on) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_nt_out), &on, sizeof(on)); }
+__device__ __forceinline__ void out_store(float* p, float v) {
+  if (g_nt_out) __builtin_nontemporal_store(v, p); else *p = v;
+}
+__device__ __forceinline__ void out_store2(float* p, float a, float b) {
+  if (g_nt_out) { csa_f2v w = {a, b}; __builtin_nontemporal_store(w, reinterpret_cast<csa_f2v*>(p)); }
+  else *reinterpret_cast<float2*>(p) = make_float2(a, b);
+}
+__device__ __forceinline__ void out_store4(float* p, float4 v) {
+  if (g_nt_out) { csa_f4v w = {v.x, v.y, v.z, v.w}; __builtin_nontemporal_store(w, reinterpret_cast<csa_f4v*>(p)); }
+  else *reinterpret_cast<float4*>(p) = v;
+}
+
 namespace csa {
 
 enum Act : int { ACT_NONE = 0, ACT_SIGMOID = 1, ACT_RELU = 2, ACT_LEAKY = 3 };

@@ -1507,7 +1507,7 @@ __global__ __launch_bounds__(CPV_T) void cpv_fwd_kernel(CPVFwdArgs a, CPZero z, 
     const int oo = u * g.C2 + c2;
     const long off = g.pool ? (((long)b * g.PH + pr0) * g.PW) * g.C2 + oo
                             : (((long)b * g.H2 + r2a) * g.W2) * g.C2 + oo;
-    *reinterpret_cast<float2*>(a.y + off) = make_float2(best0, best1);
+    out_store2(a.y + off, best0, best1);
     if (g.pool && a.argmax) {
       a.argmax[off] = (uint8_t)am0;
       a.argmax[off + 1] = (uint8_t)am1;
@@ -2025,6 +2025,8 @@ CSA_API int csa_cp_debug(long long* p) {
 CSA_API int csa_cp_du_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_du_dbg), &p, sizeof(p));
 }
+
+CSA_NT_SETTER(csa_nt_out_cp)
 
 CSA_API int csa_cpv_life_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cpv_life), &p, sizeof(p));

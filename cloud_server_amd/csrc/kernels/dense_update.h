@@ -581,7 +581,7 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
         v2[r] = a.bn_on ? g[r] * (x[r] - s_bn[ch]) * s_bn[MAXC_DU + ch] : 0.f;
       }
     }
-    *reinterpret_cast<float4*>(a.dX + (long)em * K + f0 + fq) = make_float4(g[0], g[1], g[2], g[3]);
+    out_store4(a.dX + (long)em * K + f0 + fq, make_float4(g[0], g[1], g[2], g[3]));
   }
   DU_STAMP(5);
   if (a.bn_on && a.bwd_slab) {

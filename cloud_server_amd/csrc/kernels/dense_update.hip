@@ -59,6 +59,8 @@ using namespace csa;
 static thread_local float* g_du_grad_w = nullptr;
 static thread_local float* g_du_grad_b = nullptr;
 
+CSA_NT_SETTER(csa_nt_out_du)
+
 CSA_API int csa_du_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_du_dbg), &p, sizeof(p));
 }

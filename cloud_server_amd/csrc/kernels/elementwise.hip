@@ -43,12 +43,14 @@ __global__ __launch_bounds__(256) void bn_act_apply_kernel(ApplyArgs a) {
     o[u] = act_fwd(o[u] * s_bn[256 + c] + s_bn[384 + c], a.act, a.alpha);
     c = (c + 1 == a.C) ? 0 : c + 1;
   }
-  reinterpret_cast<float4*>(a.y)[i4] = make_float4(o[0], o[1], o[2], o[3]);
+  out_store4(a.y + 4 * i4, make_float4(o[0], o[1], o[2], o[3]));
 }
 
 }  // namespace csa
 
 using namespace csa;
+
+CSA_NT_SETTER(csa_nt_out_ew)
 
 CSA_API int csa_ew_life_debug(long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ew_life), &p, sizeof(p));

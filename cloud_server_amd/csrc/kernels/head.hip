@@ -718,6 +718,8 @@ using namespace csa;
 
 // Rows per workgroup of the partial-output head (0: shape outside its family: more than
 // 16 groups of <= 16 rows, K % 4, or the LDS budget).
+CSA_NT_SETTER(csa_nt_out_head)
+
 CSA_API int csa_head_debug(long long* p) {
   const int rc = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hd_dbg), &p, sizeof(p));
   return rc ? rc : (int)hipMemcpyToSymbol(HIP_SYMBOL(g_head_dbg), &p, sizeof(p));

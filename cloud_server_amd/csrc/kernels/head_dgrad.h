@@ -241,7 +241,7 @@ __device__ __forceinline__ void head_dgrad_body(const HeadDgradArgs& a, const in
       if (a.in_act) g = act_bwd(g, hv[r][u], hx[r][u], a.in_act, a.in_alpha);   // x-based: any alpha
       g = r < nr ? g : 0.f;
       s_dh[r][k] = g;
-      if (fs == 0 && r < nr) a.dh[(long)(m0 + r) * Kh + k] = g;
+      if (fs == 0 && r < nr) out_store(a.dh + (long)(m0 + r) * Kh + k, g);
     }
   }
   __syncthreads();
@@ -269,7 +269,7 @@ __device__ __forceinline__ void head_dgrad_body(const HeadDgradArgs& a, const in
   if (c < nr && f0 + f < K1) {
     float g = mine;
     if (a.act) g = act_bwd(g, xe, act_fwd(xe, a.act, a.alpha), a.act, a.alpha);
-    a.dX[(long)(m0 + c) * K1 + f0 + f] = g;
+    out_store(a.dX + (long)(m0 + c) * K1 + f0 + f, g);
   }
   HD_STAMP(5);
 }

@@ -82,6 +82,10 @@ _SIGS = {
     "csa_cpv_life_debug": (I, [P]),
     "csa_dd_group_begin": (None, []),
     "csa_chain_begin": (None, []),
+    "csa_nt_out_ew": (I, [I]),
+    "csa_nt_out_cp": (I, [I]),
+    "csa_nt_out_head": (I, [I]),
+    "csa_nt_out_du": (I, [I]),
     "csa_chain_reset": (None, []),
     "csa_chain_ok": (I, [I]),
     "csa_chain_words": (I, []),

@@ -47,6 +47,24 @@ from ..ops import optim_ref
 from ..utils.streams import dedicated_stream
 
 
+_NT_SET = [None]
+
+
+def _set_nt_out(lib) -> None:
+    """``CSA_NT_OUT=1``: the activations a launch writes for the next one (pair forward y,
+    bn_act xt, head dh / dX, fc1's dX) go out as non-temporal stores (A/B knob; once per
+    process and value)."""
+    want = int(os.environ.get("CSA_NT_OUT", "0") == "1")
+    if _NT_SET[0] == want:
+        return
+    for name in ("csa_nt_out_ew", "csa_nt_out_cp", "csa_nt_out_head", "csa_nt_out_du"):
+        try:
+            getattr(lib, name)(want)
+        except AttributeError:          # an A/B baseline library without the knob
+            pass
+    _NT_SET[0] = want
+
+
 class Unsupported(Exception):
     pass
 
@@ -123,6 +141,7 @@ class HipProgram:
         self.e = eng
         self.forward_only = forward_only
         self.lib = K.load(required=True)
+        _set_nt_out(self.lib)
         if eng.device.type != "cuda":
             raise Unsupported("HIP program needs a GPU device")
         # CSA_DETERMINISTIC=1: bitwise-reproducible steps on the same kernels (det.hip):
