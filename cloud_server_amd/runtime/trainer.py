@@ -118,17 +118,25 @@ def _tail_timeout_step(model_dir: str) -> int:
     return int(v)
 
 
-def _strip_final_tail(path: str) -> None:
-    """A resumed (extended) job appends its step lines after the previous run's; drop that
-    run's ``final_accuracy`` tail first, so the file stays one run of step lines and then
-    one final line — the reference monitor reads only up to the first non-step line
-    (apps/runtime/views.py:55)."""
+def _strip_final_tail(path: str, resume_step: int) -> None:
+    """A resumed (extended or restarted) job appends its step lines after the previous
+    run's; first drop that run's ``final_accuracy`` tail and every row at or after the step
+    it resumes from (a restart from an older checkpoint re-logs them; the compat row at
+    step == iter, see ``JobRun.finish``), so the file stays one run of increasing step
+    lines and then one final line — the reference monitor reads only up to the first
+    non-step line (apps/runtime/views.py:55)."""
     if not os.path.exists(path):
         return
     with open(path) as f:
         lines = f.readlines()
     keep = 0
     while keep < len(lines) and lines[keep].startswith("step"):
+        try:
+            st = int(lines[keep].split(",")[0].split(":")[1])
+        except (IndexError, ValueError):
+            break
+        if st >= resume_step:
+            break
         keep += 1
     if keep < len(lines):
         tmp = path + ".tmp"
@@ -157,10 +165,11 @@ class _MetricLog:
         self.h_step = eng.host_step
         self.last_acc = float("nan")
         if chief:
-            _strip_final_tail(result_path)
+            _strip_final_tail(result_path, eng.host_step)
         self.fr = open(result_path, "a") if chief else None
         self.fm = open(metrics_path, "a") if chief else None
         self.lines = 0
+        self.last_dt = 0.0
         # one rank: the in-kernel timeout words ride with the metric copies (no host sync)
         # and a nonzero one fails the job when its log line drains; under data parallelism
         # the ranks' agreed check at control points reads them instead
@@ -206,6 +215,7 @@ class _MetricLog:
             else:
                 step_time = (th - self.t_host) / n
             self.prev_ev, self.t_host, self.h_step = ev, th, s1
+            self.last_dt = step_time
             acc = float(pc[step % RING]) / B
             self.last_acc = acc
             k = min(max(s1 - s0, 1), RING)
@@ -397,6 +407,14 @@ class JobRun:
             final_acc = eng.evaluate(self.test) if len(self.test) else self.mlog.last_acc
             if chief:
                 with open(os.path.join(self.model_dir, RESULT), "a") as f:
+                    # the reference's loop (construct_distribute.py:402-414) reads the global
+                    # step BEFORE each train op, so it also logs step == iter (and runs one
+                    # op more): iter/100 + 1 rows, which is what its monitor's final-line gate
+                    # counts on (views.py:66).  This job runs exactly iter steps; its row at
+                    # step == iter repeats the final step's batch accuracy
+                    if eng.host_step == self.cfg.iter and self.cfg.iter % self.log_every == 0:
+                        f.write("step:%d,accuracy:%f,duration:%f\n"
+                                % (eng.host_step, eng.last_batch_accuracy(), self.mlog.last_dt))
                     f.write("final_accuracy:%f\n\n" % final_acc)
         if state != "paused":
             self.ckpter.save(chief)

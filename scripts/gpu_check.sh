@@ -8,7 +8,7 @@ tail -1 gpurun_out/check_smoke.txt
 timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/check_b20.json 2>> gpurun_out/check.err || exit 4
 timeout -k 10 200 python3 bench.py --steps 2000 --warmup 200 > gpurun_out/check_b2000.json 2>> gpurun_out/check.err || exit 5
 echo "bench 20/5 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/check_b20.json); 2000/200 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/check_b2000.json)"
-for s in allreduce allreduce:hf ps ps:hf; do
+for s in allreduce allreduce:hf ps ps:hf async_ps; do
   timeout -k 10 200 python3 scripts/bench_dp1.py --strategy $s > gpurun_out/check_dp_$s.json 2>> gpurun_out/check.err || exit 6
   echo "dp1 $s $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/check_dp_$s.json)"
 done

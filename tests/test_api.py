@@ -205,7 +205,7 @@ def test_full_user_flow(client):
     jid = r.json()["job"]
     assert client.app.state.jobs.wait(jid, 300) == "done"
     res = client.get("/runtime/train/m1/40/", headers=h).json()
-    assert len(res["every_result"]) == 4 and 0.0 <= float(res["final_accuracy"]) <= 1.0
+    assert len(res["every_result"]) == 5 and 0.0 <= float(res["final_accuracy"]) <= 1.0   # 0..40
     assert client.get("/construct/config/", headers=h).json() == ["m1"]
     assert client.get("/construct/detail/m1/", headers=h).json()["iter"] == 40
     assert client.get("/construct/detail/zz/", headers=h).status_code == 404
@@ -316,7 +316,7 @@ def test_url_dataset_and_url_training(client, tmp_path):
     jid = client.post("/construct/construction/mu/url/", json=cfg, headers=h).json()["job"]
     assert client.app.state.jobs.wait(jid, 300) == "done"
     res = client.get("/runtime/train/mu/20/", headers=h).json()
-    assert len(res["every_result"]) == 2 and "final_accuracy" in res
+    assert len(res["every_result"]) == 3 and "final_accuracy" in res      # 0, 10, 20
 
 
 def test_url_fetch_refuses_file_and_private(client, tmp_path):
@@ -485,6 +485,6 @@ def test_construct_twice_is_409_and_result_stays_clean(tmp_path):
         assert r1.status_code == 200 and r2.status_code == 409, (r1.text, r2.text)
         assert c.app.state.jobs.wait(r1.json()["job"], 300) == "done"
         res = c.get("/runtime/train/m/200/", headers=h).json()
-        assert [r["step"] for r in res["every_result"]] == ["0", "50", "100", "150"]
+        assert [r["step"] for r in res["every_result"]] == ["0", "50", "100", "150", "200"]
         assert "final_accuracy" in res
         assert len(c.app.state.db.jobs_for(1, "m")) == 1

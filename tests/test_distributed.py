@@ -200,8 +200,8 @@ def test_distributed_job_rank0_writes_and_ps_resume(tmp_path):
     out = _spawn(_job, 2, mdir, cfg)
     assert out == {0: 12, 1: 12}
     lines = open(os.path.join(mdir, "result.txt")).read().splitlines()
-    assert [l.split(",")[0] for l in lines[:3]] == ["step:0", "step:4", "step:8"]   # one writer
-    assert lines[3].startswith("final_accuracy:")
+    assert [l.split(",")[0] for l in lines[:4]] == ["step:0", "step:4", "step:8", "step:12"]   # one writer
+    assert lines[4].startswith("final_accuracy:")
     from cloud_server_amd.runtime import checkpoint as ckpt
     obj = ckpt.load(ckpt.latest(mdir)[1])
     full = obj["slots"]
@@ -448,8 +448,8 @@ def test_distributed_job_async_ps(tmp_path):
     out = _spawn(_job, 2, mdir, cfg)
     assert out == {0: 12, 1: 12}
     lines = open(os.path.join(mdir, "result.txt")).read().splitlines()
-    assert [l.split(",")[0] for l in lines[:3]] == ["step:0", "step:4", "step:8"]
-    assert lines[3].startswith("final_accuracy:")
+    assert [l.split(",")[0] for l in lines[:4]] == ["step:0", "step:4", "step:8", "step:12"]
+    assert lines[4].startswith("final_accuracy:")
 
 
 def _aps_save(rank, world, port, path, out):

@@ -244,3 +244,26 @@ def test_hf_programs_match_single_gpu(pg, monkeypatch, strategy):
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
     ma, mb = a.metrics_since(0), b.metrics_since(0)
     assert abs(ma["loss"] - mb["loss"]) < 1e-3 * max(1.0, mb["loss"])
+
+
+def test_carry_flush_is_idempotent_mid_run(pg, monkeypatch):
+    """the deferred dense update's pending flag is retired by the carrying
+    workgroups themselves, so host flushes at any point between steps (a checkpoint every
+    few steps, a second flush right after) never apply the update twice."""
+    monkeypatch.setenv("CSA_XGMI", "0")
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy="allreduce")
+    assert a.program.carry is not None, "the allreduce program carries the dense update"
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for i in range(12):
+        a.step(); b.step()
+        if i % 3 == 1:
+            a.flush_params()
+            a.flush_params()                 # a second flush: nothing pending any more
+            torch.cuda.synchronize()
+            assert int(a.program.carry_pending[0].item()) == 0
+            assert int(a.program.carry_pending[1].item()) == 0     # retire ticket reset
+    a.sync_device(); b.sync_device()
+    torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)

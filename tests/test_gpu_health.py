@@ -93,9 +93,11 @@ def test_job_with_tail_timeout_fails_then_restarts_from_checkpoint(tmp_path, mon
         assert ckpt.latest(mdir)[0] == 100
         lines = open(os.path.join(mdir, "result.txt")).read().splitlines()
         steps = [int(ln.split(",")[0].split(":")[1]) for ln in lines if ln.startswith("step")]
-        # the restart resumed from step 40 (the last checkpoint before the timeout at 45)
-        # and logged 40.. again; the run is one sequence of step lines then one final line
-        assert steps[-1] == 90 and 40 in steps
+        # the restart resumed from step 40 (the last checkpoint before the timeout at 45):
+        # the failed run's rows from 40 on were dropped and re-logged once; the run is one
+        # increasing sequence of step lines (0 .. 100: the reference's step == iter row),
+        # then one final line
+        assert steps == list(range(0, 101, 10)), steps
         assert sum(ln.startswith("final_accuracy:") for ln in lines) == 1
     finally:
         jm.shutdown()

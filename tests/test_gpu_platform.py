@@ -44,7 +44,7 @@ def test_gpu_job_hip_backend_and_inference(tmp_path):
     out = run_job(mdir, _cfg(600), device="cuda:0", backend="hip", data=ds.split(0.9))
     assert out["backend"] == "hip" and out["state"] == "done" and out["step"] == 600
     res = read_train_results(os.path.join(mdir, RESULT), 600)
-    assert [r["step"] for r in res["every_result"]] == [str(s) for s in range(0, 600, 100)]
+    assert [r["step"] for r in res["every_result"]] == [str(s) for s in range(0, 601, 100)]
     assert float(res["final_accuracy"]) > 0.9
     obj = ckpt.load(ckpt.latest(mdir)[1])
     assert obj["host_step"] == 600

@@ -80,7 +80,7 @@ def test_gpu_host_runs_concurrent_jobs(tmp_path):
             st = json.load(open(os.path.join(mdir, STATUS)))
             assert st["state"] == "done" and st["step"] == 20 + 10 * i
             res = read_train_results(os.path.join(mdir, RESULT), 20 + 10 * i)
-            assert len(res["every_result"]) == 2 + i and "final_accuracy" in res
+            assert len(res["every_result"]) == 3 + i and "final_accuracy" in res   # + the step == iter row
         # all of them were hosted by ONE process
         pids = {json.load(open(os.path.join(m, STATUS)))["pid"] for m in mdirs}
         assert len(pids) == 1

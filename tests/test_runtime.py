@@ -113,10 +113,12 @@ def test_run_job_result_contract_and_resume(tmp_path):
     out = run_job(mdir, SMALL, device="cpu", backend="torch", data=data)
     assert out["state"] == "done" and out["step"] == 30
     lines = open(os.path.join(mdir, RESULT)).read().splitlines()
-    assert [l.split(",")[0] for l in lines[:3]] == ["step:0", "step:10", "step:20"]
-    assert lines[3].startswith("final_accuracy:") and lines[4] == ""
+    # rows 0, 10, 20 and the reference's row at step == iter (its loop logs it), then the
+    # final line: iter/100 + 1 rows, as the monitor's gate expects (views.py:66)
+    assert [l.split(",")[0] for l in lines[:4]] == ["step:0", "step:10", "step:20", "step:30"]
+    assert lines[4].startswith("final_accuracy:") and lines[5] == ""
     res = read_train_results(os.path.join(mdir, RESULT), 30)
-    assert len(res["every_result"]) == 3 and isinstance(res["final_accuracy"], str)   # views.py:70
+    assert len(res["every_result"]) == 4 and isinstance(res["final_accuracy"], str)   # views.py:70
     assert float(res["final_accuracy"]) == pytest.approx(out["final_accuracy"], abs=1e-6)
     last = ckpt.latest(mdir)
     assert last[0] == 30
@@ -127,7 +129,7 @@ def test_run_job_result_contract_and_resume(tmp_path):
     out2 = run_job(mdir, cfg2, device="cpu", backend="torch", data=data)
     assert out2["step"] == 50
     steps = [r["step"] for r in read_train_results(os.path.join(mdir, RESULT), 50)["every_result"]]
-    assert steps == ["0", "10", "20", "30", "40"]
+    assert steps == ["0", "10", "20", "30", "40", "50"]     # resumed at 30: rows >= 30 re-logged once
 
 
 def test_fault_injection_then_resume(tmp_path, monkeypatch):
@@ -237,7 +239,7 @@ def test_job_manager_executors(tmp_path, executor):
             if os.path.exists(os.path.join(mdir, "worker.log")) else jm.status(jid)
         st = jm.status(jid)
         assert st["progress"]["state"] == "done" and st["progress"]["step"] == 20
-        assert len(read_train_results(os.path.join(mdir, RESULT), 20)["every_result"]) == 2
+        assert len(read_train_results(os.path.join(mdir, RESULT), 20)["every_result"]) == 3   # 0, 10, 20
         # a failing job is marked failed and can be resumed
         bad = jm.submit(uid, "empty", "file", dict(SMALL, iter=5))
         assert jm.wait(bad, 300) == "failed"
@@ -488,7 +490,7 @@ def test_one_job_per_model_conflict_and_supersede(tmp_path):
         assert jm.wait(jid, 300) == "done" and jm.wait(other, 300) in ("done", "failed")
         lines = open(os.path.join(mdir, RESULT)).read().splitlines()
         steps = [int(l.split(",")[0].split(":")[1]) for l in lines if l.startswith("step:")]
-        assert steps == list(range(0, 300, 20))
+        assert steps == list(range(0, 301, 20))          # (+ the reference's step == iter row)
         assert sum(l.startswith("final_accuracy:") for l in lines) == 1
         # paused -> a new construct supersedes it; resume of a paused job marks it resumed
         jid2 = jm.submit(uid, "m", "file", dict(cfg, iter=100000))
