@@ -89,8 +89,8 @@ struct CPOptCarry {
   int blocks;                          // extra workgroups (0: no carry)
   int opt; float lr; const int64_t* step;
   float* w; const float* g; float* s0; float* s1;
-  unsigned* pending;                   // [0] 1: the exchanged gradient awaits its update;
-                                       // [1] retire ticket (the last workgroup clears [0])
+  unsigned* pending;                   // 1: the exchanged gradient awaits its update (cleared
+                                       // by the launch after the carrying forward: bn_act_apply)
   int count; long lo4[CP_MAXCS]; long start4[CP_MAXCS + 1];   // flat spans, float4 units
 };
 
@@ -100,22 +100,16 @@ struct CPOptCarry {
 // argument struct).
 __device__ __forceinline__ void cp_opt_carry_apply(const CPOptCarry& c, int k, int nblk);
 
-// The flag is retired by the carry itself: every workgroup takes a ticket after it read the
-// flag, and the last one clears it — so a host flush after the carrying forward (or a carry
-// after a flush) never applies the update twice, at any point of the step.
+// The flag is cleared right after the carrying forward by the NEXT launch of the step
+// (bn_act_apply's block 0: csa_ew_clear_next), so a host flush anywhere after the carry never
+// applies the update twice.  (A retire ticket taken by every carrying workgroup
+// did the same inside this launch, but ~1 000 same-address atomics made the data-parallel
+// step 0.0852 -> 0.1005 ms — measured round 6, profiles/r6_notes.md.)
 __device__ __forceinline__ void cp_opt_carry(const CPOptCarry& c, int k, int nblk) {
   __shared__ unsigned s_pend;
   if (threadIdx.x == 0) s_pend = __hip_atomic_load(c.pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_pend) cp_opt_carry_apply(c, k, nblk);
-  if (threadIdx.x == 0) {
-    // (relaxed: the flag carries no data; thread 0 read it before the barrier above)
-    unsigned* tk = c.pending + 1;
-    if (__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1) {
-      __hip_atomic_store(c.pending, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 __device__ __forceinline__ void cp_opt_carry_apply(const CPOptCarry& c, int k, int nblk) {

@@ -571,9 +571,9 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     float g[4] = {g4.x, g4.y, g4.z, g4.w};
     const float x[4] = {xf.x, xf.y, xf.z, xf.w};
     if (tf) {
+      int ch = (f0 + fq) % C;                             // one division, then wrap
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ch = (f0 + fq + r) % C;
+      for (int r = 0; r < 4; ++r, ch = (ch + 1 == C) ? 0 : ch + 1) {
         const float z = a.bn_on ? x[r] * s_bn[2 * MAXC_DU + ch] + s_bn[3 * MAXC_DU + ch] : x[r];
         const float y = act_fwd(z, a.act, a.alpha);
         g[r] = act_bwd(g[r], z, y, a.act, a.alpha);

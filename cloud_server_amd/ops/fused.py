@@ -83,6 +83,7 @@ _SIGS = {
     "csa_dd_group_begin": (None, []),
     "csa_chain_begin": (None, []),
     "csa_nt_out_ew": (I, [I]),
+    "csa_ew_clear_next": (None, [P]),
     "csa_nt_out_cp": (I, [I]),
     "csa_nt_out_head": (I, [I]),
     "csa_nt_out_du": (I, [I]),

@@ -47,6 +47,16 @@ from ..ops import optim_ref
 from ..utils.streams import dedicated_stream
 
 
+def _opt_call(lib, name: str, *args):
+    """Call an entry point that an A/B baseline library (CSA_KERNEL_LIB, an older revision)
+    may lack; the in-tree library has them all (ops.fused.load checks)."""
+    try:
+        fn = getattr(lib, name)
+    except AttributeError:
+        return None
+    return fn(*args)
+
+
 _NT_SET = [None]
 
 
@@ -290,8 +300,12 @@ class HipProgram:
         self.carry = segs
         self.carry_offsets = carried
         self.carry_blocks = max(1, min(1024, -(-m4 // 256)))
-        # [flag, retire ticket]: the carrying workgroups clear the flag themselves
-        self.carry_pending = torch.zeros(2, dtype=torch.int32, device=e.device)
+        # the pending flag: set by the optimizer launch, read by the carrying forward, cleared
+        # by the launch right after it (bn_act_apply, when the first dense layer takes the
+        # pair's BatchNorm output; else only by a flush)
+        self.carry_pending = torch.zeros(1, dtype=torch.int32, device=e.device)
+        u2 = self.units[2] if len(self.units) > 2 else None
+        self.carry_clear = bool(u2 is not None and u2.kind == "dense" and u2.xt is not None)
 
     def _carry_args(self):
         e = self.e
@@ -780,7 +794,7 @@ class HipProgram:
         deferred dense segments) and switch the head segment to in-place updates."""
         e, lib = self.e, self.lib
         P = C.c_void_p
-        lib.csa_conv_pair_tail_force(K.ptr(self.tail_force))
+        _opt_call(lib, "csa_conv_pair_tail_force", K.ptr(self.tail_force))
         if not self.tail_update:           # the ":hf" data-parallel fold: nothing else
             self._rc(lib.csa_conv_pair_tail_set(
                 K.ptr(self.tail_tk), K.ptr(self.tail_err), 0, 0.0, K.ptr(e.dstep), K.ptr(self.tail_table),
@@ -1544,7 +1558,8 @@ class HipProgram:
             # (the tail program: the dense split-K outputs of this step, zeroed by the pair
             # forward's threads — not when predicting, which zeroes them itself)
             fz = [] if getattr(self, "_predicting", False) else getattr(self, "fwd_zero", [])
-            if getattr(self, "carry", None) is not None and not getattr(self, "_predicting", False):
+            carrying = getattr(self, "carry", None) is not None and not getattr(self, "_predicting", False)
+            if carrying:
                 self._rc(lib.csa_conv_pair_fwd_carry(*self._carry_args()), "conv_pair_fwd_carry")
             self._rc(lib.csa_conv_pair_fwd(
                 K.ints(self.pair), K.ptr(simg), K.ptr(srows), K.ptr(scur),
@@ -1555,6 +1570,8 @@ class HipProgram:
                 nt.prod_rows if self.det else self.lib.csa_conv_fwd_nslab(None, None),
                 (C.c_void_p * 4)(*[t.data_ptr() for t in fz]), (C.c_long * 4)(*[t.numel() for t in fz]), len(fz),
                 st), "conv_pair_fwd")
+            if carrying and self.carry_clear:
+                _opt_call(lib, "csa_ew_clear_next", K.ptr(self.carry_pending))   # (next: bn_act_apply)
             if oslab is not None and self.det:
                 self._row_fold(oslab, nt.prod_rows, oslab.shape[1] * oslab.shape[2], oslab, 0, st)
             if oslab is not None and self.sync_bn:

@@ -247,9 +247,9 @@ def test_hf_programs_match_single_gpu(pg, monkeypatch, strategy):
 
 
 def test_carry_flush_is_idempotent_mid_run(pg, monkeypatch):
-    """the deferred dense update's pending flag is retired by the carrying
-    workgroups themselves, so host flushes at any point between steps (a checkpoint every
-    few steps, a second flush right after) never apply the update twice."""
+    """the deferred dense update's pending flag is cleared by the launch right
+    after the carrying forward (bn_act_apply), so host flushes between steps (a checkpoint
+    every few steps, a second flush right after) never apply the update twice."""
     monkeypatch.setenv("CSA_XGMI", "0")
     cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdagradOptimizer", learning_rate=1e-3))
     ds = synthetic_mnist(2000, seed=0)
@@ -264,6 +264,5 @@ def test_carry_flush_is_idempotent_mid_run(pg, monkeypatch):
             a.flush_params()                 # a second flush: nothing pending any more
             torch.cuda.synchronize()
             assert int(a.program.carry_pending[0].item()) == 0
-            assert int(a.program.carry_pending[1].item()) == 0     # retire ticket reset
     a.sync_device(); b.sync_device()
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
