@@ -169,7 +169,7 @@ _SIGS = {
     "csa_xgmi_diag_words": (I, []),
     "csa_xgmi_run": (I, [I, I, I, L, P, P, I, P, P, P, P, C.c_double, I, P, P]),
     "csa_xgmi_reduce_scatter": (I, [I, I, L, P, P, P, L, L, L, P, P, C.c_double, I, P, P]),
-    "csa_aps_step": (I, [I, I, I, I, L, I, P, P, P, P, P, I, F, P, P, P, I, C.c_double, P]),
+    "csa_aps_step": (I, [I, I, I, I, L, I, P, P, P, P, P, P, I, F, P, P, I, C.c_double, P]),
 }
 
 

@@ -202,7 +202,9 @@ class AsyncPSDevice:
         self.R = 2 * staleness + 2
         # every workgroup of a step waits on its peers' (bounded): CSA_XGMI_BLOCKS caps them
         # so ranks sharing one GPU keep all their workgroups resident (parallel/xgmi.py)
-        self.nb = max(1, min(256, (shard + 4095) // 4096))
+        # (chunks of >= 4096 floats; up to 512 of them: two workgroups per CU, each thread
+        # with few enough float4 rounds that the chunk is not a chain of load latencies)
+        self.nb = max(1, min(512, (shard + 4095) // 4096))
         cap = max_blocks_from_env()
         if cap:
             self.nb = max(1, min(self.nb, cap))
@@ -249,9 +251,11 @@ class AsyncPSDevice:
                 self.close(barrier=False)
                 raise RuntimeError("async_ps: mapping a peer buffer failed")
         self._bufs = (C.c_void_p * (5 * world))(*ptrs)
-        self.prog = torch.zeros(3 * self.nb, dtype=torch.int32, device=device)
-        self.stale = torch.zeros(1, dtype=torch.int32, device=device)
-        self.state = torch.zeros(4, dtype=torch.int32, device=device)     # t, done, err
+        # per workgroup: next clock, next source, pushes applied, clock t, max staleness
+        self.prog = torch.zeros(5 * self.nb, dtype=torch.int32, device=device)
+        self.state = torch.zeros(4, dtype=torch.int32, device=device)     # -, -, err
+        # my own pushes not applied in their own launch: local (cached) memory, never mapped
+        self.selfbox = torch.zeros(self.R * shard, dtype=torch.float32, device=device)
         self.group = group
 
     def reset(self) -> None:
@@ -264,7 +268,7 @@ class AsyncPSDevice:
         ptrs = [self._local[1], self._local[3], self._local[4]]
         self.lib.csa_zero((C.c_void_p * 3)(*ptrs), (C.c_long * 3)(*[n // 4 for n in nbytes]), 3,
                           torch.cuda.current_stream(self.device).cuda_stream)
-        self.prog.zero_(); self.stale.zero_(); self.state.zero_()
+        self.prog.zero_(); self.state.zero_()
         torch.cuda.synchronize(self.device)
         if dist.is_initialized():
             _line_up(self.group, self.device)
@@ -274,8 +278,9 @@ class AsyncPSDevice:
         s1 = slots[1, :] if slots.shape[0] > 1 else None
         rc = self.lib.csa_aps_step(
             self.r, self.W, self.R, self.s, self.sh, self.nb, self._bufs, flat_grad.data_ptr(), flat.data_ptr(),
-            None if s0 is None else s0.data_ptr(), None if s1 is None else s1.data_ptr(), self.opt_id,
-            float(self.lr), self.prog.data_ptr(), self.stale.data_ptr(), self.state.data_ptr(), drain,
+            None if s0 is None else s0.data_ptr(), None if s1 is None else s1.data_ptr(),
+            self.selfbox.data_ptr(), self.opt_id,
+            float(self.lr), self.prog.data_ptr(), self.state.data_ptr(), drain,
             self.timeout_s, torch.cuda.current_stream(self.device).cuda_stream)
         if rc:
             raise RuntimeError(f"async_ps step launch failed ({rc})")
@@ -297,16 +302,16 @@ class AsyncPSDevice:
 
     @property
     def max_staleness(self) -> int:
-        return int(self.stale.item())
+        return int(self.prog.view(-1, 5)[:, 4].max().item())
 
     @property
     def applied(self) -> int:
         """Pushes applied to EVERY chunk of this owner's shard (the slowest workgroup's count)."""
-        return int(self.prog.view(-1, 3)[:, 2].min().item())
+        return int(self.prog.view(-1, 5)[:, 2].min().item())
 
     @property
     def t(self) -> int:
-        return int(self.state[0].item())
+        return int(self.prog.view(-1, 5)[:, 3].min().item())
 
     def close(self, barrier: bool = True) -> None:
         """Collective: every rank's kernels drain before any buffer is freed."""

@@ -89,7 +89,12 @@ class TrainEngine:
         # (dense weight gradients formed inside the pair backward launch, no bucket overlap);
         # the start-up tuner times it against the overlapped program (parallel/strategy.py)
         strategy, _, variant = strategy.partition(":")
-        self.dp_variant = variant
+        if strategy == "async_ps" and not variant:
+            # async_ps runs the ":hf" program by default (world 1: 0.0997 against 0.1112
+            # ms/step for the bucketed one, profiles/r6_notes.md); "async_ps:flat" (or
+            # CSA_APS_VARIANT=flat) keeps the bucketed program
+            variant = os.environ.get("CSA_APS_VARIANT", "hf")
+        self.dp_variant = "" if variant == "flat" else variant
         if deterministic_mode() and strategy == "lowrank" and ctx is not None and ctx.enabled:
             # same exact DP math; its gathered-operand GEMMs have no fixed-order variant
             strategy = "allreduce"

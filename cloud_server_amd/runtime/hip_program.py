@@ -619,7 +619,7 @@ class HipProgram:
         # segments store dW / db whole into the flat gradient, the pair backward's tail folds
         # the conv stripes into it, then the exchange and the flat optimizer follow
         self.dp_hf = bool(self.fused_grad and getattr(self.e, "dp_variant", "") == "hf"
-                          and self.e.sync.strategy in ("allreduce", "ps"))
+                          and self.e.sync.strategy in ("allreduce", "ps", "async_ps"))
         packed_ok = os.environ.get("CSA_PACKED_HFUSE", "0") == "1"
         if (self.forward_only or not (self.fused or self.dp_hf) or self.det or self.pair is None
                 or (self.packed and not packed_ok) or os.environ.get("CSA_HFUSE", "1") != "1"):

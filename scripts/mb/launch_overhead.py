@@ -1,0 +1,84 @@
+"""Where the fixed cost of a short timed loop goes (bench --steps 20 --warmup 5).
+
+The 20-step bench reads ~2 us/step more than the 2000-step one; at K = 20 that is ~40 us
+of fixed cost per timed region.  This splits one timed region (one 20-step graph replay
+bracketed by ``torch.cuda.synchronize``) into:
+
+* host: the Python + ``hipGraphLaunch`` time of ``run_steps`` itself;
+* gpu:  start -> end events recorded around the replay (what the device spends);
+* wall: the bench's timed region;
+* idle_sync: one synchronize on an idle device.
+
+MB_SPIN=1 sets hipDeviceScheduleSpin on the runtime torch loads, before any context
+exists (the host spins in synchronize instead of sleeping on a completion interrupt).
+Env knobs of the runtime (ROC_ACTIVE_WAIT_TIMEOUT, ...) are passed through by the caller.
+Prints one JSON line.
+"""
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+if os.environ.get("MB_SPIN") == "1":
+    import torch as _t  # noqa: E402  (loads the runtime; no HIP call yet)
+    _hip = ctypes.CDLL(os.path.join(os.path.dirname(_t.__file__), "lib", "libamdhip64.so"))
+    _rc = _hip.hipSetDeviceFlags(ctypes.c_uint(1))   # hipDeviceScheduleSpin
+    assert _rc == 0, f"hipSetDeviceFlags: {_rc}"
+
+import torch  # noqa: E402
+
+from bench import _sample_cfg  # noqa: E402
+from cloud_server_amd.data.datasets import synthetic_mnist  # noqa: E402
+from cloud_server_amd.runtime.engine import TrainEngine  # noqa: E402
+
+
+class _A:
+    optimizer = "AdagradOptimizer"
+    batch = 50
+
+
+def main():
+    k = int(os.environ.get("MB_K", "20"))
+    reps = int(os.environ.get("MB_REPS", "30"))
+    eng = TrainEngine(_sample_cfg(_A), synthetic_mnist(60000, seed=0), device="cuda:0",
+                      backend="hip", use_graph=True)
+    eng.step()
+    eng.extra_group_sizes = [k]
+    eng.prepare_group_graph()
+    eng.run_steps(4)
+    eng.sync_device()
+    res = {"host": [], "gpu": [], "wall": [], "idle_sync": []}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(reps):
+        if eng.stream.used + k >= eng.stream.chunk:
+            eng.sync_device()
+        t = time.perf_counter()
+        eng.sync_device()
+        res["idle_sync"].append(time.perf_counter() - t)
+        t0 = time.perf_counter()
+        e0.record()
+        eng.run_steps(k)
+        t1 = time.perf_counter()
+        e1.record()
+        eng.sync_device()
+        t2 = time.perf_counter()
+        res["host"].append(t1 - t0)
+        res["wall"].append(t2 - t0)
+        res["gpu"].append(e0.elapsed_time(e1) * 1e-3)
+    eng.check_health()
+    out = {k2: round(statistics.median(v) * 1e6, 2) for k2, v in res.items()}
+    out["wall_ms_per_step"] = round(statistics.median(res["wall"]) * 1e3 / k, 5)
+    out["gpu_ms_per_step"] = round(statistics.median(res["gpu"]) * 1e3 / k, 5)
+    out["env"] = {e: os.environ.get(e) for e in ("MB_SPIN", "ROC_ACTIVE_WAIT_TIMEOUT", "DEBUG_CLR_GRAPH_PACKET_CAPTURE")
+                  if os.environ.get(e) is not None}
+    out["k"] = k
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -266,3 +266,31 @@ def test_carry_flush_is_idempotent_mid_run(pg, monkeypatch):
             assert int(a.program.carry_pending[0].item()) == 0
     a.sync_device(); b.sync_device()
     torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
+
+
+@pytest.mark.parametrize("strategy", ["async_ps:flat", "async_ps"])
+@pytest.mark.parametrize("opt", ["AdagradOptimizer", "AdamOptimizer"])
+def test_async_ps_world1_matches_single_gpu(pg, opt, strategy):
+    """async_ps at world 1 (csrc/comm/async_ps.hip): the rank's own push is applied straight
+    from its gradient in the step's launch (it never waits on a peer), no publication is
+    written (no reader) — the parameters must follow the plain single-GPU step."""
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name=opt, learning_rate=1e-3,
+                                  options={"batch_size": 50, "staleness": 2}))
+    ds = synthetic_mnist(2000, seed=0)
+    ctx = _DPContext(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+    a = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
+    assert a.backend == "hip", a.fallback_reason
+    assert type(a.aps).__name__ == "AsyncPSDevice"
+    # ":hf": the one-GPU step's structure in gradient mode (dense weight gradients inside
+    # the pair backward launch, its tail folds the conv stripes), then the push / apply
+    assert a.program.dp_hf == (strategy == "async_ps")   # (the default: the :hf program)
+    b = TrainEngine(cfg, ds, device="cuda:0", backend="hip")
+    for _ in range(12):
+        a.step(); b.step()
+    a.sync_device(); b.sync_device()
+    a.aps.check()
+    assert a.aps.applied == 12 and a.staleness() == 0
+    torch.testing.assert_close(a.flat, b.flat, rtol=2e-3, atol=2e-5)
+    a.finish_async()
+    assert a.aps.applied == 12
+    a.close()

@@ -370,7 +370,7 @@ def test_xgmi_two_shot_bitexact(world):
         assert res[r]["errors"] == 0, res[r]
 
 
-def _worker_aps(rank: int, world: int, port: int, fix_dir: str, q) -> None:
+def _worker_aps(rank: int, world: int, port: int, fix_dir: str, q, strategy: str = "async_ps") -> None:
     """async_ps on the device transport (csrc/comm/async_ps.hip) in ``world`` processes on
     one GPU, training the reference's 99 labelled digit JPEGs."""
     import torch.distributed as dist
@@ -394,9 +394,10 @@ def _worker_aps(rank: int, world: int, port: int, fix_dir: str, q) -> None:
         cfg = parse_train_config(dict(SAMPLE_CONFIG, optimizer_name="AdamOptimizer", learning_rate=1e-3,
                                       options={"batch_size": 20, "staleness": 2}))
         ctx = DistContext(rank=rank, world=world, local_rank=0, backend="nccl", device=dev)
-        eng = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy="async_ps")
+        eng = TrainEngine(cfg, ds, device="cuda:0", ctx=ctx, backend="hip", strategy=strategy)
         assert eng.backend == "hip", eng.fallback_reason
         assert eng.aps is not None and type(eng.aps).__name__ == "AsyncPSDevice"
+        assert eng.program.dp_hf == (strategy == "async_ps")   # (the default: the :hf program)
         for i in range(240):
             eng.step()
             if i == 19:
@@ -416,8 +417,9 @@ def _worker_aps(rank: int, world: int, port: int, fix_dir: str, q) -> None:
         q.put((rank, {"exception": traceback.format_exc()}))
 
 
+@pytest.mark.parametrize("strategy", ["async_ps:flat", "async_ps"])
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_async_ps_device_converges_with_bounded_staleness(world):
+def test_async_ps_device_converges_with_bounded_staleness(world, strategy):
     """VERDICT r3 missing #1 on the GPU: ranks push gradient shards into the owners' IPC
     inboxes with no step barrier, owners apply each push on arrival, ranks pull parameters
     at most 2s clocks stale — one kernel launch per step inside the HIP graph.  On the 99
@@ -429,7 +431,7 @@ def test_async_ps_device_converges_with_bounded_staleness(world):
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker_aps, args=(r, world, port, fix, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker_aps, args=(r, world, port, fix, q, strategy)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
