@@ -54,6 +54,20 @@ def main():
     eng.sync_device()
     res = {"host": [], "gpu": [], "wall": [], "idle_sync": []}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the same graph replayed back to back (no synchronize in between) for ~MB_B2B_MS ms:
+    # the device time per step when the GPU never idles
+    b2b_ms = float(os.environ.get("MB_B2B_MS", "0"))
+    if b2b_ms > 0:
+        nrep = max(1, int(b2b_ms * 1e-3 / (k * 76e-6)))
+        while nrep * k + eng.stream.used >= eng.stream.chunk and nrep > 1:
+            nrep //= 2
+        eng.sync_device()
+        e0.record()
+        for _ in range(nrep):
+            eng.run_steps(k)
+        e1.record()
+        eng.sync_device()
+        out_b2b = e0.elapsed_time(e1) * 1e-3 / (nrep * k)
     for _ in range(reps):
         if eng.stream.used + k >= eng.stream.chunk:
             eng.sync_device()
@@ -72,6 +86,9 @@ def main():
         res["gpu"].append(e0.elapsed_time(e1) * 1e-3)
     eng.check_health()
     out = {k2: round(statistics.median(v) * 1e6, 2) for k2, v in res.items()}
+    if b2b_ms > 0:
+        out["b2b_ms_per_step"] = round(out_b2b * 1e3, 5)
+        out["b2b_steps"] = nrep * k
     out["wall_ms_per_step"] = round(statistics.median(res["wall"]) * 1e3 / k, 5)
     out["gpu_ms_per_step"] = round(statistics.median(res["gpu"]) * 1e3 / k, 5)
     out["env"] = {e: os.environ.get(e) for e in ("MB_SPIN", "ROC_ACTIVE_WAIT_TIMEOUT", "DEBUG_CLR_GRAPH_PACKET_CAPTURE")
