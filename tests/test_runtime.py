@@ -674,3 +674,20 @@ def test_job_manager_launches_8_gpu_dp_job(tmp_path):
     finally:
         jm._req = real
         jm.shutdown()
+
+
+@pytest.mark.parametrize("strategy,variant", [("async_ps", "hf"), ("async_ps:flat", ""),
+                                              ("allreduce", ""), ("allreduce:hf", "hf")])
+def test_strategy_variant_parse(strategy, variant, monkeypatch):
+    """``async_ps`` runs the ``:hf`` program by default (``async_ps:flat`` / CSA_APS_VARIANT
+    keep the bucketed one); other strategies take the variant as written."""
+    from cloud_server_amd.models.dsl import SAMPLE_CONFIG, parse_train_config
+    from cloud_server_amd.runtime.engine import TrainEngine
+    monkeypatch.delenv("CSA_APS_VARIANT", raising=False)
+    cfg = parse_train_config(dict(SAMPLE_CONFIG, options={"batch_size": 8}))
+    eng = TrainEngine(cfg, synthetic_mnist(64, seed=0), device="cpu", strategy=strategy)
+    assert eng.dp_variant == variant
+    assert eng.sync.strategy == strategy.split(":")[0]
+    monkeypatch.setenv("CSA_APS_VARIANT", "flat")
+    if strategy == "async_ps":
+        assert TrainEngine(cfg, synthetic_mnist(64, seed=0), device="cpu", strategy=strategy).dp_variant == ""
