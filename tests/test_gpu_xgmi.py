@@ -537,7 +537,7 @@ def _spawn_prod(world: int, sync_bn: bool, det: bool) -> dict:
     try:
         for _ in range(world):
             try:
-                r, d = q.get(timeout=300)
+                r, d = q.get(timeout=float(os.environ.get("CSA_TEST_PROD_TIMEOUT", "300" if world <= 2 else "600")))
             except EOFError:
                 break
             res[r] = d
@@ -578,11 +578,10 @@ def _prod_results(world: int):
     return _PROD_CACHE[world]
 
 
-# world 4 on the box's ONE GPU: the production programs (buckets overlapped with the
-# backward on side streams, spinning peer waits) of 4 processes sharing one device ran
-# 1-2 min per engine phase (GPU time-slicing between the processes' queues;
-# profiles/r6_notes.md) — opt in with CSA_TEST_WORLD4=1.  On a node every rank has its GPU.
-_WORLDS = [2, 4] if os.environ.get("CSA_TEST_WORLD4") == "1" else [2]
+# world 4 on the box's ONE GPU: four processes time-slice the device (spinning peer waits
+# included); the four world-4 cases took 158 s in one run (scripts/gpu_r6o.sh,
+# profiles/r6_notes.md).  CSA_TEST_WORLD4=0 skips them.  On a node every rank has its GPU.
+_WORLDS = [2] if os.environ.get("CSA_TEST_WORLD4") == "0" else [2, 4]
 
 
 @pytest.mark.parametrize("world", _WORLDS)
