@@ -612,15 +612,17 @@ class HipProgram:
         layer's deferred segment exactly as they rode in its fused backward."""
         self.hfuse = False
         self.head_dgrad = False
-        # (not in the packed profile: there the other jobs' kernels already fill the CUs the
-        # pair backward leaves idle, and K = 4 / 8 packs measured 1.10 / 1.12 M samples/s with
-        # the deferred updates against 1.17 / 1.23 M without — profiles/r4_multitenant.md)
+        # Packed profile too (round 6): with the round-6 carrier (5 workgroups per CU, the
+        # tail program) K = 4 / 8 packs measured 1.295 / 1.313 M samples/s with the deferred
+        # updates against 1.249 / 1.264 M without (scripts/gpu_r6q.sh, profiles/
+        # r6_multitenant.md; rounds 4-5 measured the opposite with the older carriers).
+        # CSA_PACKED_HFUSE=0 restores the packed profile without it.
         # data parallel ("<strategy>:hf"): the same split in GRADIENT mode — the deferred
         # segments store dW / db whole into the flat gradient, the pair backward's tail folds
         # the conv stripes into it, then the exchange and the flat optimizer follow
         self.dp_hf = bool(self.fused_grad and getattr(self.e, "dp_variant", "") == "hf"
                           and self.e.sync.strategy in ("allreduce", "ps", "async_ps"))
-        packed_ok = os.environ.get("CSA_PACKED_HFUSE", "0") == "1"
+        packed_ok = os.environ.get("CSA_PACKED_HFUSE", "1") == "1"
         if (self.forward_only or not (self.fused or self.dp_hf) or self.det or self.pair is None
                 or (self.packed and not packed_ok) or os.environ.get("CSA_HFUSE", "1") != "1"):
             self.dp_hf = False
