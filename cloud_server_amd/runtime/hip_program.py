@@ -161,7 +161,8 @@ class HipProgram:
         self.det = bool(getattr(eng, "deterministic", False)) and not forward_only
         # packed profile (engines built to run as branches of one multi-job graph): launch
         # shapes with less CU-time per step (conv_pair.hip, dense_update.hip)
-        self.packed = bool(getattr(eng, "packed", False))
+        # (CSA_PACKED_PROFILE=0: packed engines keep the one-job launch shapes — A/B knob)
+        self.packed = bool(getattr(eng, "packed", False)) and os.environ.get("CSA_PACKED_PROFILE", "1") == "1"
         # shared-GPU profile (several ranks of this job on ONE device): no 16-wave
         # workgroups (dense_update.hip du_cs; profiles/r5_notes.md, the world-2 stall)
         self.shared_gpu = bool(getattr(eng, "shared_gpu", False))
