@@ -97,6 +97,11 @@ static __constant__ long long* g_du_dbg = nullptr;   // (per code object)
   } while (0)
 
 __host__ __device__ constexpr int du_nb(int waves) { return 32 * waves; }      // columns per block
+// The input-gradient fold in LDS: [wave][t][q] blocks of DU_FT features x 4 rows, each
+// feature's 4 rows at stride DU_FOLD_FS = 5 (not 4): the item threads' reads (feature
+// quads 16 floats apart, q blocks 64 apart with stride 4) hit 8 banks 4-8 times over;
+// with the odd stride both the writes and the reads are conflict-free (32 or 64 banks)
+constexpr int DU_FOLD_FS = 5, DU_FOLD_BLK = DU_FT * DU_FOLD_FS;
 // Update-only (carried) body, 4 waves: the two 64-column dY halves land in LDS straight from
 // global memory (global_load_lds_dwordx4: no staging registers), each as [M4][64] with the
 // column quads of row r rotated by r (the bank spread the +4 row padding gave the register
@@ -110,7 +115,7 @@ __host__ __device__ inline size_t du_upo_lds_floats(int M) {
   return 2 * m4 * 64 + tail;
 }
 __host__ __device__ inline size_t du_lds_floats(int M, int waves) {
-  const size_t a = (size_t)M * (du_nb(waves) + 4), b = (size_t)waves * 4 * 16 * DU_FT;   // dY | the fold
+  const size_t a = (size_t)M * (du_nb(waves) + 4), b = (size_t)waves * 4 * 4 * DU_FOLD_BLK;   // dY | the fold
   return (a > b ? a : b) + DU_MAXM * DU_FT + 6 * MAXC_DU + 4;
 }
 
@@ -508,14 +513,16 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
     return;
   }
 
-  // ---- fold the waves' partials.  Layout [wave][t][q][i][r]: lane (i, q) of tile t holds
-  // rows 16t + 4q + r of feature i, written as one conflict-free float4
+  // ---- fold the waves' partials.  Layout [wave][t][q][i][r] (feature stride DU_FOLD_FS):
+  // lane (i, q) of tile t holds rows 16t + 4q + r of feature i
   __syncthreads();                                         // every dY read is done
   float* fold = sdy;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     if (16 * t >= M) break;
-    *reinterpret_cast<du_f32x4*>(fold + ((wave * 4 + t) * 4 + q) * 64 + 4 * i) = dacc[t];
+    float* dst = fold + ((wave * 4 + t) * 4 + q) * DU_FOLD_BLK + DU_FOLD_FS * i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dst[r] = dacc[t][r];
   }
   __syncthreads();
   DU_STAMP(4);
@@ -523,11 +530,11 @@ __device__ __forceinline__ void du_body(const DUArgs& a, const int bid, const in
   float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (eitem && em < M) {
     const int t = em >> 4, qq = (em >> 2) & 3, r = em & 3;
-    const float* src = fold + (t * 4 + qq) * 64 + 4 * fq + r;
+    const float* src = fold + (t * 4 + qq) * DU_FOLD_BLK + DU_FOLD_FS * fq + r;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) {
-      const float* p = src + w * 4 * 4 * 64;
-      g4.x += p[0]; g4.y += p[4]; g4.z += p[8]; g4.w += p[12];
+      const float* p = src + w * 4 * 4 * DU_FOLD_BLK;
+      g4.x += p[0]; g4.y += p[DU_FOLD_FS]; g4.z += p[2 * DU_FOLD_FS]; g4.w += p[3 * DU_FOLD_FS];
     }
   }
   if (cs > 1) {
