@@ -1,19 +1,19 @@
 #!/bin/bash
-# round 6: VALU remainder rows of the dense input gradient (M = 50: rows 48-49 off the 4th MFMA tile) —
-# numerics, in-graph phases, 1-GPU A/B vs ab/r6c
+# round 6: two-level fold sum in the 16-wave dense input gradient —
+# numerics, in-graph phases, 1-GPU A/B vs ab/r6d
 set -o pipefail
 mkdir -p gpurun_out
 T="timeout -k 10"
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 $T 900 $PYT tests/test_hip_step.py tests/test_deterministic.py tests/test_gpu_dp_overlap.py tests/test_gpu_sync_bn.py > gpurun_out/t_fold.log 2>&1 || { tail -30 gpurun_out/t_fold.log; exit 3; }
 tail -1 gpurun_out/t_fold.log
-$T 180 python scripts/mb/graph_life.py --reps 1 > gpurun_out/glife_vrem.txt 2>&1 || exit $?
-grep -A1 "fc1 dgrad" gpurun_out/glife_vrem.txt
+$T 180 python scripts/mb/graph_life.py --reps 1 > gpurun_out/glife_twolevel.txt 2>&1 || exit $?
+grep -A1 "fc1 dgrad" gpurun_out/glife_twolevel.txt
 for r in 1 2 3; do
-  for v in r6c new; do
-    if [ $v = r6c ]; then export CSA_KERNEL_LIB=ab/r6c/libcsa_kernels.so; else unset CSA_KERNEL_LIB; fi
+  for v in r6d new; do
+    if [ $v = r6d ]; then export CSA_KERNEL_LIB=ab/r6d/libcsa_kernels.so; else unset CSA_KERNEL_LIB; fi
     $T 120 python bench.py --steps 2000 --warmup 200 > gpurun_out/ab_${v}_2000_$r.json 2>>gpurun_out/ab.err || exit $?
     $T 120 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_${v}_20_$r.json 2>>gpurun_out/ab.err || exit $?
   done
 done
-for v in r6c new; do for n in 2000 20; do echo -n "$v $n: "; for r in 1 2 3; do grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${v}_${n}_$r.json | cut -d' ' -f2 | tr '\n' ' '; done; echo; done; done
+for v in r6d new; do for n in 2000 20; do echo -n "$v $n: "; for r in 1 2 3; do grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${v}_${n}_$r.json | cut -d' ' -f2 | tr '\n' ' '; done; echo; done; done
