@@ -8,10 +8,6 @@ tail -1 gpurun_out/check_smoke.txt
 timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/check_b20.json 2>> gpurun_out/check.err || exit 4
 timeout -k 10 200 python3 bench.py --steps 2000 --warmup 200 > gpurun_out/check_b2000.json 2>> gpurun_out/check.err || exit 5
 echo "bench 20/5 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/check_b20.json); 2000/200 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/check_b2000.json)"
-# the capture-right-after-eager-collectives path with the RCCL watchdog thread ACTIVE
-# (TORCH_NCCL_BLOCKING_WAIT=0: the retirement wait is exercised)
-TORCH_NCCL_BLOCKING_WAIT=0 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dp_overlap.py -x -q -p no:cacheprovider -k capture_right_after --timeout 200 --timeout-method thread > gpurun_out/check_watchdog.log 2>&1 || { tail -20 gpurun_out/check_watchdog.log; exit 7; }
-echo "watchdog-active capture test: $(grep -E 'passed|failed' gpurun_out/check_watchdog.log | tail -1)"
 for s in allreduce allreduce:hf ps ps:hf async_ps async_ps:flat; do
   timeout -k 10 200 python3 scripts/bench_dp1.py --strategy $s > gpurun_out/check_dp_$s.json 2>> gpurun_out/check.err || exit 6
   echo "dp1 $s $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/check_dp_$s.json)"
