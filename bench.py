@@ -297,6 +297,10 @@ def main() -> int:
                 "xgmi": eng.sync.xgmi_reason,
                 "collective_tuning_us": eng.sync.xgmi_tuning,
                 "strategy_tuning_ms_per_step": tuning,
+                # CSA_DIST_SHARED_GPU=1 (parallel/dist.py): every rank on ONE GPU over a gloo
+                # group — a rehearsal of the N-rank code path, NOT an N-GPU measurement
+                **({"rehearsal": f"{ctx.world} ranks sharing one GPU (CSA_DIST_SHARED_GPU=1): not a multi-GPU number"}
+                   if os.environ.get("CSA_DIST_SHARED_GPU") == "1" and ctx.world > 1 else {}),
             },
             "final_loss": round(m["loss"], 4),
             "final_batch_accuracy": round(m["accuracy"], 4),

@@ -75,7 +75,21 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 300.0) -> Dis
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if device_type == "auto":
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
-    if device_type == "cuda":
+    # CSA_DIST_SHARED_GPU=1: a REHEARSAL of the N-rank GPU path on a box with fewer GPUs —
+    # every rank on cuda:0, a gloo process group (RCCL refuses two ranks on one device),
+    # every collective on the xGMI peer-buffer kernels (CSA_XGMI=1), the blocks of a call
+    # capped so the ranks' kernels stay co-resident (the device tests' set-up)
+    rehearse = device_type == "cuda" and world > 1 and os.environ.get("CSA_DIST_SHARED_GPU") == "1"
+    if rehearse:
+        from .xgmi import shared_gpu_block_cap
+        os.environ["CSA_XGMI"] = "1"
+        os.environ.setdefault("CSA_XGMI_BLOCKS", str(shared_gpu_block_cap(world)))
+        os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
+        local_rank = 0
+        torch.cuda.set_device(0)
+        device = torch.device("cuda", 0)
+        backend = "gloo"
+    elif device_type == "cuda":
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
         backend = "nccl"
@@ -90,12 +104,15 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 300.0) -> Dis
             kw["device_id"] = device
             rccl_env_defaults()
         dist.init_process_group(**kw)
-    return DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
+    # (rehearsal: the GPU code paths of an RCCL job — xGMI collectives, HIP programs — on
+    # the gloo group, as the multi-process device tests run them)
+    label = "nccl" if rehearse else backend
+    return DistContext(rank, world, local_rank, label if world > 1 else "none", device)
 
 
 def barrier(ctx: DistContext) -> None:
     if ctx.enabled:
-        if ctx.backend == "nccl":
+        if ctx.backend == "nccl" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[ctx.local_rank])
         else:
             dist.barrier()
