@@ -126,3 +126,26 @@ def test_bench_world_size_mismatch_fails():
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode != 0
     assert "WORLD_SIZE=2" in out.stderr and not out.stdout.strip()
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_rehearsal_on_one_gpu():
+    """The driver's N-GPU bench path on the GPU box: ``bench.py --gpus 2`` (it starts
+    torch.distributed.run itself) with both ranks on cuda:0 over gloo and the xGMI
+    collectives (CSA_DIST_SHARED_GPU=1): strategy tuner, HIP programs, timed loop, one JSON
+    line marked as a rehearsal."""
+    env = dict(os.environ, CSA_DIST_SHARED_GPU="1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+                          "--warmup", "2"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    c = d["config"]
+    assert d["n_gpus"] == 2 and c["global_batch"] == 100 and c["backend"] == "hip"
+    assert "rehearsal" in c and c["parallelism"].startswith("dp2")
+    assert c["collectives"] and all(v == "xgmi" for v in c["collectives"].values()), c["collectives"]
+    assert {"allreduce", "allreduce:hf", "ps", "ps:hf"} <= set(c["strategy_tuning_ms_per_step"])
