@@ -615,7 +615,7 @@ class HipProgram:
         self.head_dgrad = False
         # Packed profile too (round 6): with the round-6 carrier (5 workgroups per CU, the
         # tail program) K = 4 / 8 packs measured 1.295 / 1.313 M samples/s with the deferred
-        # updates against 1.249 / 1.264 M without (scripts/gpu_r6q.sh, profiles/
+        # updates against 1.249 / 1.264 M without (scripts/archive/gpu_r6q.sh, profiles/
         # r6_multitenant.md; rounds 4-5 measured the opposite with the older carriers).
         # CSA_PACKED_HFUSE=0 restores the packed profile without it.
         # data parallel ("<strategy>:hf"): the same split in GRADIENT mode — the deferred

@@ -579,7 +579,7 @@ def _prod_results(world: int):
 
 
 # world 4 on the box's ONE GPU: four processes time-slice the device (spinning peer waits
-# included); the four world-4 cases took 158 s in one run (scripts/gpu_r6o.sh,
+# included); the four world-4 cases took 158 s in one run (scripts/archive/gpu_r6o.sh,
 # profiles/r6_notes.md).  CSA_TEST_WORLD4=0 skips them.  On a node every rank has its GPU.
 _WORLDS = [2] if os.environ.get("CSA_TEST_WORLD4") == "0" else [2, 4]
 
