@@ -93,8 +93,10 @@ static int du_cs(int K, int N) {
   // not to be placed for as long as another process's kernel spun in a peer wait (the
   // round-5 world-2 stall: profiles/r5_notes.md); 256-thread blocks always were
   // CSA_DU_WIDE=0: 128-column blocks everywhere (an A/B knob for the one-GPU programs)
-  static const bool narrow_env = [] { const char* e = getenv("CSA_DU_WIDE"); return e && e[0] == '0'; }();
-  const int minb = (g_csa_packed || g_csa_shared || narrow_env) ? (1 << 30) : 128;
+  // CSA_DU_WIDE=1: the wide blocks in the packed profile too (A/B knob)
+  static const int wide_env = [] { const char* e = getenv("CSA_DU_WIDE"); return e ? (e[0] == '0' ? 0 : 1) : -1; }();
+  const bool narrow = wide_env == 0 || g_csa_shared || (g_csa_packed && wide_env != 1);
+  const int minb = narrow ? (1 << 30) : 128;
   if (N <= 512 && groups >= minb) return 1;
   return (N + 127) / 128;
 }
