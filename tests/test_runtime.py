@@ -691,3 +691,30 @@ def test_strategy_variant_parse(strategy, variant, monkeypatch):
     monkeypatch.setenv("CSA_APS_VARIANT", "flat")
     if strategy == "async_ps":
         assert TrainEngine(cfg, synthetic_mnist(64, seed=0), device="cpu", strategy=strategy).dp_variant == ""
+
+
+def test_strip_final_tail_keeps_one_increasing_run(tmp_path):
+    """A resumed job's result.txt: the previous run's rows at or after the resume step and
+    its final line are dropped before the new rows are appended (trainer._strip_final_tail),
+    so the reference monitor still reads one increasing run of step lines."""
+    from cloud_server_amd.runtime.trainer import _strip_final_tail
+    p = tmp_path / "result.txt"
+    rows = [f"step:{s},accuracy:0.5,duration:0.1\n" for s in range(0, 60, 10)]
+    p.write_text("".join(rows) + "final_accuracy:0.9\n")
+    _strip_final_tail(str(p), 40)
+    assert p.read_text() == "".join(rows[:4])
+    _strip_final_tail(str(p), 100)                     # nothing at/after 100, no final line
+    assert p.read_text() == "".join(rows[:4])
+    _strip_final_tail(str(tmp_path / "missing.txt"), 0)   # (no file: no-op)
+
+
+def test_tail_timeout_knob_fires_once_per_model_dir(tmp_path, monkeypatch):
+    """CSA_TAIL_TIMEOUT_AT_STEP arms the forced in-kernel timeout once per model dir (a
+    marker file), so the automatic restart from the last checkpoint runs clean."""
+    from cloud_server_amd.runtime.trainer import _tail_timeout_step
+    monkeypatch.delenv("CSA_TAIL_TIMEOUT_AT_STEP", raising=False)
+    assert _tail_timeout_step(str(tmp_path)) == -1
+    monkeypatch.setenv("CSA_TAIL_TIMEOUT_AT_STEP", "45")
+    assert _tail_timeout_step(str(tmp_path)) == 45
+    assert os.path.exists(tmp_path / ".tail_timeout_fired")
+    assert _tail_timeout_step(str(tmp_path)) == -1     # the restarted run is not re-armed
