@@ -84,8 +84,29 @@ def main():
         res["host"].append(t1 - t0)
         res["wall"].append(t2 - t0)
         res["gpu"].append(e0.elapsed_time(e1) * 1e-3)
+    # device time of one k-step replay after the GPU idled for ~gap us (host busy-wait
+    # between a synchronize and the replay): is the short loop's premium idle-dependent?
+    gaps = [float(x) for x in os.environ.get("MB_GAPS_US", "").split(",") if x]
+    gap_res = {}
+    for gap in gaps:
+        vals = []
+        for _ in range(max(3, reps // 2)):
+            if eng.stream.used + k >= eng.stream.chunk:
+                eng.sync_device()
+            eng.sync_device()
+            t = time.perf_counter()
+            while (time.perf_counter() - t) * 1e6 < gap:
+                pass
+            e0.record()
+            eng.run_steps(k)
+            e1.record()
+            eng.sync_device()
+            vals.append(e0.elapsed_time(e1) * 1e-3 / k)
+        gap_res[str(int(gap))] = round(statistics.median(vals) * 1e6, 2)
     eng.check_health()
     out = {k2: round(statistics.median(v) * 1e6, 2) for k2, v in res.items()}
+    if gaps:
+        out["us_per_step_after_idle_gap_us"] = gap_res
     if b2b_ms > 0:
         out["b2b_ms_per_step"] = round(out_b2b * 1e3, 5)
         out["b2b_steps"] = nrep * k
