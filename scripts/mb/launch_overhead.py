@@ -48,7 +48,8 @@ def main():
     eng = TrainEngine(_sample_cfg(_A), synthetic_mnist(60000, seed=0), device="cuda:0",
                       backend="hip", use_graph=True)
     eng.step()
-    eng.extra_group_sizes = [k]
+    lead = int(os.environ.get("MB_LEAD", "0"))      # (MB_LEAD=n: an n-step graph, then k - n)
+    eng.extra_group_sizes = [k] if not lead else [k - lead] + ([lead] if lead > 1 else [])
     eng.prepare_group_graph()
     eng.run_steps(4)
     eng.sync_device()
@@ -76,7 +77,11 @@ def main():
         res["idle_sync"].append(time.perf_counter() - t)
         t0 = time.perf_counter()
         e0.record()
-        eng.run_steps(k)
+        if lead:
+            eng.run_steps(lead)             # a short graph first: the device starts sooner
+            eng.run_steps(k - lead)
+        else:
+            eng.run_steps(k)
         t1 = time.perf_counter()
         e1.record()
         eng.sync_device()
@@ -115,6 +120,7 @@ def main():
     out["env"] = {e: os.environ.get(e) for e in ("MB_SPIN", "ROC_ACTIVE_WAIT_TIMEOUT", "DEBUG_CLR_GRAPH_PACKET_CAPTURE")
                   if os.environ.get(e) is not None}
     out["k"] = k
+    out["lead"] = lead
     print(json.dumps(out), flush=True)
 
 
