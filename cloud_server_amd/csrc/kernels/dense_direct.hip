@@ -594,7 +594,11 @@ __global__ __launch_bounds__(DD_THREADS) void dd_wgrad_kernel(DDWgrad a) {
 static int dd_splits(int tiles, int K) {
   if (g_csa_det) return 1;                 // deterministic mode: whole-K outputs, plain stores
   // waves per launch: swept 512 / 1024 / 2048 / 4096 -> graph step 125.4 / 120.3 / 119.5 / 122.5 us
-  constexpr int target = 2048;
+  static const int target = [] {                   // (CSA_DD_TARGET: A/B knob)
+    const char* e = std::getenv("CSA_DD_TARGET");
+    const int v = e ? std::atoi(e) : 2048;
+    return v >= 256 && v <= 16384 ? v : 2048;
+  }();
   int ks = (target / DD_WAVES + tiles - 1) / tiles;
   const int maxks = (K + 8 * DD_WAVES * 2 - 1) / (8 * DD_WAVES * 2);   // >= 16 k per wave
   ks = ks < 1 ? 1 : ks;
