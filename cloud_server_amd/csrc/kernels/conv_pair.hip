@@ -1089,7 +1089,7 @@ constexpr int CPT_MAXSEG = 8;
 // next vmcnt wait includes its own atomic — so each count is spread over CPT_SPREAD words
 // on separate 64-byte lines (workgroup b adds into word b % CPT_SPREAD; waiters sum them).
 constexpr int CPT_SPREAD = 16, CPT_LINE = 16;         // words, words per line
-constexpr int CPT_TK_WORDS = (2 * CPT_SPREAD + 1) * CPT_LINE;
+constexpr int CPT_TK_WORDS = (2 * CPT_SPREAD + 1) * CPT_LINE;   // (the last line: unused)
 static_assert(CPT_SPREAD == 16 && CPT_LINE == 16, "cp_bwd_body spreads the image ticket the same way");
 __host__ __device__ __forceinline__ unsigned* cpt_word(unsigned* tk, int count, int b) {
   return tk + (count * CPT_SPREAD + (b % CPT_SPREAD)) * CPT_LINE;
@@ -1217,22 +1217,13 @@ __device__ __forceinline__ void cp_tail_body(const CPTail& t, int npair, int k) 
     // XCD's L2 under the update workgroups)
     if (cp_tail_wait(t, 1, want, false)) cp_tail_stage(t, k - t.param_blocks);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned ntail = (unsigned)(t.param_blocks + t.stage_blocks);
-    unsigned* fin = t.tk + 2 * CPT_SPREAD * CPT_LINE;
-    // relaxed: this workgroup's ticket polls have returned (its exit depended on them)
-    // before the add issues, and the reset stores depend on its result.  An acq_rel add
-    // would write back this XCD's L2 (the update workgroups' dirty W / slot lines) on the
-    // launch's critical path; the launch's end publishes the parameters anyway.
-    const unsigned prev = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == ntail - 1) {                      // every tail read the tickets: reset them
-      for (int j = 0; j < 2 * CPT_SPREAD; ++j)
-        __hip_atomic_store(t.tk + j * CPT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t.force) __hip_atomic_store(t.force, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  // The tickets are NOT reset here: the next step's pair forward zeroes them (its zero
+  // list, hip_program._plan_tail), after this launch ended.  A closing "last tail resets"
+  // counter made every tail's exit wait for an RMW round trip — on the launch's critical
+  // path, after the last pair.  (A forced timeout is disarmed by the tails that saw it: they
+  // all read the flag at their start, a second before any of them times out.)
+  if (want != (unsigned)npair && threadIdx.x == 0)
+    __hip_atomic_store(t.force, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool ONE, int NSLOT>

@@ -739,6 +739,9 @@ class HipProgram:
                             slot(s1, "head.weight"), slot(s0, "head.bias"), slot(s1, "head.bias"))
         self.tail_tk = torch.zeros(int(self.lib.csa_conv_pair_tail_ticket_words()), dtype=torch.int32,
                                    device=e.device)                           # spread tickets
+        # the tickets are zeroed by the NEXT step's pair forward (no closing reset counter in
+        # the carrier's tail: conv_pair.hip cp_tail_body)
+        self.fwd_zero.append(self.tail_tk)
         self.tail_err = torch.zeros(1, dtype=torch.int32, device=e.device)
         self.tail_force = torch.zeros(1, dtype=torch.int32, device=e.device)   # debug: arm_tail_timeout
         # the parameter workgroups' table (one entry per 256 elements of a parameter)
@@ -775,6 +778,7 @@ class HipProgram:
                 jobs.append((G[f"{lp.name}.bias"].view(-1), u.db_acc, u.wg_stripes, u.db_acc.shape[1]))
         self.tail_tk = torch.zeros(int(self.lib.csa_conv_pair_tail_ticket_words()), dtype=torch.int32,
                                    device=e.device)
+        self.fwd_zero = [self.tail_tk]            # (zeroed by the next step's pair forward)
         self.tail_err = torch.zeros(1, dtype=torch.int32, device=e.device)
         self.tail_force = torch.zeros(1, dtype=torch.int32, device=e.device)   # debug: arm_tail_timeout
         P = C.c_void_p
