@@ -142,7 +142,7 @@ class Unit:
 
 
 class HipProgram:
-    WGRAD_STRIPES = 16
+    WGRAD_STRIPES = int(os.environ.get("CSA_WGRAD_STRIPES", "16"))   # (A/B knob; <= 16: the tail's loads)
 
     def __init__(self, eng, forward_only: bool = False):
         """``forward_only``: the serving program (``serve.hip_infer``) — the same forward
